@@ -1,0 +1,190 @@
+#!/usr/bin/env python3
+"""Benchmark: SDF+grad point-evals/s, 1M-point cloud x 64-primitive model (M64).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+A step is ONE residual pass of the hot path over the resident cloud: ship the
+64 hull poses (pinned ring -> H2D), the pose kernel, the pass kernel (per point:
+nearest hull d*, k*, ∇d* written to HBM + the cost/wrench partial sums), the
+fixed-order reduce kernel and, for N > 1, the RCCL all-reduce of the 385-double
+accumulator. Weak scaling: every rank owns its own 2^20-point shard (BASELINE
+config 4 is 10M points over 8 GPUs = 1.31M per GPU), seeded per rank.
+
+Rank 0 prints one JSON line (contract in the task description) with:
+  roofline      the pass kernel: algorithmic bytes (24 B point in + 36 B per-point
+                outputs out) per launch / its mean HIP-event time
+  cpu_baseline  the C oracle (brute force over all hulls, the reference's loop)
+                on a bounded sample of the same cloud, on this host's cores
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "point-cloud-signed-distance_amd"))
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP64_VALU_PEAK_TFLOPS = 78.6    # AMD spec, FP64 vector (not in the local guide)
+BYTES_PER_EVAL = 24 + 36        # xyz f64 in; d f64 + k* i32 + grad 3xf64 out
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--points", type=int, default=1 << 20, help="points per GPU")
+    p.add_argument("--precision", type=int, default=64, choices=(64, 32))
+    p.add_argument("--no-cull", action="store_true")
+    p.add_argument("--order", default="raster", choices=("raster", "shuffled"))
+    p.add_argument("--no-per-point", action="store_true", help="reduction-only pass (no per-point outputs)")
+    p.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of the CPU baseline leg")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--seed", type=int, default=1234)
+    return p.parse_args()
+
+
+def cpu_baseline(manip, pts, q_eval, target_s):
+    """Oracle (test infrastructure, the checker/baseline only) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import flash
+    import oracle
+    om = oracle.OracleModel.from_manipulator(manip)
+    poses = flash.hull_poses(manip, q_eval)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    n = 2048
+    t = time.perf_counter()
+    om.skin(poses, pts[:n], threads=threads)
+    dt = time.perf_counter() - t
+    n = int(min(len(pts), max(n, n * target_s / max(dt, 1e-6))))
+    t = time.perf_counter()
+    om.skin(poses, pts[:n], threads=threads)
+    dt = time.perf_counter() - t
+    return {"value": n / dt, "unit": "point-evals/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} points of rank 0's cloud, M64 brute force over all 64 hulls "
+                      f"(reference loop order), {dt:.2f} s wall on {threads} threads"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import flash
+    from flash import Models, synthetic
+    from flash.distributed import allreduce_accum
+
+    m64 = Models.arm_grid()
+    q_true, q_eval = synthetic.perturbed_configuration(m64, args.seed)
+    pts = synthetic.depth_cloud(m64, q_true, args.points, seed=args.seed + 17 * (rank + 1), order=args.order)
+    q_alt = q_eval + 1e-3  # alternate between two configurations step to step
+    poses = [flash.hull_poses(m64, q_eval), flash.hull_poses(m64, q_alt)]
+
+    ctx = m64.engine(device=local, precision=args.precision, cull=not args.no_cull)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+    d_pts = torch.as_tensor(pts, device=dev)
+    ctx.set_points_device(d_pts.data_ptr(), len(pts))
+    del d_pts
+    n = len(pts)
+    accum = torch.zeros(1 + 6 * ctx.K, dtype=torch.float64, device=dev)
+    if args.no_per_point:
+        outs = (0, 0, 0)
+    else:
+        kstar = torch.empty(n, dtype=torch.int32, device=dev)
+        dd = torch.empty(n, dtype=torch.float64, device=dev)
+        gg = torch.empty((n, 3), dtype=torch.float64, device=dev)
+        outs = (kstar.data_ptr(), dd.data_ptr(), gg.data_ptr())
+
+    def step(i):
+        ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs)
+        allreduce_accum(accum)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    ctx.profile_pass(True)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(args.steps):
+        step(i)
+    ev1.record(stream)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    pass_ms, launches = ctx.pass_time()
+    ctx.profile_pass(False)
+    elapsed = max(wall, ev0.elapsed_time(ev1) / 1e3)
+    t = torch.tensor([elapsed, pass_ms / max(launches, 1)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, pass_avg_ms = float(t[0]), float(t[1])
+
+    # sanity: the last pass is finite and non-trivial
+    acc = accum.cpu().numpy()
+    assert np.isfinite(acc).all() and acc[0] > 0
+
+    if rank == 0:
+        total_evals = n * world * args.steps
+        value = total_evals / elapsed
+        bytes_per_launch = BYTES_PER_EVAL * n if not args.no_per_point else 24 * n
+        achieved = bytes_per_launch / (pass_avg_ms / 1e3) / 1e9
+        out = {
+            "metric": "SDF+grad point-evals/sec, 1M-pt cloud x 64-prim model (M64)",
+            "value": value,
+            "unit": "point-evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64" if args.precision == 64 else "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": "M64: 8 IRB140 arms (7 link hulls + ATI hull each) on a 2x4 grid, 64 convex hulls, "
+                            "48 DOF; seeded synthetic depth cloud per GPU (SURVEY.md §8d generator G)",
+                "points_per_gpu": n, "global_points": n * world, "hulls": ctx.K, "dof": m64.mechanism.num_positions,
+                "order": args.order, "cull": not args.no_cull, "per_point_outputs": not args.no_per_point,
+                "parallelism": f"points sharded x{world}, RCCL all-reduce of {1 + 6 * ctx.K} f64 per pass",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "kernel": "pass_kernel", "kernel_ms": pass_avg_ms,
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "note": "VALU-bound (exact polytope SDF, ~100 fp64 plane tests per candidate hull); "
+                        "the HBM fraction is structurally small (DESIGN.md §5)",
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(m64, pts, q_eval, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

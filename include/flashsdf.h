@@ -1,0 +1,144 @@
+/*
+ * flashsdf.h — C-ABI of the MI355X-native signed-distance residual pass.
+ *
+ * This is the drop-in boundary for the hot path of Flash.jl
+ * (JuliaTagBot/point-cloud-signed-distance). In the reference the path is pure
+ * Julia; no FFI exists. The entry points below are exactly what a Julia
+ * `ccall` shim under src/tracking.jl would bind:
+ *
+ *   reference                                     replaced by
+ *   ---------------------------------------------------------------------------
+ *   Flash.skin(state)          src/Flash.jl:265-268   fsdf_eval / fsdf_skin
+ *     (min over surfaces, one closure per point)      (all points in one launch)
+ *   skin(state, ::ConvexGeometry) src/Flash.jl:245-250 fsdf_set_model + poses
+ *     + ConvexSurface functor  src/Flash.jl:233-243    (exact polytope SDF)
+ *   GradientDescent.cost       src/gradientdescent.jl:28-39
+ *     c = Σ_p skin(p)^2                               accum[0]
+ *     ∂c/∂x via ForwardDiff (Dual{9} chunk passes)    accum[1..6K] wrenches,
+ *                                                     chained to ∂c/∂q on host
+ *   CostFunctor(manip, pts)    src/gradientdescent.jl:41-57
+ *     sensed_points held by reference             fsdf_set_points (once/frame)
+ *   EnhancedGJK.NeighborMesh / conv(vertices)   src/models.jl:152
+ *                                                     fsdf_convex_hull
+ *
+ * Conventions
+ *   - All host buffers are caller-owned. Nothing is retained past a call
+ *     except what set_model / set_points copy to the device.
+ *   - Points are AoS xyz float64, exactly Julia's Vector{SVector{3,Float64}}.
+ *   - A pose is 12 float64: R (3x3, row-major) then t (3); x_world = R x_local + t.
+ *   - Every function returns 0 (FSDF_OK) or a nonzero status; the message of the
+ *     last failure on a context is fsdf_last_error(ctx).
+ *   - Accumulator layout (length 1 + 6K, K = number of hulls):
+ *       accum[0]            = Σ_p d*(p)^2                     (cost, no regularizer)
+ *       accum[1+6k+0..2]    = Σ_{p: k*(p)=k} 2 d*(p) ∇d*(p)   (force-like, world)
+ *       accum[1+6k+3..5]    = Σ_{p: k*(p)=k} 2 d*(p) p × ∇d*(p) (moment about origin)
+ *     so that for a world twist (ω, v) of hull k:  δc = -(ω·M_k + v·F_k).
+ *   - Nearest-primitive index k*(p) is the FIRST k attaining the minimum,
+ *     matching Julia's left-fold `minimum` (src/Flash.jl:267).
+ *   - The library never falls back to a CPU path: without a usable gfx950
+ *     device every compute call fails with FSDF_ERR_HIP.
+ */
+#ifndef FLASHSDF_H
+#define FLASHSDF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FSDF_OK 0
+#define FSDF_ERR_ARG 1        /* bad argument (null pointer, size, index)      */
+#define FSDF_ERR_HIP 2        /* HIP runtime failure / no device                */
+#define FSDF_ERR_STATE 3      /* call order violated (no model / no points)     */
+#define FSDF_ERR_NOMEM 4      /* allocation failure                             */
+#define FSDF_ERR_DEGENERATE 5 /* geometry degenerate (coplanar hull input, ...) */
+
+#define FSDF_PRECISION_F64 64
+#define FSDF_PRECISION_F32 32
+
+typedef struct fsdf_ctx fsdf_ctx;
+
+typedef struct fsdf_opts {
+  int32_t device;      /* HIP device ordinal (process-local)                      */
+  int32_t precision;   /* FSDF_PRECISION_F64 (default) or FSDF_PRECISION_F32       */
+  int32_t sort_points; /* 1: reorder the resident cloud spatially at set_points
+                          (outputs are still returned in caller order)            */
+  int32_t cull;        /* 1 (default): exact-safe bounding-sphere culling;
+                          0: brute force over every hull (reference loop order)    */
+} fsdf_opts;
+
+/* One convex primitive in its body (local) frame.
+ * Replaces ConvexGeometry(NeighborMesh(mesh), frame) (src/models.jl:152,159). */
+typedef struct fsdf_hull {
+  int32_t n_vertices;
+  int32_t n_faces;
+  const double* vertices; /* [n_vertices][3]                                     */
+  const int32_t* faces;   /* [n_faces][3], counter-clockwise seen from outside    */
+  const double* planes;   /* [n_faces][4] = (n, d), |n| = 1, n·x <= d inside      */
+} fsdf_hull;
+
+/* ---- geometry ingest (host only, no device needed) --------------------------
+ * Convex hull of a point set (the shape GJK's support function sees,
+ * EnhancedGJK.NeighborMesh over the mesh vertices, src/models.jl:152).
+ * Capacities: vertices_out >= 3n doubles, faces_out >= 3(2n-4) ints,
+ * planes_out >= 4(2n-4) doubles. Output faces are triangles, outward, CCW. */
+int fsdf_convex_hull(const double* points, int32_t n, int32_t* n_vertices_out,
+                     double* vertices_out, int32_t* n_faces_out, int32_t* faces_out,
+                     double* planes_out);
+
+/* ---- context ---------------------------------------------------------------- */
+int fsdf_create(fsdf_ctx** out, const fsdf_opts* opts);
+int fsdf_destroy(fsdf_ctx* ctx);
+const char* fsdf_last_error(const fsdf_ctx* ctx);
+/* Launch on a caller-owned hipStream_t (NULL = the context's own stream). */
+int fsdf_set_stream(fsdf_ctx* ctx, void* hip_stream);
+int fsdf_num_hulls(const fsdf_ctx* ctx, int32_t* k_out);
+int fsdf_accum_len(const fsdf_ctx* ctx, int32_t* len_out); /* 1 + 6K */
+
+/* Upload the model once (per model). Replaces the per-evaluation
+ * CollisionCache construction of src/Flash.jl:246. */
+int fsdf_set_model(fsdf_ctx* ctx, const fsdf_hull* hulls, int32_t n_hulls);
+
+/* Upload the sensed cloud once per frame (src/gradientdescent.jl:43 holds it
+ * by reference across every cost evaluation). */
+int fsdf_set_points(fsdf_ctx* ctx, const double* xyz, int64_t n);
+/* Same, from a device-resident AoS buffer (copied device-to-device). */
+int fsdf_set_points_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n);
+int fsdf_num_points(const fsdf_ctx* ctx, int64_t* n_out);
+
+/* One residual pass over the resident cloud (synchronous, host buffers).
+ * poses: [K][12] host. Outputs may be NULL when not wanted:
+ *   cost_out   1 double         accum_out  1+6K doubles
+ *   kstar_out  n int32          d_out      n doubles      grad_out [n][3] doubles */
+int fsdf_eval(fsdf_ctx* ctx, const double* poses, double* cost_out, double* accum_out,
+              int32_t* kstar_out, double* d_out, double* grad_out);
+
+/* Same pass, asynchronous on the context stream, outputs in DEVICE memory
+ * (used by the multi-GPU path: the caller all-reduces d_accum over RCCL).
+ * d_accum: 1+6K doubles (required); per-point outputs may be NULL. */
+int fsdf_eval_device(fsdf_ctx* ctx, const double* poses, double* d_accum,
+                     int32_t* d_kstar, double* d_d, double* d_grad);
+
+/* Scene signed distance at arbitrary query points (the closure returned by
+ * Flash.skin(state), src/Flash.jl:265-268), not touching the resident cloud.
+ * xyz: [n][3] host; outputs host, any may be NULL. Synchronous. */
+int fsdf_skin(fsdf_ctx* ctx, const double* poses, const double* xyz, int64_t n,
+              double* d_out, int32_t* kstar_out, double* grad_out);
+
+/* Block until all work queued on the context stream has finished. */
+int fsdf_synchronize(fsdf_ctx* ctx);
+
+/* ---- measurement ------------------------------------------------------------
+ * With profiling enabled, every residual pass brackets the pass kernel (the
+ * dominant launch) with a pair of HIP events on the context stream.
+ * fsdf_pass_time synchronizes, returns the summed kernel time of the passes
+ * recorded since the last query and their count, and resets the record. */
+int fsdf_profile_pass(fsdf_ctx* ctx, int32_t enable);
+int fsdf_pass_time(fsdf_ctx* ctx, double* total_ms_out, int64_t* launches_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FLASHSDF_H */

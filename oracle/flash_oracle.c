@@ -1,0 +1,242 @@
+/*
+ * flash_oracle.c — CPU restatement of the Flash.jl residual pass.
+ *
+ * TEST INFRASTRUCTURE ONLY. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / the timed
+ * CPU baseline — never as the product path.
+ *
+ * What it restates (reference file:line):
+ *   skin(state)(x) = minimum(s(x) for s in all_surfaces)      src/Flash.jl:265-268
+ *       first surface wins ties (Julia left-fold `minimum`)    -> oracle_skin
+ *   s(x) for ConvexGeometry = gjk!(cache, pose, Translation(x)).signed_distance
+ *                                                              src/Flash.jl:233-250
+ *       restated as the exact signed distance to conv(V):      -> oracle_hull_sdf
+ *         inside:  max_f (n_f·x − d_f);  outside: distance to the closest
+ *         boundary point (EnhancedGJK @404de6a9 is un-vendored: outside it
+ *         converges to this value; inside it returns a termination-simplex
+ *         estimate, replaced here by the exact value — DESIGN.md §2).
+ *   pose of a surface = transform_to_root(state, frame)       src/Flash.jl:248
+ *       given as R|t per hull; world planes/vertices          -> oracle_pose_model
+ *   cost = Σ_p skin(p)^2                                      src/gradientdescent.jl:32
+ *       plus the per-hull wrench sums that carry ∂cost/∂pose   -> oracle_cost_accum
+ *
+ * Arithmetic is written operation-for-operation like the gfx950 kernel
+ * (point-cloud-signed-distance_amd/csrc/sdf_kernels.hip): explicit fma(),
+ * -ffp-contract=off, correctly rounded sqrt and division, so per-hull values
+ * and the argmin k* agree bit for bit. Parity of the SDF values themselves
+ * against the Julia reference is UNPINNED for convex hulls (no reference test
+ * touches ConvexGeometry); they are pinned by closed forms and
+ * an independent numpy formulation in tests/.
+ *
+ * Build: oracle/Makefile (gcc -O2 -mfma -ffp-contract=off -fopenmp).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define FX 24 /* stride of the per-face extra record, as in the kernel */
+
+static inline void xf_point(const double* P, const double* v, double* o) {
+  o[0] = fma(P[0], v[0], fma(P[1], v[1], fma(P[2], v[2], P[9])));
+  o[1] = fma(P[3], v[0], fma(P[4], v[1], fma(P[5], v[2], P[10])));
+  o[2] = fma(P[6], v[0], fma(P[7], v[1], fma(P[8], v[2], P[11])));
+}
+static inline void rot_vec(const double* P, const double* v, double* o) {
+  o[0] = fma(P[0], v[0], fma(P[1], v[1], P[2] * v[2]));
+  o[1] = fma(P[3], v[0], fma(P[4], v[1], P[5] * v[2]));
+  o[2] = fma(P[6], v[0], fma(P[7], v[1], P[8] * v[2]));
+}
+static inline void cross3(const double* a, const double* b, double* o) {
+  o[0] = fma(a[1], b[2], -(a[2] * b[1]));
+  o[1] = fma(a[2], b[0], -(a[0] * b[2]));
+  o[2] = fma(a[0], b[1], -(a[1] * b[0]));
+}
+static inline double dot3(const double* a, const double* b) { return fma(a[0], b[0], fma(a[1], b[1], a[2] * b[2])); }
+
+/* World-frame planes and per-face records for every hull (src/Flash.jl:248:
+ * the surface pose is transform_to_root of the geometry frame). */
+void oracle_pose_model(int32_t F, const double* verts_l, const int32_t* faces, const double* planes_l,
+                       const int32_t* face_hull, const double* poses, double* planes_w, double* facex_w) {
+  for (int f = 0; f < F; ++f) {
+    const double* P = poses + 12 * face_hull[f];
+    const double* pl = planes_l + 4 * f;
+    double nw[3];
+    rot_vec(P, pl, nw);
+    const double dw = fma(nw[0], P[9], fma(nw[1], P[10], fma(nw[2], P[11], pl[3])));
+    double a[3], b[3], c[3];
+    xf_point(P, verts_l + 3 * faces[3 * f + 0], a);
+    xf_point(P, verts_l + 3 * faces[3 * f + 1], b);
+    xf_point(P, verts_l + 3 * faces[3 * f + 2], c);
+    const double e0[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+    const double e1[3] = {c[0] - b[0], c[1] - b[1], c[2] - b[2]};
+    const double e2[3] = {a[0] - c[0], a[1] - c[1], a[2] - c[2]};
+    double m0[3], m1[3], m2[3];
+    cross3(nw, e0, m0);
+    cross3(nw, e1, m1);
+    cross3(nw, e2, m2);
+    double* pw = planes_w + 4 * f;
+    pw[0] = nw[0]; pw[1] = nw[1]; pw[2] = nw[2]; pw[3] = dw;
+    double* fx = facex_w + FX * f;
+    fx[0] = m0[0]; fx[1] = m0[1]; fx[2] = m0[2]; fx[3] = dot3(m0, a);
+    fx[4] = m1[0]; fx[5] = m1[1]; fx[6] = m1[2]; fx[7] = dot3(m1, b);
+    fx[8] = m2[0]; fx[9] = m2[1]; fx[10] = m2[2]; fx[11] = dot3(m2, c);
+    fx[12] = a[0]; fx[13] = a[1]; fx[14] = a[2];
+    fx[15] = b[0]; fx[16] = b[1]; fx[17] = b[2];
+    fx[18] = c[0]; fx[19] = c[1]; fx[20] = c[2];
+    fx[21] = 0; fx[22] = 0; fx[23] = 0;
+  }
+}
+
+/* Closest point on triangle v = (a, b, c) to p, Voronoi-region walk. */
+static void closest_on_triangle(const double* p, const double* v, double* q) {
+  const double ax = v[0], ay = v[1], az = v[2];
+  const double bx = v[3], by = v[4], bz = v[5];
+  const double cx = v[6], cy = v[7], cz = v[8];
+  const double abx = bx - ax, aby = by - ay, abz = bz - az;
+  const double acx = cx - ax, acy = cy - ay, acz = cz - az;
+  const double apx = p[0] - ax, apy = p[1] - ay, apz = p[2] - az;
+  const double d1 = fma(abx, apx, fma(aby, apy, abz * apz));
+  const double d2 = fma(acx, apx, fma(acy, apy, acz * apz));
+  if (d1 <= 0 && d2 <= 0) { q[0] = ax; q[1] = ay; q[2] = az; return; }
+  const double bpx = p[0] - bx, bpy = p[1] - by, bpz = p[2] - bz;
+  const double d3 = fma(abx, bpx, fma(aby, bpy, abz * bpz));
+  const double d4 = fma(acx, bpx, fma(acy, bpy, acz * bpz));
+  if (d3 >= 0 && d4 <= d3) { q[0] = bx; q[1] = by; q[2] = bz; return; }
+  const double vc = fma(d1, d4, -(d3 * d2));
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) {
+    const double t = d1 / (d1 - d3);
+    q[0] = fma(t, abx, ax); q[1] = fma(t, aby, ay); q[2] = fma(t, abz, az);
+    return;
+  }
+  const double cpx = p[0] - cx, cpy = p[1] - cy, cpz = p[2] - cz;
+  const double d5 = fma(abx, cpx, fma(aby, cpy, abz * cpz));
+  const double d6 = fma(acx, cpx, fma(acy, cpy, acz * cpz));
+  if (d6 >= 0 && d5 <= d6) { q[0] = cx; q[1] = cy; q[2] = cz; return; }
+  const double vb = fma(d5, d2, -(d1 * d6));
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) {
+    const double t = d2 / (d2 - d6);
+    q[0] = fma(t, acx, ax); q[1] = fma(t, acy, ay); q[2] = fma(t, acz, az);
+    return;
+  }
+  const double va = fma(d3, d6, -(d5 * d4));
+  const double e43 = d4 - d3, e56 = d5 - d6;
+  if (va <= 0 && e43 >= 0 && e56 >= 0) {
+    const double t = e43 / (e43 + e56);
+    q[0] = fma(t, cx - bx, bx); q[1] = fma(t, cy - by, by); q[2] = fma(t, cz - bz, bz);
+    return;
+  }
+  const double inv = 1.0 / (va + vb + vc);
+  const double vv = vb * inv, ww = vc * inv;
+  q[0] = fma(ww, acx, fma(vv, abx, ax));
+  q[1] = fma(ww, acy, fma(vv, aby, ay));
+  q[2] = fma(ww, acz, fma(vv, abz, az));
+}
+
+/* Signed distance of p to one posed hull (faces [f0, f1)), with its unit
+ * gradient. Restates ConvexSurface(x) (src/Flash.jl:238-243). */
+void oracle_hull_sdf(const double* p, int32_t f0, int32_t f1, const double* planes_w, const double* facex_w,
+                     double* d, double* g) {
+  double hmax = -INFINITY;
+  int fs = f0;
+  for (int f = f0; f < f1; ++f) {
+    const double* pl = planes_w + 4 * f;
+    const double h = fma(pl[0], p[0], fma(pl[1], p[1], fma(pl[2], p[2], -pl[3])));
+    if (h > hmax) { hmax = h; fs = f; }
+  }
+  const double* pls = planes_w + 4 * fs;
+  *d = hmax;
+  g[0] = pls[0]; g[1] = pls[1]; g[2] = pls[2];
+  if (!(hmax > 0)) return;
+  const double* fx = facex_w + FX * fs;
+  const double s0 = fma(fx[0], p[0], fma(fx[1], p[1], fma(fx[2], p[2], -fx[3])));
+  const double s1 = fma(fx[4], p[0], fma(fx[5], p[1], fma(fx[6], p[2], -fx[7])));
+  const double s2 = fma(fx[8], p[0], fma(fx[9], p[1], fma(fx[10], p[2], -fx[11])));
+  if (s0 >= 0 && s1 >= 0 && s2 >= 0) return;
+  double best2 = INFINITY, qb[3] = {0, 0, 0};
+  for (int f = f0; f < f1; ++f) {
+    const double* pl = planes_w + 4 * f;
+    const double h = fma(pl[0], p[0], fma(pl[1], p[1], fma(pl[2], p[2], -pl[3])));
+    if (h > 0) {
+      double q[3];
+      closest_on_triangle(p, facex_w + FX * f + 12, q);
+      const double dx = p[0] - q[0], dy = p[1] - q[1], dz = p[2] - q[2];
+      const double dist2 = fma(dx, dx, fma(dy, dy, dz * dz));
+      if (dist2 < best2) { best2 = dist2; qb[0] = q[0]; qb[1] = q[1]; qb[2] = q[2]; }
+    }
+  }
+  *d = sqrt(best2);
+  const double inv = 1.0 / *d;
+  g[0] = (p[0] - qb[0]) * inv;
+  g[1] = (p[1] - qb[1]) * inv;
+  g[2] = (p[2] - qb[2]) * inv;
+}
+
+/* Scene SDF: brute-force minimum over ALL surfaces in index order, strict <,
+ * i.e. exactly the reference's `minimum(s(x) for s in all_surfaces)`. */
+static void skin_one(const double* p, int32_t K, const int32_t* face_off, const double* planes_w,
+                     const double* facex_w, double* d, int32_t* k, double* g) {
+  double best = INFINITY, gb[3] = {0, 0, 0};
+  int32_t bk = 0;
+  for (int32_t kk = 0; kk < K; ++kk) {
+    double dk, gk[3];
+    oracle_hull_sdf(p, face_off[kk], face_off[kk + 1], planes_w, facex_w, &dk, gk);
+    if (dk < best) { best = dk; bk = kk; gb[0] = gk[0]; gb[1] = gk[1]; gb[2] = gk[2]; }
+  }
+  *d = best;
+  *k = bk;
+  g[0] = gb[0]; g[1] = gb[1]; g[2] = gb[2];
+}
+
+/* Per-point skin over a cloud. Any output may be NULL. threads <= 0: all. */
+void oracle_skin(const double* pts, int64_t n, int32_t K, const int32_t* face_off, const double* planes_w,
+                 const double* facex_w, double* d_out, int32_t* k_out, double* g_out, int32_t threads) {
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 256)
+#endif
+  for (int64_t i = 0; i < n; ++i) {
+    double d, g[3];
+    int32_t k;
+    skin_one(pts + 3 * i, K, face_off, planes_w, facex_w, &d, &k, g);
+    if (d_out) d_out[i] = d;
+    if (k_out) k_out[i] = k;
+    if (g_out) { g_out[3 * i] = g[0]; g_out[3 * i + 1] = g[1]; g_out[3 * i + 2] = g[2]; }
+  }
+  (void)threads;
+}
+
+/* cost = Σ d*² and the per-hull wrench sums (layout of include/flashsdf.h):
+ * accum[0] = Σ d², accum[1+6k..] = Σ 2d∇d, Σ 2d (p×∇d) over points with k*=k.
+ * Serial in point order (the reference's `sum` is pairwise; both agree to
+ * rounding, compared at 1e-6 relative). */
+void oracle_cost_accum(const double* pts, int64_t n, int32_t K, const int32_t* face_off, const double* planes_w,
+                       const double* facex_w, double* accum) {
+  memset(accum, 0, sizeof(double) * (size_t)(1 + 6 * K));
+  for (int64_t i = 0; i < n; ++i) {
+    const double* p = pts + 3 * i;
+    double d, g[3];
+    int32_t k;
+    skin_one(p, K, face_off, planes_w, facex_w, &d, &k, g);
+    accum[0] = fma(d, d, accum[0]);
+    const double w = 2.0 * d;
+    double* a = accum + 1 + 6 * k;
+    a[0] += w * g[0];
+    a[1] += w * g[1];
+    a[2] += w * g[2];
+    a[3] += w * fma(p[1], g[2], -(p[2] * g[1]));
+    a[4] += w * fma(p[2], g[0], -(p[0] * g[2]));
+    a[5] += w * fma(p[0], g[1], -(p[1] * g[0]));
+  }
+}
+
+/* Threads the oracle would use (for the bench's cpu_baseline "cores"). */
+int32_t oracle_max_threads(void) {
+#ifdef _OPENMP
+  return (int32_t)omp_get_max_threads();
+#else
+  return 1;
+#endif
+}

@@ -1,0 +1,152 @@
+"""Python face of the CPU oracle (liboracle.so) — TEST INFRASTRUCTURE ONLY.
+
+Loaded only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg,
+as the checker / timed CPU baseline; never by the product package `flash`.
+
+Contents
+  * OracleModel.from_manipulator: the concatenated local model (same layout the
+    C-ABI builds in fsdf_set_model), from a flash.Manipulator's convex surfaces.
+  * pose / skin / cost_accum: ctypes calls into flash_oracle.c (the bit-exact
+    restatement of src/Flash.jl:233-268 + src/gradientdescent.jl:28-39).
+  * numpy_hull_sdf: an INDEPENDENT formulation of the polytope SDF (vertex /
+    edge / face-interior candidates, no shared code or operation order), used to
+    pin the C restatement at 1e-12.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_int32, c_int64, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+FX = 24
+
+_lib = None
+
+
+def build():
+    import subprocess
+    subprocess.run(["make", "-C", HERE], check=True, stdout=subprocess.DEVNULL)
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        lib = ctypes.CDLL(LIB)
+        lib.oracle_pose_model.argtypes = [c_int32] + [c_void_p] * 7
+        lib.oracle_hull_sdf.argtypes = [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]
+        lib.oracle_skin.argtypes = [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_int32]
+        lib.oracle_cost_accum.argtypes = [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]
+        lib.oracle_max_threads.restype = c_int32
+        _lib = lib
+    return _lib
+
+
+def _p(a):
+    return None if a is None else c_void_p(a.ctypes.data)
+
+
+class OracleModel:
+    def __init__(self, hulls):
+        """hulls: list of (vertices, faces, planes) in local frames."""
+        V, Fc, P, FH, off = [], [], [], [], [0]
+        vbase = 0
+        for k, (v, f, p) in enumerate(hulls):
+            V.append(np.asarray(v, np.float64))
+            Fc.append(np.asarray(f, np.int32) + vbase)
+            P.append(np.asarray(p, np.float64))
+            FH.append(np.full(len(f), k, np.int32))
+            off.append(off[-1] + len(f))
+            vbase += len(v)
+        self.K = len(hulls)
+        self.verts_l = np.ascontiguousarray(np.concatenate(V))
+        self.faces = np.ascontiguousarray(np.concatenate(Fc))
+        self.planes_l = np.ascontiguousarray(np.concatenate(P))
+        self.face_hull = np.ascontiguousarray(np.concatenate(FH))
+        self.face_off = np.asarray(off, np.int32)
+        self.F = len(self.face_hull)
+        self.hulls = hulls
+
+    @staticmethod
+    def from_manipulator(manip):
+        return OracleModel([(s.hull.vertices, s.hull.faces, s.hull.planes) for s in manip.convex_surfaces()])
+
+    def pose(self, poses):
+        poses = np.ascontiguousarray(poses, np.float64).reshape(self.K, 12)
+        pw = np.empty((self.F, 4))
+        fx = np.empty((self.F, FX))
+        load().oracle_pose_model(self.F, _p(self.verts_l), _p(self.faces), _p(self.planes_l), _p(self.face_hull),
+                                 _p(poses), _p(pw), _p(fx))
+        return pw, fx
+
+    def skin(self, poses, pts, threads: int = 0):
+        pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
+        pw, fx = self.pose(poses)
+        n = len(pts)
+        d = np.empty(n)
+        k = np.empty(n, np.int32)
+        g = np.empty((n, 3))
+        load().oracle_skin(_p(pts), n, self.K, _p(self.face_off), _p(pw), _p(fx), _p(d), _p(k), _p(g), threads)
+        return d, k, g
+
+    def cost_accum(self, poses, pts):
+        pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
+        pw, fx = self.pose(poses)
+        acc = np.empty(1 + 6 * self.K)
+        load().oracle_cost_accum(_p(pts), len(pts), self.K, _p(self.face_off), _p(pw), _p(fx), _p(acc))
+        return acc
+
+    def world_hull(self, poses, k):
+        """(world vertices, faces, world planes) of hull k, plain numpy."""
+        P = np.asarray(poses, np.float64).reshape(self.K, 12)[k]
+        R, t = P[:9].reshape(3, 3), P[9:]
+        v, f, p = self.hulls[k]
+        n = p[:, :3] @ R.T
+        return v @ R.T + t, f, np.concatenate([n, (p[:, 3] + n @ t)[:, None]], axis=1)
+
+
+def max_threads() -> int:
+    return int(load().oracle_max_threads())
+
+
+# ---------------------------------------------------------------------------
+# Independent numpy formulation (no shared code with flash_oracle.c)
+# ---------------------------------------------------------------------------
+def _seg_dist2(p, a, b):
+    ab = b - a
+    t = np.clip(((p[:, None, :] - a[None]) * ab[None]).sum(-1) / (ab * ab).sum(-1)[None], 0.0, 1.0)
+    q = a[None] + t[..., None] * ab[None]
+    return ((p[:, None, :] - q) ** 2).sum(-1)
+
+
+def numpy_hull_sdf(verts, faces, planes, pts):
+    """Signed distance to conv(verts): inside max plane value; outside the min
+    over {vertices, edges, face interiors whose projection falls inside}."""
+    pts = np.asarray(pts, np.float64).reshape(-1, 3)
+    h = pts @ planes[:, :3].T - planes[:, 3][None]
+    hmax = h.max(1)
+    out = hmax > 0
+    d = hmax.copy()
+    if out.any():
+        p = pts[out]
+        best = ((p[:, None, :] - verts[None]) ** 2).sum(-1).min(1)
+        edges = np.concatenate([faces[:, [0, 1]], faces[:, [1, 2]], faces[:, [2, 0]]])
+        edges = np.unique(np.sort(edges, 1), axis=0)
+        best = np.minimum(best, _seg_dist2(p, verts[edges[:, 0]], verts[edges[:, 1]]).min(1))
+        a, b, c = verts[faces[:, 0]], verts[faces[:, 1]], verts[faces[:, 2]]
+        n = planes[:, :3]
+        hp = h[out]
+        proj = p[:, None, :] - hp[..., None] * n[None]
+        def side(u, v):
+            return (np.cross(v - u, proj - u[None]) * n[None]).sum(-1) >= -1e-15
+        inside_face = side(a, b) & side(b, c) & side(c, a) & (hp > 0)
+        face_d2 = np.where(inside_face, hp ** 2, np.inf).min(1)
+        best = np.minimum(best, face_d2)
+        d[out] = np.sqrt(best)
+    return d

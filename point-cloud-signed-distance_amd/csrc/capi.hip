@@ -1,0 +1,533 @@
+// capi.hip — the C-ABI of include/flashsdf.h: context, resident model and
+// cloud, and the three-launch residual pass (pose -> pass -> reduce).
+//
+// Ownership mirrors the reference: the cloud is held for a whole frame
+// (CostFunctor keeps sensed_points by reference, src/gradientdescent.jl:41-47)
+// and every evaluation only ships the K poses (what set_configuration! +
+// transform_to_root produce in src/Flash.jl:248). No CPU fallback exists: a
+// context cannot be created without a HIP device.
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "flashsdf.h"
+#include "fsdf_internal.h"
+
+namespace {
+
+constexpr int kPoseRing = 8;
+
+template <typename P>
+hipError_t dalloc(P** p, size_t bytes) {
+  *p = nullptr;
+  if (bytes == 0) return hipSuccess;
+  return hipMalloc((void**)p, bytes);
+}
+template <typename P>
+void dfree(P*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+}  // namespace
+
+struct fsdf_ctx {
+  int device = 0;
+  int precision = 64;
+  int sort_points = 0;
+  int cull = 1;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  // local model
+  fsdf::LocalModel lm;
+  double* d_verts_l = nullptr;
+  int32_t* d_faces = nullptr;
+  double* d_planes_l = nullptr;
+  int32_t* d_face_hull = nullptr;
+  double* d_sphere_l = nullptr;
+  int32_t* d_face_off = nullptr;
+  // posed model
+  fsdf::PosedModel pm;
+  // poses: pinned ring + device copy
+  double* h_poses[kPoseRing] = {};
+  hipEvent_t pose_ev[kPoseRing] = {};
+  int pose_slot = 0;
+  double* d_poses = nullptr;
+  // resident cloud (precision-typed AoS)
+  int64_t n = 0;
+  void* d_pts = nullptr;
+  int64_t pts_cap = 0;
+  int64_t* d_perm = nullptr;
+  // work
+  double* d_partials = nullptr;
+  size_t partials_cap = 0;
+  double* d_accum = nullptr;
+  int32_t* d_kstar = nullptr;
+  double* d_d = nullptr;
+  double* d_grad = nullptr;
+  int64_t out_cap = 0;
+  // query scratch (fsdf_skin)
+  void* d_q = nullptr;
+  int64_t q_cap = 0;
+  double* d_q64 = nullptr;
+  int64_t q64_cap = 0;
+  // pass-kernel timing (fsdf_profile_pass)
+  bool profiling = false;
+  std::vector<hipEvent_t> prof_ev;  // pairs
+  size_t prof_used = 0;             // events recorded (2 per pass)
+};
+
+static int fail(fsdf_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return code;
+}
+
+#define HIPCHECK(ctx, expr)                                                                             \
+  do {                                                                                                  \
+    hipError_t e_ = (expr);                                                                             \
+    if (e_ != hipSuccess) return fail((ctx), FSDF_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+static void free_model(fsdf_ctx* c) {
+  dfree(c->d_verts_l);
+  dfree(c->d_faces);
+  dfree(c->d_planes_l);
+  dfree(c->d_face_hull);
+  dfree(c->d_sphere_l);
+  dfree(c->d_face_off);
+  dfree(c->pm.planes_w);
+  dfree(c->pm.facex_w);
+  dfree(c->pm.spheres_w);
+  dfree(c->d_poses);
+  dfree(c->d_accum);
+  c->lm = fsdf::LocalModel();
+}
+
+extern "C" int fsdf_create(fsdf_ctx** out, const fsdf_opts* opts) {
+  if (!out) return FSDF_ERR_ARG;
+  *out = nullptr;
+  fsdf_ctx* c = new (std::nothrow) fsdf_ctx();
+  if (!c) return FSDF_ERR_NOMEM;
+  if (opts) {
+    c->device = opts->device;
+    c->precision = opts->precision ? opts->precision : 64;
+    c->sort_points = opts->sort_points;
+    c->cull = opts->cull;
+  }
+  if (c->precision != 64 && c->precision != 32) {
+    delete c;
+    return FSDF_ERR_ARG;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || c->device < 0 || c->device >= ndev) {
+    delete c;
+    return FSDF_ERR_HIP;
+  }
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return FSDF_ERR_HIP;
+  }
+  c->stream = c->own_stream;
+  for (int i = 0; i < kPoseRing; ++i) c->pose_ev[i] = nullptr;
+  *out = c;
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_destroy(fsdf_ctx* c) {
+  if (!c) return FSDF_ERR_ARG;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  free_model(c);
+  dfree(c->d_pts);
+  dfree(c->d_perm);
+  dfree(c->d_partials);
+  dfree(c->d_kstar);
+  dfree(c->d_d);
+  dfree(c->d_grad);
+  dfree(c->d_q);
+  dfree(c->d_q64);
+  for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
+  for (int i = 0; i < kPoseRing; ++i) {
+    if (c->pose_ev[i]) (void)hipEventDestroy(c->pose_ev[i]);
+    if (c->h_poses[i]) (void)hipHostFree(c->h_poses[i]);
+  }
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+  return FSDF_OK;
+}
+
+extern "C" const char* fsdf_last_error(const fsdf_ctx* c) {
+  if (!c) return "null context";
+  return c->err.c_str();
+}
+
+extern "C" int fsdf_set_stream(fsdf_ctx* c, void* s) {
+  if (!c) return FSDF_ERR_ARG;
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_num_hulls(const fsdf_ctx* c, int32_t* k) {
+  if (!c || !k) return FSDF_ERR_ARG;
+  *k = c->lm.K;
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_accum_len(const fsdf_ctx* c, int32_t* len) {
+  if (!c || !len) return FSDF_ERR_ARG;
+  *len = 1 + 6 * c->lm.K;
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_num_points(const fsdf_ctx* c, int64_t* n) {
+  if (!c || !n) return FSDF_ERR_ARG;
+  *n = c->n;
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_set_model(fsdf_ctx* c, const fsdf_hull* hulls, int32_t K) {
+  if (!c) return FSDF_ERR_ARG;
+  if (!hulls || K < 1) return fail(c, FSDF_ERR_ARG, "set_model: need at least one hull");
+  if (K > fsdf::kMaxHulls) return fail(c, FSDF_ERR_ARG, "set_model: %d hulls exceeds the limit %d", K, fsdf::kMaxHulls);
+  std::vector<double> verts, planes, sph;
+  std::vector<int32_t> faces, face_hull, face_off;
+  face_off.push_back(0);
+  for (int k = 0; k < K; ++k) {
+    const fsdf_hull& h = hulls[k];
+    if (h.n_vertices < 4 || h.n_faces < 4 || !h.vertices || !h.faces)
+      return fail(c, FSDF_ERR_ARG, "set_model: hull %d has %d vertices / %d faces", k, h.n_vertices, h.n_faces);
+    const int vbase = (int)(verts.size() / 3);
+    double cen[3] = {0, 0, 0};
+    for (int i = 0; i < h.n_vertices; ++i)
+      for (int j = 0; j < 3; ++j) {
+        const double v = h.vertices[3 * i + j];
+        if (!std::isfinite(v)) return fail(c, FSDF_ERR_ARG, "set_model: hull %d vertex %d not finite", k, i);
+        verts.push_back(v);
+        cen[j] += v;
+      }
+    for (int j = 0; j < 3; ++j) cen[j] /= h.n_vertices;
+    double r2 = 0;
+    for (int i = 0; i < h.n_vertices; ++i) {
+      double s = 0;
+      for (int j = 0; j < 3; ++j) {
+        const double e = h.vertices[3 * i + j] - cen[j];
+        s += e * e;
+      }
+      r2 = std::max(r2, s);
+    }
+    // radius padded and rounded up to float: the culling bound stays exact-safe
+    float rf = (float)(sqrt(r2) * (1.0 + 1e-9) + 1e-12);
+    rf = nextafterf(rf, INFINITY);
+    sph.push_back(cen[0]);
+    sph.push_back(cen[1]);
+    sph.push_back(cen[2]);
+    sph.push_back((double)rf);
+    for (int f = 0; f < h.n_faces; ++f) {
+      for (int j = 0; j < 3; ++j) {
+        const int vi = h.faces[3 * f + j];
+        if (vi < 0 || vi >= h.n_vertices)
+          return fail(c, FSDF_ERR_ARG, "set_model: hull %d face %d vertex index %d out of range", k, f, vi);
+        faces.push_back(vbase + vi);
+      }
+      double pl[4];
+      if (h.planes) {
+        for (int j = 0; j < 4; ++j) pl[j] = h.planes[4 * f + j];
+      } else {
+        const double* a = h.vertices + 3 * h.faces[3 * f];
+        const double* b = h.vertices + 3 * h.faces[3 * f + 1];
+        const double* cc = h.vertices + 3 * h.faces[3 * f + 2];
+        const double ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+        const double ac[3] = {cc[0] - a[0], cc[1] - a[1], cc[2] - a[2]};
+        double nn[3] = {ab[1] * ac[2] - ab[2] * ac[1], ab[2] * ac[0] - ab[0] * ac[2], ab[0] * ac[1] - ab[1] * ac[0]};
+        const double l = sqrt(nn[0] * nn[0] + nn[1] * nn[1] + nn[2] * nn[2]);
+        if (!(l > 0)) return fail(c, FSDF_ERR_DEGENERATE, "set_model: hull %d face %d degenerate", k, f);
+        for (int j = 0; j < 3; ++j) pl[j] = nn[j] / l;
+        pl[3] = pl[0] * a[0] + pl[1] * a[1] + pl[2] * a[2];
+      }
+      for (int j = 0; j < 4; ++j) planes.push_back(pl[j]);
+      face_hull.push_back(k);
+    }
+    face_off.push_back((int32_t)(face_hull.size()));
+  }
+  HIPCHECK(c, hipSetDevice(c->device));
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  free_model(c);
+  const int F = (int)face_hull.size(), V = (int)(verts.size() / 3);
+  const size_t tsz = c->precision == 64 ? sizeof(double) : sizeof(float);
+  HIPCHECK(c, dalloc(&c->d_verts_l, verts.size() * sizeof(double)));
+  HIPCHECK(c, dalloc(&c->d_faces, faces.size() * sizeof(int32_t)));
+  HIPCHECK(c, dalloc(&c->d_planes_l, planes.size() * sizeof(double)));
+  HIPCHECK(c, dalloc(&c->d_face_hull, face_hull.size() * sizeof(int32_t)));
+  HIPCHECK(c, dalloc(&c->d_sphere_l, sph.size() * sizeof(double)));
+  HIPCHECK(c, dalloc(&c->d_face_off, face_off.size() * sizeof(int32_t)));
+  HIPCHECK(c, dalloc((char**)&c->pm.planes_w, (size_t)F * 4 * tsz));
+  HIPCHECK(c, dalloc((char**)&c->pm.facex_w, (size_t)F * fsdf::kFaceX * tsz));
+  HIPCHECK(c, dalloc(&c->pm.spheres_w, (size_t)K * 4 * sizeof(float)));
+  HIPCHECK(c, dalloc(&c->d_poses, (size_t)K * 12 * sizeof(double)));
+  HIPCHECK(c, dalloc(&c->d_accum, (size_t)(1 + 6 * K) * sizeof(double)));
+  HIPCHECK(c, hipMemcpy(c->d_verts_l, verts.data(), verts.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHECK(c, hipMemcpy(c->d_faces, faces.data(), faces.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHECK(c, hipMemcpy(c->d_planes_l, planes.data(), planes.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHECK(c, hipMemcpy(c->d_face_hull, face_hull.data(), face_hull.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHECK(c, hipMemcpy(c->d_sphere_l, sph.data(), sph.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHECK(c, hipMemcpy(c->d_face_off, face_off.data(), face_off.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  for (int i = 0; i < kPoseRing; ++i) {
+    if (c->h_poses[i]) (void)hipHostFree(c->h_poses[i]);
+    c->h_poses[i] = nullptr;
+    HIPCHECK(c, hipHostMalloc((void**)&c->h_poses[i], (size_t)K * 12 * sizeof(double), hipHostMallocDefault));
+    if (!c->pose_ev[i]) HIPCHECK(c, hipEventCreateWithFlags(&c->pose_ev[i], hipEventDisableTiming));
+  }
+  c->lm.K = K;
+  c->lm.F = F;
+  c->lm.V = V;
+  c->lm.verts_l = c->d_verts_l;
+  c->lm.faces = c->d_faces;
+  c->lm.planes_l = c->d_planes_l;
+  c->lm.face_hull = c->d_face_hull;
+  c->lm.sphere_l = c->d_sphere_l;
+  c->lm.face_off = c->d_face_off;
+  return FSDF_OK;
+}
+
+// Convert/copy AoS f64 points already on the device into a resident buffer of
+// the context precision, growing it when needed.
+static int adopt_points_device(fsdf_ctx* c, const double* d_src, int64_t n, void** d_dst, int64_t* cap) {
+  const size_t tsz = c->precision == 64 ? sizeof(double) : sizeof(float);
+  if (*cap < n || !*d_dst) {
+    dfree(*d_dst);
+    *cap = 0;
+    HIPCHECK(c, hipMalloc(d_dst, (size_t)std::max<int64_t>(n, 1) * 3 * tsz));
+    *cap = std::max<int64_t>(n, 1);
+  }
+  if (n == 0) return FSDF_OK;
+  if (c->precision == 64) {
+    HIPCHECK(c, hipMemcpyAsync(*d_dst, d_src, (size_t)n * 3 * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+  } else {
+    HIPCHECK(c, fsdf::launch_to_f32(d_src, (float*)*d_dst, n * 3, c->stream));
+  }
+  return FSDF_OK;
+}
+
+static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool device_src) {
+  if (!c) return FSDF_ERR_ARG;
+  if (n < 0 || (n > 0 && !src)) return fail(c, FSDF_ERR_ARG, "set_points: bad buffer (n=%lld)", (long long)n);
+  if (c->sort_points) return fail(c, FSDF_ERR_ARG, "set_points: sort_points is not available in this build");
+  HIPCHECK(c, hipSetDevice(c->device));
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  c->n = 0;
+  const double* d_src = src;
+  double* staging = nullptr;
+  if (!device_src && n > 0) {
+    HIPCHECK(c, hipMalloc(&staging, (size_t)n * 3 * sizeof(double)));
+    hipError_t e = hipMemcpy(staging, src, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(staging);
+      return fail(c, FSDF_ERR_HIP, "set_points: %s", hipGetErrorString(e));
+    }
+    d_src = staging;
+  }
+  int rc = adopt_points_device(c, d_src, n, &c->d_pts, &c->pts_cap);
+  if (rc == FSDF_OK) {
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) rc = fail(c, FSDF_ERR_HIP, "set_points: %s", hipGetErrorString(e));
+  }
+  if (staging) (void)hipFree(staging);
+  if (rc == FSDF_OK) c->n = n;
+  return rc;
+}
+
+extern "C" int fsdf_set_points(fsdf_ctx* c, const double* xyz, int64_t n) { return set_points_impl(c, xyz, n, false); }
+
+extern "C" int fsdf_set_points_device(fsdf_ctx* c, const double* d_xyz, int64_t n) {
+  return set_points_impl(c, d_xyz, n, true);
+}
+
+static int ensure_partials(fsdf_ctx* c, int nblocks) {
+  const size_t need = (size_t)(1 + 6 * c->lm.K) * nblocks;
+  if (c->partials_cap < need) {
+    dfree(c->d_partials);
+    c->partials_cap = 0;
+    HIPCHECK(c, hipMalloc(&c->d_partials, need * sizeof(double)));
+    c->partials_cap = need;
+  }
+  return FSDF_OK;
+}
+
+static int upload_poses(fsdf_ctx* c, const double* poses) {
+  for (int i = 0; i < 12 * c->lm.K; ++i)
+    if (!std::isfinite(poses[i])) return fail(c, FSDF_ERR_ARG, "poses: entry %d is not finite", i);
+  const int s = c->pose_slot;
+  c->pose_slot = (s + 1) % kPoseRing;
+  HIPCHECK(c, hipEventSynchronize(c->pose_ev[s]));  // slot free once its last copy ran
+  memcpy(c->h_poses[s], poses, (size_t)c->lm.K * 12 * sizeof(double));
+  HIPCHECK(c, hipMemcpyAsync(c->d_poses, c->h_poses[s], (size_t)c->lm.K * 12 * sizeof(double),
+                             hipMemcpyHostToDevice, c->stream));
+  HIPCHECK(c, hipEventRecord(c->pose_ev[s], c->stream));
+  return FSDF_OK;
+}
+
+static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t n, double* d_accum,
+                    int32_t* d_kstar, double* d_d, double* d_grad, const int64_t* d_perm) {
+  int rc = upload_poses(c, poses);
+  if (rc) return rc;
+  HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, c->d_poses, c->pm, c->stream));
+  const int nblocks = fsdf::pass_blocks(n);
+  rc = ensure_partials(c, nblocks);
+  if (rc) return rc;
+  fsdf::PassOutputs out;
+  out.partials = c->d_partials;
+  out.kstar = d_kstar;
+  out.d = d_d;
+  out.grad = d_grad;
+  out.perm = d_perm;
+  if (n > 0) {
+    const bool prof = c->profiling && c->prof_used + 2 <= c->prof_ev.size();
+    if (prof) HIPCHECK(c, hipEventRecord(c->prof_ev[c->prof_used], c->stream));
+    HIPCHECK(c, fsdf::launch_pass(c->precision, c->cull != 0, c->lm, c->pm, d_pts, n, nblocks, out, c->stream));
+    if (prof) {
+      HIPCHECK(c, hipEventRecord(c->prof_ev[c->prof_used + 1], c->stream));
+      c->prof_used += 2;
+    }
+    HIPCHECK(c, fsdf::launch_reduce(c->d_partials, nblocks, 1 + 6 * c->lm.K, d_accum, c->stream));
+  } else {
+    HIPCHECK(c, hipMemsetAsync(d_accum, 0, (size_t)(1 + 6 * c->lm.K) * sizeof(double), c->stream));
+  }
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_eval_device(fsdf_ctx* c, const double* poses, double* d_accum, int32_t* d_kstar, double* d_d,
+                                double* d_grad) {
+  if (!c) return FSDF_ERR_ARG;
+  if (c->lm.K == 0) return fail(c, FSDF_ERR_STATE, "eval: no model (call fsdf_set_model first)");
+  if (!poses || !d_accum) return fail(c, FSDF_ERR_ARG, "eval_device: poses and d_accum are required");
+  HIPCHECK(c, hipSetDevice(c->device));
+  return run_pass(c, poses, c->d_pts, c->n, d_accum, d_kstar, d_d, d_grad, c->d_perm);
+}
+
+static int ensure_outputs(fsdf_ctx* c, int64_t n) {
+  if (c->out_cap >= n) return FSDF_OK;
+  dfree(c->d_kstar);
+  dfree(c->d_d);
+  dfree(c->d_grad);
+  c->out_cap = 0;
+  HIPCHECK(c, hipMalloc(&c->d_kstar, (size_t)std::max<int64_t>(n, 1) * sizeof(int32_t)));
+  HIPCHECK(c, hipMalloc(&c->d_d, (size_t)std::max<int64_t>(n, 1) * sizeof(double)));
+  HIPCHECK(c, hipMalloc(&c->d_grad, (size_t)std::max<int64_t>(n, 1) * 3 * sizeof(double)));
+  c->out_cap = n;
+  return FSDF_OK;
+}
+
+static int fetch(fsdf_ctx* c, int64_t n, double* cost_out, double* accum_out, int32_t* kstar_out, double* d_out,
+                 double* grad_out, bool want_pp) {
+  const int len = 1 + 6 * c->lm.K;
+  std::vector<double> acc(len);
+  HIPCHECK(c, hipMemcpyAsync(acc.data(), c->d_accum, len * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (want_pp && n > 0) {
+    if (kstar_out)
+      HIPCHECK(c, hipMemcpyAsync(kstar_out, c->d_kstar, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    if (d_out) HIPCHECK(c, hipMemcpyAsync(d_out, c->d_d, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (grad_out)
+      HIPCHECK(c, hipMemcpyAsync(grad_out, c->d_grad, n * 3 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  if (cost_out) *cost_out = acc[0];
+  if (accum_out) memcpy(accum_out, acc.data(), len * sizeof(double));
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_eval(fsdf_ctx* c, const double* poses, double* cost_out, double* accum_out, int32_t* kstar_out,
+                         double* d_out, double* grad_out) {
+  if (!c) return FSDF_ERR_ARG;
+  if (c->lm.K == 0) return fail(c, FSDF_ERR_STATE, "eval: no model (call fsdf_set_model first)");
+  if (!poses) return fail(c, FSDF_ERR_ARG, "eval: poses required");
+  HIPCHECK(c, hipSetDevice(c->device));
+  const bool want_pp = kstar_out || d_out || grad_out;
+  if (want_pp) {
+    int rc = ensure_outputs(c, c->n);
+    if (rc) return rc;
+  }
+  int rc = run_pass(c, poses, c->d_pts, c->n, c->d_accum, want_pp ? c->d_kstar : nullptr,
+                    want_pp ? c->d_d : nullptr, want_pp ? c->d_grad : nullptr, c->d_perm);
+  if (rc) return rc;
+  return fetch(c, c->n, cost_out, accum_out, kstar_out, d_out, grad_out, want_pp);
+}
+
+extern "C" int fsdf_skin(fsdf_ctx* c, const double* poses, const double* xyz, int64_t n, double* d_out,
+                         int32_t* kstar_out, double* grad_out) {
+  if (!c) return FSDF_ERR_ARG;
+  if (c->lm.K == 0) return fail(c, FSDF_ERR_STATE, "skin: no model (call fsdf_set_model first)");
+  if (!poses || n < 0 || (n > 0 && !xyz)) return fail(c, FSDF_ERR_ARG, "skin: bad arguments");
+  HIPCHECK(c, hipSetDevice(c->device));
+  if (n == 0) return FSDF_OK;
+  int rc = ensure_outputs(c, n);
+  if (rc) return rc;
+  // stage the query points (f64 on the device, then the context precision)
+  if (c->q64_cap < n) {
+    HIPCHECK(c, hipStreamSynchronize(c->stream));
+    dfree(c->d_q64);
+    c->q64_cap = 0;
+    HIPCHECK(c, hipMalloc(&c->d_q64, (size_t)n * 3 * sizeof(double)));
+    c->q64_cap = n;
+  }
+  HIPCHECK(c, hipMemcpyAsync(c->d_q64, xyz, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  const void* d_query = c->d_q64;
+  if (c->precision != 64) {
+    rc = adopt_points_device(c, c->d_q64, n, &c->d_q, &c->q_cap);
+    if (rc) return rc;
+    d_query = c->d_q;
+  }
+  rc = run_pass(c, poses, d_query, n, c->d_accum, c->d_kstar, c->d_d, c->d_grad, nullptr);
+  if (rc) return rc;
+  return fetch(c, n, nullptr, nullptr, kstar_out, d_out, grad_out, true);
+}
+
+extern "C" int fsdf_synchronize(fsdf_ctx* c) {
+  if (!c) return FSDF_ERR_ARG;
+  HIPCHECK(c, hipSetDevice(c->device));
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_profile_pass(fsdf_ctx* c, int32_t enable) {
+  if (!c) return FSDF_ERR_ARG;
+  HIPCHECK(c, hipSetDevice(c->device));
+  if (enable && c->prof_ev.empty()) {
+    c->prof_ev.resize(2 * 4096, nullptr);
+    for (auto& e : c->prof_ev) HIPCHECK(c, hipEventCreate(&e));
+  }
+  c->profiling = enable != 0;
+  c->prof_used = 0;
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_pass_time(fsdf_ctx* c, double* total_ms, int64_t* launches) {
+  if (!c || !total_ms || !launches) return FSDF_ERR_ARG;
+  HIPCHECK(c, hipSetDevice(c->device));
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  double t = 0.0;
+  for (size_t i = 0; i + 1 < c->prof_used; i += 2) {
+    float ms = 0.f;
+    HIPCHECK(c, hipEventElapsedTime(&ms, c->prof_ev[i], c->prof_ev[i + 1]));
+    t += ms;
+  }
+  *total_ms = t;
+  *launches = (int64_t)(c->prof_used / 2);
+  c->prof_used = 0;
+  return FSDF_OK;
+}

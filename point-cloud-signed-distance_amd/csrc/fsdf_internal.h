@@ -1,0 +1,69 @@
+// Internal declarations shared by the kernel translation unit and the C-ABI.
+// Device layouts (all per-evaluation "world" arrays are produced on the device
+// by the pose kernel from the resident local model and the K poses):
+//
+//   local model (uploaded once by fsdf_set_model)
+//     verts_l   [V][3]  f64     hull vertices, body frame
+//     faces     [F][3]  i32     global vertex indices (CCW from outside)
+//     planes_l  [F][4]  f64     (n, d), n·x <= d inside
+//     face_hull [F]     i32     owning hull of each face
+//     sphere_l  [K][4]  f64     vertex centroid (inside the hull) + radius
+//     face_off  [K+1]   i32     faces of hull k are [face_off[k], face_off[k+1])
+//
+//   posed model (rewritten by every evaluation; T = double or float)
+//     planes_w  [F][4]  T       world plane
+//     facex_w   [F][24] T       3 inward edge planes (m_i, o_i) then a, b, c
+//     spheres_w [K][4]  f32     world centroid + radius (culling only)
+//
+//   per-block partial sums  partials [1+6K][nblocks] f64 (column = block)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fsdf {
+
+constexpr int kBlock = 256;        // 4 waves of 64
+constexpr int kFaceX = 24;         // stride of facex_w rows
+constexpr int kMaxHulls = 256;     // 4 accumulator slots per lane
+constexpr int kMaxBlocks = 2048;
+
+struct LocalModel {
+  int K = 0, F = 0, V = 0;
+  const double* verts_l = nullptr;
+  const int32_t* faces = nullptr;
+  const double* planes_l = nullptr;
+  const int32_t* face_hull = nullptr;
+  const double* sphere_l = nullptr;
+  const int32_t* face_off = nullptr;
+};
+
+struct PosedModel {
+  void* planes_w = nullptr;   // T
+  void* facex_w = nullptr;    // T
+  float* spheres_w = nullptr;
+};
+
+struct PassOutputs {
+  double* partials = nullptr;  // [1+6K][nblocks]
+  int32_t* kstar = nullptr;    // optional, caller order
+  double* d = nullptr;         // optional
+  double* grad = nullptr;      // optional [n][3]
+  const int64_t* perm = nullptr;  // optional: resident index -> caller index
+};
+
+// precision: 64 or 32. Points are AoS of the matching precision.
+hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_poses,
+                       const PosedModel& pm, hipStream_t s);
+
+hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm,
+                       const void* d_pts, int64_t n, int nblocks, const PassOutputs& out,
+                       hipStream_t s);
+
+hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum,
+                         hipStream_t s);
+
+hipError_t launch_to_f32(const double* src, float* dst, int64_t count, hipStream_t s);
+
+int pass_blocks(int64_t n);
+
+}  // namespace fsdf

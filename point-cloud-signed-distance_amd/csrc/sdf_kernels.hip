@@ -1,0 +1,451 @@
+// sdf_kernels.hip — the residual pass of Flash.jl on CDNA4 (gfx950).
+//
+// Reference semantics (src/Flash.jl:265-268, src/gradientdescent.jl:28-39):
+//   d*(p)  = minimum(s_k(p) for k in surfaces)       first k wins ties
+//   s_k(p) = gjk!(cache, pose_k, Translation(p)).signed_distance   (:238-243)
+//   c      = Σ_p d*(p)^2
+// restated here as the EXACT signed distance to the convex polytope conv(V_k):
+//   inside / on the surface:  max_f (n_f·p − d_f)
+//   outside:                  Euclidean distance to the closest boundary point
+// (EnhancedGJK returns the same value outside; its penetration value inside is a
+//  termination-simplex estimate and is replaced by the exact one — DESIGN.md §2).
+//
+// Kernel design:
+//   * one lane per point; each wave owns 64 consecutive resident points;
+//   * the posed model is read with wave-uniform (scalar) loads: every lane of a
+//     wave walks the same face list, so plane data is broadcast, never gathered;
+//   * exact-safe culling: a hull is skipped by a lane when the bounding-sphere
+//     lower bound |p−c_k|−r_k exceeds min(centroid upper bound, best so far) by a
+//     rounding margin; a wave evaluates hull k iff any lane needs it;
+//   * per-hull wrench sums are segmented by k* inside the wave (ballot loop +
+//     xor-shuffle tree), owned in registers by lane k mod 64, combined per block
+//     in LDS in fixed wave order, then reduced over blocks in fixed order: the
+//     whole reduction is deterministic for a given (n, grid).
+//
+// All arithmetic is written with explicit fma() and compiled with
+// -ffp-contract=off so that oracle/flash_oracle.c reproduces every per-hull
+// value bit for bit (the argmin k* must match exactly).
+
+#include "fsdf_internal.h"
+
+#include <math.h>
+
+namespace fsdf {
+
+template <typename T> __device__ __forceinline__ T mfma_(T a, T b, T c);
+template <> __device__ __forceinline__ double mfma_(double a, double b, double c) {
+  return __builtin_fma(a, b, c);
+}
+template <> __device__ __forceinline__ float mfma_(float a, float b, float c) {
+  return __builtin_fmaf(a, b, c);
+}
+template <typename T> __device__ __forceinline__ T tsqrt(T a);
+template <> __device__ __forceinline__ double tsqrt(double a) { return __builtin_sqrt(a); }
+template <> __device__ __forceinline__ float tsqrt(float a) { return __builtin_sqrtf(a); }
+template <typename T> __device__ __forceinline__ T tinf();
+template <> __device__ __forceinline__ double tinf() { return __builtin_huge_val(); }
+template <> __device__ __forceinline__ float tinf() { return __builtin_huge_valf(); }
+
+// ---------------------------------------------------------------------------
+// Pose kernel: local model + poses -> world-frame planes, edge planes, vertices.
+// One thread per face, then one per hull (spheres).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void xf_point(const double* P, const double* v, double* o) {
+  // o = R v + t, R row-major P[0..8], t = P[9..11]
+  o[0] = __builtin_fma(P[0], v[0], __builtin_fma(P[1], v[1], __builtin_fma(P[2], v[2], P[9])));
+  o[1] = __builtin_fma(P[3], v[0], __builtin_fma(P[4], v[1], __builtin_fma(P[5], v[2], P[10])));
+  o[2] = __builtin_fma(P[6], v[0], __builtin_fma(P[7], v[1], __builtin_fma(P[8], v[2], P[11])));
+}
+__device__ __forceinline__ void rot_vec(const double* P, const double* v, double* o) {
+  o[0] = __builtin_fma(P[0], v[0], __builtin_fma(P[1], v[1], P[2] * v[2]));
+  o[1] = __builtin_fma(P[3], v[0], __builtin_fma(P[4], v[1], P[5] * v[2]));
+  o[2] = __builtin_fma(P[6], v[0], __builtin_fma(P[7], v[1], P[8] * v[2]));
+}
+__device__ __forceinline__ void cross3(const double* a, const double* b, double* o) {
+  o[0] = __builtin_fma(a[1], b[2], -(a[2] * b[1]));
+  o[1] = __builtin_fma(a[2], b[0], -(a[0] * b[2]));
+  o[2] = __builtin_fma(a[0], b[1], -(a[1] * b[0]));
+}
+__device__ __forceinline__ double dot3(const double* a, const double* b) {
+  return __builtin_fma(a[0], b[0], __builtin_fma(a[1], b[1], a[2] * b[2]));
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const double* __restrict__ poses,
+                                                      T* __restrict__ planes_w, T* __restrict__ facex_w,
+                                                      float* __restrict__ spheres_w) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid < lm.F) {
+    const int f = tid;
+    const int k = lm.face_hull[f];
+    double P[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) P[i] = poses[12 * k + i];
+    const double* pl = lm.planes_l + 4 * f;
+    double n[3] = {pl[0], pl[1], pl[2]};
+    double nw[3];
+    rot_vec(P, n, nw);
+    // d_w = d + n_w · t
+    const double dw = __builtin_fma(nw[0], P[9], __builtin_fma(nw[1], P[10], __builtin_fma(nw[2], P[11], pl[3])));
+    double a[3], b[3], c[3];
+    xf_point(P, lm.verts_l + 3 * lm.faces[3 * f + 0], a);
+    xf_point(P, lm.verts_l + 3 * lm.faces[3 * f + 1], b);
+    xf_point(P, lm.verts_l + 3 * lm.faces[3 * f + 2], c);
+    const double e0[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+    const double e1[3] = {c[0] - b[0], c[1] - b[1], c[2] - b[2]};
+    const double e2[3] = {a[0] - c[0], a[1] - c[1], a[2] - c[2]};
+    double m0[3], m1[3], m2[3];
+    cross3(nw, e0, m0);
+    cross3(nw, e1, m1);
+    cross3(nw, e2, m2);
+    const double o0 = dot3(m0, a), o1 = dot3(m1, b), o2 = dot3(m2, c);
+    T* pw = planes_w + 4 * f;
+    pw[0] = (T)nw[0]; pw[1] = (T)nw[1]; pw[2] = (T)nw[2]; pw[3] = (T)dw;
+    T* fx = facex_w + kFaceX * f;
+    fx[0] = (T)m0[0]; fx[1] = (T)m0[1]; fx[2] = (T)m0[2]; fx[3] = (T)o0;
+    fx[4] = (T)m1[0]; fx[5] = (T)m1[1]; fx[6] = (T)m1[2]; fx[7] = (T)o1;
+    fx[8] = (T)m2[0]; fx[9] = (T)m2[1]; fx[10] = (T)m2[2]; fx[11] = (T)o2;
+    fx[12] = (T)a[0]; fx[13] = (T)a[1]; fx[14] = (T)a[2];
+    fx[15] = (T)b[0]; fx[16] = (T)b[1]; fx[17] = (T)b[2];
+    fx[18] = (T)c[0]; fx[19] = (T)c[1]; fx[20] = (T)c[2];
+    fx[21] = (T)0; fx[22] = (T)0; fx[23] = (T)0;
+  } else if (tid < lm.F + lm.K) {
+    const int k = tid - lm.F;
+    double P[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) P[i] = poses[12 * k + i];
+    double cw[3];
+    xf_point(P, lm.sphere_l + 4 * k, cw);
+    spheres_w[4 * k + 0] = (float)cw[0];
+    spheres_w[4 * k + 1] = (float)cw[1];
+    spheres_w[4 * k + 2] = (float)cw[2];
+    // radius was rounded up to float on the host (exact-safe)
+    spheres_w[4 * k + 3] = (float)lm.sphere_l[4 * k + 3];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Closest point on triangle (a, b, c) to p — Voronoi-region walk.
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void closest_on_triangle(T px, T py, T pz, const T* __restrict__ v, T& qx,
+                                                    T& qy, T& qz) {
+  const T ax = v[0], ay = v[1], az = v[2];
+  const T bx = v[3], by = v[4], bz = v[5];
+  const T cx = v[6], cy = v[7], cz = v[8];
+  const T abx = bx - ax, aby = by - ay, abz = bz - az;
+  const T acx = cx - ax, acy = cy - ay, acz = cz - az;
+  const T apx = px - ax, apy = py - ay, apz = pz - az;
+  const T d1 = mfma_(abx, apx, mfma_(aby, apy, abz * apz));
+  const T d2 = mfma_(acx, apx, mfma_(acy, apy, acz * apz));
+  if (d1 <= (T)0 && d2 <= (T)0) { qx = ax; qy = ay; qz = az; return; }
+  const T bpx = px - bx, bpy = py - by, bpz = pz - bz;
+  const T d3 = mfma_(abx, bpx, mfma_(aby, bpy, abz * bpz));
+  const T d4 = mfma_(acx, bpx, mfma_(acy, bpy, acz * bpz));
+  if (d3 >= (T)0 && d4 <= d3) { qx = bx; qy = by; qz = bz; return; }
+  const T vc = mfma_(d1, d4, -(d3 * d2));
+  if (vc <= (T)0 && d1 >= (T)0 && d3 <= (T)0) {
+    const T t = d1 / (d1 - d3);
+    qx = mfma_(t, abx, ax); qy = mfma_(t, aby, ay); qz = mfma_(t, abz, az);
+    return;
+  }
+  const T cpx = px - cx, cpy = py - cy, cpz = pz - cz;
+  const T d5 = mfma_(abx, cpx, mfma_(aby, cpy, abz * cpz));
+  const T d6 = mfma_(acx, cpx, mfma_(acy, cpy, acz * cpz));
+  if (d6 >= (T)0 && d5 <= d6) { qx = cx; qy = cy; qz = cz; return; }
+  const T vb = mfma_(d5, d2, -(d1 * d6));
+  if (vb <= (T)0 && d2 >= (T)0 && d6 <= (T)0) {
+    const T t = d2 / (d2 - d6);
+    qx = mfma_(t, acx, ax); qy = mfma_(t, acy, ay); qz = mfma_(t, acz, az);
+    return;
+  }
+  const T va = mfma_(d3, d6, -(d5 * d4));
+  const T e43 = d4 - d3, e56 = d5 - d6;
+  if (va <= (T)0 && e43 >= (T)0 && e56 >= (T)0) {
+    const T t = e43 / (e43 + e56);
+    qx = mfma_(t, cx - bx, bx); qy = mfma_(t, cy - by, by); qz = mfma_(t, cz - bz, bz);
+    return;
+  }
+  const T inv = (T)1 / (va + vb + vc);
+  const T v_ = vb * inv, w_ = vc * inv;
+  qx = mfma_(w_, acx, mfma_(v_, abx, ax));
+  qy = mfma_(w_, acy, mfma_(v_, aby, ay));
+  qz = mfma_(w_, acz, mfma_(v_, abz, az));
+}
+
+// ---------------------------------------------------------------------------
+// Exact signed distance of p to posed hull with faces [f0, f1).
+// `active`: this lane's result is used (controls only the wave-uniform branch
+// into the closest-feature scan). Result gradient is world-frame, unit length.
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ void hull_sdf(T px, T py, T pz, int f0, int f1, const T* __restrict__ planes,
+                                         const T* __restrict__ facex, bool active, T& d, T& gx, T& gy,
+                                         T& gz) {
+  T hmax = -tinf<T>();
+  int fs = f0;
+#pragma unroll 4
+  for (int f = f0; f < f1; ++f) {
+    const T* pl = planes + 4 * f;
+    const T h = mfma_(pl[0], px, mfma_(pl[1], py, mfma_(pl[2], pz, -pl[3])));
+    if (h > hmax) { hmax = h; fs = f; }
+  }
+  const T* pls = planes + 4 * fs;
+  d = hmax;
+  gx = pls[0]; gy = pls[1]; gz = pls[2];
+  bool slow = false;
+  if (hmax > (T)0) {
+    // Fast path: the projection of p on the max-violated face lies inside that
+    // triangle => it is the closest point and the distance equals hmax.
+    const T* fx = facex + kFaceX * fs;
+    const T s0 = mfma_(fx[0], px, mfma_(fx[1], py, mfma_(fx[2], pz, -fx[3])));
+    const T s1 = mfma_(fx[4], px, mfma_(fx[5], py, mfma_(fx[6], pz, -fx[7])));
+    const T s2 = mfma_(fx[8], px, mfma_(fx[9], py, mfma_(fx[10], pz, -fx[11])));
+    slow = !(s0 >= (T)0 && s1 >= (T)0 && s2 >= (T)0);
+  }
+  slow = slow && active;
+  if (__any(slow)) {
+    // Closest feature over the faces visible from p (h_f > 0): the closest
+    // boundary point of a convex polytope lies on one of them.
+    T best2 = tinf<T>();
+    T qbx = (T)0, qby = (T)0, qbz = (T)0;
+    for (int f = f0; f < f1; ++f) {
+      const T* pl = planes + 4 * f;
+      const T h = mfma_(pl[0], px, mfma_(pl[1], py, mfma_(pl[2], pz, -pl[3])));
+      if (slow && h > (T)0) {
+        T qx, qy, qz;
+        closest_on_triangle(px, py, pz, facex + kFaceX * f + 12, qx, qy, qz);
+        const T dx = px - qx, dy = py - qy, dz = pz - qz;
+        const T dist2 = mfma_(dx, dx, mfma_(dy, dy, dz * dz));
+        if (dist2 < best2) { best2 = dist2; qbx = qx; qby = qy; qbz = qz; }
+      }
+    }
+    if (slow) {
+      d = tsqrt(best2);
+      const T inv = (T)1 / d;
+      gx = (px - qbx) * inv; gy = (py - qby) * inv; gz = (pz - qbz) * inv;
+    }
+  }
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Residual pass.
+// ---------------------------------------------------------------------------
+template <typename T, int SLOTS, bool CULL>
+__global__ __launch_bounds__(kBlock) void pass_kernel(const T* __restrict__ pts, int64_t n, int K,
+                                                      const int32_t* __restrict__ face_off,
+                                                      const T* __restrict__ planes,
+                                                      const T* __restrict__ facex,
+                                                      const float* __restrict__ spheres, PassOutputs out) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  double accF[SLOTS][3], accM[SLOTS][3];
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { accF[s][j] = 0.0; accM[s][j] = 0.0; }
+  double cost_acc = 0.0;
+
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t base = (int64_t)blockIdx.x * kBlock + wave * 64; base < n; base += stride) {
+    const int64_t i = base + lane;
+    const bool valid = i < n;
+    const int64_t ii = valid ? i : n - 1;
+    const T px = pts[3 * ii + 0], py = pts[3 * ii + 1], pz = pts[3 * ii + 2];
+
+    float ub = __builtin_huge_valf();
+    float pxf = 0.f, pyf = 0.f, pzf = 0.f, pmag = 0.f;
+    if (CULL) {
+      pxf = (float)px; pyf = (float)py; pzf = (float)pz;
+      pmag = fabsf(pxf) + fabsf(pyf) + fabsf(pzf);
+      for (int k = 0; k < K; ++k) {
+        const float* sp = spheres + 4 * k;
+        const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
+        ub = fminf(ub, __builtin_sqrtf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz))));
+      }
+    }
+
+    T best = tinf<T>();
+    int bk = 0;
+    T gx = (T)0, gy = (T)0, gz = (T)0;
+    for (int k = 0; k < K; ++k) {
+      bool need = valid;
+      if (CULL) {
+        const float* sp = spheres + 4 * k;
+        const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
+        const float dist = __builtin_sqrtf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)));
+        const float lb = dist - sp[3];
+        const float bf = fminf(ub, (float)best);
+        const float mrg = 1e-5f * (1.0f + pmag + fabsf(sp[0]) + fabsf(sp[1]) + fabsf(sp[2]) + sp[3] + dist +
+                                   fabsf(bf));
+        need = valid && (lb <= bf + mrg);
+      }
+      if (!__any(need)) continue;
+      const int f0 = __builtin_amdgcn_readfirstlane(face_off[k]);
+      const int f1 = __builtin_amdgcn_readfirstlane(face_off[k + 1]);
+      T dk, hx, hy, hz;
+      hull_sdf<T>(px, py, pz, f0, f1, planes, facex, need, dk, hx, hy, hz);
+      if (need && dk < best) { best = dk; bk = k; gx = hx; gy = hy; gz = hz; }
+    }
+
+    // contributions: c += d^2; F_k += 2 d g; M_k += 2 d (p x g)
+    double cF[3] = {0.0, 0.0, 0.0}, cM[3] = {0.0, 0.0, 0.0};
+    if (valid) {
+      const double bd = (double)best;
+      const double dgx = gx, dgy = gy, dgz = gz;
+      const double dpx = px, dpy = py, dpz = pz;
+      cost_acc = __builtin_fma(bd, bd, cost_acc);
+      const double w = 2.0 * bd;
+      cF[0] = w * dgx; cF[1] = w * dgy; cF[2] = w * dgz;
+      cM[0] = w * __builtin_fma(dpy, dgz, -(dpz * dgy));
+      cM[1] = w * __builtin_fma(dpz, dgx, -(dpx * dgz));
+      cM[2] = w * __builtin_fma(dpx, dgy, -(dpy * dgx));
+    }
+    uint64_t pending = __ballot(valid);
+    while (pending) {
+      const int leader = __builtin_ctzll(pending);
+      const int kk = __shfl(bk, leader, 64);
+      const bool sel = valid && (bk == kk);
+      pending &= ~__ballot(sel);
+      double v[6];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) { v[j] = sel ? cF[j] : 0.0; v[3 + j] = sel ? cM[j] : 0.0; }
+#pragma unroll
+      for (int j = 0; j < 6; ++j) v[j] = wave_sum(v[j]);
+      if (lane == (kk & 63)) {
+        const int slot = kk >> 6;
+#pragma unroll
+        for (int s = 0; s < SLOTS; ++s) {
+          if (s == slot) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) { accF[s][j] += v[j]; accM[s][j] += v[3 + j]; }
+          }
+        }
+      }
+    }
+
+    if (valid) {
+      const int64_t o = out.perm ? out.perm[i] : i;
+      if (out.kstar) out.kstar[o] = bk;
+      if (out.d) out.d[o] = (double)best;
+      if (out.grad) {
+        out.grad[3 * o + 0] = (double)gx;
+        out.grad[3 * o + 1] = (double)gy;
+        out.grad[3 * o + 2] = (double)gz;
+      }
+    }
+  }
+
+  // ---- block combine (fixed order) ----
+  __shared__ double red[kBlock / 64][SLOTS * 64 * 6 + 1];
+  cost_acc = wave_sum(cost_acc);
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) {
+    double* r = &red[wave][(s * 64 + lane) * 6];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { r[j] = accF[s][j]; r[3 + j] = accM[s][j]; }
+  }
+  if (lane == 0) red[wave][SLOTS * 64 * 6] = cost_acc;
+  __syncthreads();
+  const int len = 1 + 6 * K;
+  for (int t = threadIdx.x; t < len; t += kBlock) {
+    const int src = (t == 0) ? SLOTS * 64 * 6 : t - 1;
+    double s = red[0][src];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) s += red[w][src];
+    out.partials[(int64_t)t * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict__ partials, int nblocks,
+                                                        double* __restrict__ accum) {
+  const int j = blockIdx.x;
+  double s = 0.0;
+  for (int b = threadIdx.x; b < nblocks; b += kBlock) s += partials[(int64_t)j * nblocks + b];
+  __shared__ double sh[kBlock];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = kBlock / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) accum[j] = sh[0];
+}
+
+__global__ void to_f32_kernel(const double* __restrict__ src, float* __restrict__ dst, int64_t count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) dst[i] = (float)src[i];
+}
+
+// ---------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------
+int pass_blocks(int64_t n) {
+  int64_t b = (n + kBlock - 1) / kBlock;
+  if (b < 1) b = 1;
+  if (b > kMaxBlocks) b = kMaxBlocks;
+  return (int)b;
+}
+
+hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_poses, const PosedModel& pm,
+                       hipStream_t s) {
+  const int total = lm.F + lm.K;
+  const int grid = (total + kBlock - 1) / kBlock;
+  if (precision == 64) {
+    hipLaunchKernelGGL(pose_kernel<double>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses,
+                       (double*)pm.planes_w, (double*)pm.facex_w, pm.spheres_w);
+  } else {
+    hipLaunchKernelGGL(pose_kernel<float>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses, (float*)pm.planes_w,
+                       (float*)pm.facex_w, pm.spheres_w);
+  }
+  return hipGetLastError();
+}
+
+template <typename T, bool CULL>
+static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void* d_pts, int64_t n, int nblocks,
+                          const PassOutputs& out, hipStream_t s) {
+  const T* pts = (const T*)d_pts;
+  const T* planes = (const T*)pm.planes_w;
+  const T* facex = (const T*)pm.facex_w;
+  if (lm.K <= 64)
+    hipLaunchKernelGGL((pass_kernel<T, 1, CULL>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, lm.K, lm.face_off,
+                       planes, facex, pm.spheres_w, out);
+  else if (lm.K <= 128)
+    hipLaunchKernelGGL((pass_kernel<T, 2, CULL>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, lm.K, lm.face_off,
+                       planes, facex, pm.spheres_w, out);
+  else
+    hipLaunchKernelGGL((pass_kernel<T, 4, CULL>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, lm.K, lm.face_off,
+                       planes, facex, pm.spheres_w, out);
+}
+
+hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const void* d_pts,
+                       int64_t n, int nblocks, const PassOutputs& out, hipStream_t s) {
+  if (precision == 64) {
+    if (cull) launch_pass_t<double, true>(lm, pm, d_pts, n, nblocks, out, s);
+    else launch_pass_t<double, false>(lm, pm, d_pts, n, nblocks, out, s);
+  } else {
+    if (cull) launch_pass_t<float, true>(lm, pm, d_pts, n, nblocks, out, s);
+    else launch_pass_t<float, false>(lm, pm, d_pts, n, nblocks, out, s);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_kernel, dim3(len), dim3(kBlock), 0, s, partials, nblocks, d_accum);
+  return hipGetLastError();
+}
+
+hipError_t launch_to_f32(const double* src, float* dst, int64_t count, hipStream_t s) {
+  if (count <= 0) return hipSuccess;
+  const int64_t grid = (count + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(to_f32_kernel, dim3((unsigned)grid), dim3(kBlock), 0, s, src, dst, count);
+  return hipGetLastError();
+}
+
+}  // namespace fsdf

@@ -1,0 +1,177 @@
+"""Core geometry and state types + the scene signed-distance closure.
+
+Mirrors module Flash (src/Flash.jl):
+  BodyGeometry / ConvexGeometry / Rigid- & DeformableInterpolatingSkin  :30-48
+  Manipulator (mechanism + surfaces)                                    :62-67
+  ManipulatorState (configuration + deformation views)                  :71-125
+  num_deformations / num_states                                         :79-90
+  surfaces(state), skin(state)                                          :261-268
+The closure `skin(state)` evaluates every point on the GPU through
+libflashsdf (one launch per batch of points), never on the CPU.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from .geometry import ConvexHull, Transform
+from .mechanism import Mechanism
+
+
+class BodyGeometry:
+    """abstract BodyGeometry (src/Flash.jl:30)."""
+
+    def num_deformations(self) -> int:
+        return 0
+
+
+class ConvexGeometry(BodyGeometry):
+    """ConvexGeometry{GeomType}(geometry, frame) (src/Flash.jl:45-48).
+
+    `hull` is expressed in the geometry frame; `frame` is that frame's fixed
+    transform relative to body `body` (the URDF visual origin, src/models.jl:154-164)."""
+
+    def __init__(self, hull: ConvexHull, body: int, frame: Transform | None = None, name: str = ""):
+        self.hull = hull
+        self.body = body
+        self.frame = frame or Transform.identity()
+        self.name = name
+
+    def __repr__(self):
+        return f"ConvexGeometry({self.name or 'hull'}, {len(self.hull.vertices)} vertices, body={self.body})"
+
+
+class InterpolatingGeometry(BodyGeometry):
+    """abstract InterpolatingGeometry (src/Flash.jl:33): RBF skins over surface
+    points (value 0) and skeleton points (value −1), src/Flash.jl:207-213."""
+
+    def __init__(self, surface_points, skeleton_points):
+        # lists of (body index, xyz in body frame)
+        self.surface_points = [(int(b), np.asarray(p, np.float64)) for b, p in surface_points]
+        self.skeleton_points = [(int(b), np.asarray(p, np.float64)) for b, p in skeleton_points]
+
+
+class RigidInterpolatingSkin(InterpolatingGeometry):
+    """src/Flash.jl:40-43."""
+
+
+class DeformableInterpolatingSkin(InterpolatingGeometry):
+    """src/Flash.jl:35-38: every surface point carries a 3-vector deformation."""
+
+    def num_deformations(self) -> int:
+        return len(self.surface_points)
+
+
+class Manipulator:
+    """Manipulator{T}(mechanism, surfaces) (src/Flash.jl:62-65)."""
+
+    def __init__(self, mechanism: Mechanism, surfaces: list[BodyGeometry]):
+        self.mechanism = mechanism
+        self.surfaces = list(surfaces)
+        self._engines: dict = {}
+
+    def __repr__(self):
+        return (f"Manipulator with {self.mechanism.num_bodies} links and {len(self.surfaces)} surfaces")
+
+    def num_deformations(self) -> int:
+        return sum(s.num_deformations() for s in self.surfaces)
+
+    def convex_surfaces(self) -> list[ConvexGeometry]:
+        return [s for s in self.surfaces if isinstance(s, ConvexGeometry)]
+
+    def engine(self, device: int = 0, precision: int = 64, cull: bool = True) -> "_lib.Context":
+        """The native context holding this model on `device` (created once)."""
+        key = (device, precision, cull)
+        ctx = self._engines.get(key)
+        if ctx is None:
+            if len(self.convex_surfaces()) != len(self.surfaces):
+                raise NotImplementedError(
+                    "RBF (InterpolatingSkin) surfaces are not in the GPU residual pass yet "
+                    "(SURVEY.md §8f rank 2); this model has "
+                    f"{len(self.surfaces) - len(self.convex_surfaces())} of them")
+            ctx = _lib.Context(device=device, precision=precision, cull=cull)
+            ctx.set_model([(s.hull.vertices, s.hull.faces, s.hull.planes) for s in self.surfaces])
+            self._engines[key] = ctx
+        return ctx
+
+    def invalidate(self):
+        """Drop device contexts (after editing surfaces / merging)."""
+        for ctx in self._engines.values():
+            ctx.close()
+        self._engines.clear()
+
+
+def num_deformations(x) -> int:
+    return x.num_deformations()
+
+
+def num_states(manip: Manipulator) -> int:
+    """num_positions + 3·#deformable points (src/Flash.jl:90)."""
+    return manip.mechanism.num_positions + 3 * manip.num_deformations()
+
+
+@dataclass
+class ManipulatorState:
+    """ManipulatorState (src/Flash.jl:71-125). `q` is the RBD configuration,
+    `deformation_data` the flat δ vector; `deformations[i]` are (n,3) views,
+    one per surface, in surface order (src/Flash.jl:97-104)."""
+    manipulator: Manipulator
+    q: np.ndarray = None
+    deformation_data: np.ndarray = None
+    deformations: list = field(default_factory=list)
+
+    def __post_init__(self):
+        m = self.manipulator
+        if self.q is None:
+            self.q = m.mechanism.zero_configuration()
+        if self.deformation_data is None:
+            self.deformation_data = np.zeros(3 * m.num_deformations())
+        self.deformations = []
+        off = 0
+        for s in m.surfaces:
+            nd = s.num_deformations()
+            self.deformations.append(self.deformation_data[off:off + 3 * nd].reshape(nd, 3))
+            off += 3 * nd
+
+    def set_configuration(self, q):
+        self.q[:] = q
+
+
+def hull_poses(manip: Manipulator, q: np.ndarray) -> np.ndarray:
+    """[K,12] world poses of the convex surfaces: transform_to_root(state, frame)
+    (src/Flash.jl:248) = T_world_body · T_body_geometry."""
+    T = manip.mechanism.body_transforms(q)
+    return np.stack([(T[s.body] @ s.frame).as_pose12() for s in manip.convex_surfaces()])
+
+
+class SceneSkin:
+    """The closure returned by skin(state): x -> minimum(s(x) for s in surfaces)
+    (src/Flash.jl:265-268). Accepts one point (returns a float) or an (n,3)
+    batch (returns an array). `.evaluate` also returns k* and ∇d*."""
+
+    def __init__(self, state: ManipulatorState, device: int = 0, precision: int = 64):
+        self.state = state
+        self.ctx = state.manipulator.engine(device, precision)
+        self.poses = hull_poses(state.manipulator, state.manipulator.mechanism.normalize(state.q))
+
+    def evaluate(self, x):
+        pts = np.asarray(x, np.float64).reshape(-1, 3)
+        return self.ctx.skin(self.poses, pts)
+
+    def __call__(self, x):
+        x = np.asarray(x, np.float64)
+        d, _, _ = self.evaluate(x)
+        return float(d[0]) if x.ndim == 1 else d
+
+
+def surfaces(state: ManipulatorState) -> list:
+    """surfaces(state) (src/Flash.jl:261-263): one posed evaluator per surface."""
+    poses = hull_poses(state.manipulator, state.manipulator.mechanism.normalize(state.q))
+    return [(s, Transform(p[:9].reshape(3, 3), p[9:])) for s, p in zip(state.manipulator.convex_surfaces(), poses)]
+
+
+def skin(state: ManipulatorState, device: int = 0, precision: int = 64) -> SceneSkin:
+    """Flash.skin(state) (src/Flash.jl:265-268)."""
+    return SceneSkin(state, device, precision)

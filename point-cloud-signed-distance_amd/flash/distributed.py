@@ -1,0 +1,77 @@
+"""Point-sharded residual pass over several GPUs (one process per GPU).
+
+The reference is single-threaded (no parallelism anywhere); its
+cost is a plain sum over independent points (src/gradientdescent.jl:32) and k*
+is per point, so the cloud shards trivially:
+  * each rank holds a contiguous ⌈N/W⌉ slice of the cloud (uploaded once per frame);
+  * every rank computes the same forward kinematics and ships the same K poses
+    (no collective for parameters);
+  * ONE all-reduce(sum, fp64) of the 1+6K accumulator per residual pass — over
+    RCCL (torch.distributed backend "nccl") between GPUs, gloo on CPU tests.
+The accumulator never leaves the device on the GPU path: fsdf_eval_device
+writes it into a torch tensor that is all-reduced in place.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .core import Manipulator, ManipulatorState, hull_poses
+from .gradientdescent import _regularizer, default_deformation_cost_weight, normalize, unflatten
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous slice [start, stop) of n points owned by `rank`."""
+    per = -(-n // world)
+    start = min(rank * per, n)
+    return start, min(start + per, n)
+
+
+def allreduce_accum(accum, group=None):
+    """Sum the per-rank accumulators in place (torch tensor, any device)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(accum, op=dist.ReduceOp.SUM, group=group)
+    return accum
+
+
+def chain_gradient(manip: Manipulator, x: np.ndarray, accum: np.ndarray, weight) -> np.ndarray:
+    mech = manip.mechanism
+    body_w = np.zeros((mech.num_bodies, 6))
+    for k, s in enumerate(manip.convex_surfaces()):
+        body_w[s.body] += accum[1 + 6 * k: 7 + 6 * k]
+    nq = mech.num_positions
+    return np.concatenate([mech.config_gradient(x[:nq], body_w), 2.0 * weight * x[nq:]])
+
+
+class ShardedCostFunctor:
+    """CostFunctor over this rank's shard; value/gradient are global (all-reduced)."""
+
+    def __init__(self, manipulator: Manipulator, local_points, rank: int = 0, world: int = 1, device: int = 0,
+                 precision: int = 64, group=None, deformation_cost_weight=default_deformation_cost_weight):
+        import torch
+        self.torch = torch
+        self.manipulator = manipulator
+        self.group = group
+        self.weight = deformation_cost_weight
+        self.state = ManipulatorState(manipulator)
+        self.ctx = manipulator.engine(device, precision)
+        self.dev = torch.device("cuda", device)
+        pts = torch.as_tensor(np.ascontiguousarray(local_points, np.float64).reshape(-1, 3), device=self.dev)
+        self.ctx.set_points_device(pts.data_ptr(), pts.shape[0])
+        self.accum = torch.zeros(1 + 6 * self.ctx.K, dtype=torch.float64, device=self.dev)
+        self.stream = torch.cuda.current_stream(self.dev)
+        self.ctx.set_stream(self.stream.cuda_stream)
+
+    def launch(self, x):
+        """Enqueue one residual pass + all-reduce (asynchronous)."""
+        unflatten(self.state, x)
+        normalize(self.state)
+        self.ctx.eval_device(hull_poses(self.manipulator, self.state.q), self.accum.data_ptr())
+        allreduce_accum(self.accum, self.group)
+        return self.accum
+
+    def value_and_gradient(self, x):
+        x = np.asarray(x, np.float64)
+        acc = self.launch(x).cpu().numpy()
+        c = float(acc[0]) + _regularizer(self.state, self.weight)
+        return c, chain_gradient(self.manipulator, x, acc, self.weight)

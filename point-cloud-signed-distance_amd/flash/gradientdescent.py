@@ -1,0 +1,106 @@
+"""module Flash.GradientDescent (src/gradientdescent.jl).
+
+  default_deformation_cost_weight = 10          :7
+  flatten(state) / unflatten!(state, x)         :9-17
+  normalize!(mechanism_state)                   :19-26
+  cost(state, sensed_points, weight)            :28-39
+  CostFunctor(manipulator, sensed_points)(x)    :41-57
+In the reference the gradient of CostFunctor comes from ForwardDiff (Dual{9}
+chunk passes, ⌈n/9⌉ full point passes per gradient, examples/irb_and_squishable
+.ipynb:482). Here ONE GPU residual pass returns the cost and the per-hull
+wrenches, and `value_and_gradient` chains them analytically to ∂c/∂x.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .core import Manipulator, ManipulatorState, hull_poses
+
+default_deformation_cost_weight = 10
+
+
+def flatten(state: ManipulatorState) -> np.ndarray:
+    """vcat(q, deformation_data) (src/gradientdescent.jl:9-11)."""
+    return np.concatenate([state.q, state.deformation_data])
+
+
+def unflatten(state: ManipulatorState, x) -> None:
+    """unflatten!(state, x) (src/gradientdescent.jl:13-17)."""
+    x = np.asarray(x, np.float64)
+    nq = state.manipulator.mechanism.num_positions
+    state.q[:] = x[:nq]
+    state.deformation_data[:] = x[nq:]
+
+
+def normalize(state: ManipulatorState) -> None:
+    """normalize!(state.mechanism_state) in place (src/gradientdescent.jl:19-26)."""
+    state.q[:] = state.manipulator.mechanism.normalize(state.q)
+
+
+def _regularizer(state: ManipulatorState, weight) -> float:
+    return float(weight) * float(np.dot(state.deformation_data, state.deformation_data))
+
+
+def cost(state: ManipulatorState, sensed_points, deformation_cost_weight=default_deformation_cost_weight,
+         device: int = 0, precision: int = 64) -> float:
+    """Σ_p skin(p)^2 + w·Σ‖δ‖² (src/gradientdescent.jl:28-39); normalizes q in place first."""
+    normalize(state)
+    m = state.manipulator
+    ctx = m.engine(device, precision)
+    pts = np.asarray(sensed_points, np.float64).reshape(-1, 3)
+    d, _, _ = ctx.skin(hull_poses(m, state.q), pts) if len(pts) else (np.zeros(0), None, None)
+    return float(np.dot(d, d)) + _regularizer(state, deformation_cost_weight)
+
+
+class CostFunctor:
+    """CostFunctor(manipulator, sensed_points) (src/gradientdescent.jl:41-57).
+
+    The sensed cloud is uploaded once (the reference keeps it by reference for
+    every evaluation); each call ships only the hull poses."""
+
+    def __init__(self, manipulator: Manipulator, sensed_points, device: int = 0, precision: int = 64,
+                 deformation_cost_weight=default_deformation_cost_weight):
+        self.manipulator = manipulator
+        self.sensed_points = np.ascontiguousarray(sensed_points, np.float64).reshape(-1, 3)
+        self.weight = deformation_cost_weight
+        self.state = ManipulatorState(manipulator)
+        self.ctx = manipulator.engine(device, precision)
+        # a private context would be needed to keep two functors resident at once
+        self.ctx.set_points(self.sensed_points)
+        self._resident = id(self)
+        manipulator._resident_cloud = self._resident
+
+    def _ensure_resident(self):
+        if getattr(self.manipulator, "_resident_cloud", None) != self._resident:
+            self.ctx.set_points(self.sensed_points)
+            self.manipulator._resident_cloud = self._resident
+
+    def _pass(self, x, per_point=False):
+        unflatten(self.state, x)
+        normalize(self.state)
+        self._ensure_resident()
+        c, accum, extras = self.ctx.eval(hull_poses(self.manipulator, self.state.q), per_point)
+        return c + _regularizer(self.state, self.weight), accum, extras
+
+    def __call__(self, x) -> float:
+        return self._pass(x)[0]
+
+    def value_and_gradient(self, x):
+        """(c(x), ∂c/∂x) from one residual pass."""
+        x = np.asarray(x, np.float64)
+        c, accum, _ = self._pass(x)
+        m = self.manipulator
+        mech = m.mechanism
+        body_w = np.zeros((mech.num_bodies, 6))
+        for k, s in enumerate(m.convex_surfaces()):
+            body_w[s.body] += accum[1 + 6 * k: 7 + 6 * k]
+        nq = mech.num_positions
+        # the gradient is taken at the caller's (un-normalized) x: the chain
+        # rule includes the normalization projection (src/gradientdescent.jl:30)
+        gq = mech.config_gradient(x[:nq], body_w)
+        gd = 2.0 * self.weight * x[nq:]
+        return c, np.concatenate([gq, gd])
+
+    def per_point(self, x):
+        """(d*, k*, ∇d*) for every sensed point at configuration x."""
+        return self._pass(x, per_point=True)[2]

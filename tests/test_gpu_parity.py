@@ -1,0 +1,194 @@
+"""GPU parity: the HIP residual pass (through the C-ABI) against the CPU oracle
+and the committed golden vectors.
+
+Bar (BASELINE.json north_star): nearest-primitive index k* bit-exact; fp64
+distances/gradients within 1e-6 relative. The kernel and oracle share the
+operation order, so d* and ∇d* are in fact compared bit for bit; sums (cost,
+wrenches) differ only in summation order and are compared at 1e-9 relative.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, rng
+
+pytestmark = pytest.mark.gpu
+
+RTOL_SUM = 1e-9
+
+
+@pytest.fixture(scope="module")
+def ctx_factory():
+    from flash import _lib
+    made = []
+
+    def make(manip, precision=64, cull=True):
+        c = _lib.Context(device=0, precision=precision, cull=cull)
+        c.set_model([(s.hull.vertices, s.hull.faces, s.hull.planes) for s in manip.convex_surfaces()])
+        made.append(c)
+        return c
+    yield make
+    for c in made:
+        c.close()
+
+
+def _model(name):
+    from flash import Models
+    return {"c1_irb140": Models.irb140, "m64_2k": Models.arm_grid, "table_quat": Models.table}[name]()
+
+
+def _check_against(oracle_out, d, k, g, accum=None, oracle_accum=None, exact=True):
+    od, ok, og = oracle_out
+    assert np.array_equal(k, ok), f"k* mismatch at {np.nonzero(k != ok)[0][:10]}"
+    if exact:
+        assert np.array_equal(d, od), f"max |Δd| = {np.abs(d - od).max()}"
+        assert np.array_equal(g, og), f"max |Δg| = {np.abs(g - og).max()}"
+    else:
+        assert np.allclose(d, od, rtol=1e-6, atol=1e-12)
+        assert np.allclose(g, og, rtol=1e-6, atol=1e-9)
+    if accum is not None:
+        assert np.allclose(accum, oracle_accum, rtol=RTOL_SUM, atol=1e-9 * max(1.0, abs(oracle_accum).max()))
+
+
+@pytest.mark.parametrize("name", ["c1_irb140", "m64_2k", "table_quat"])
+@pytest.mark.parametrize("cull", [True, False])
+def test_golden_parity(name, cull, ctx_factory):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    ctx = ctx_factory(_model(name), cull=cull)
+    ctx.set_points(z["points"])
+    cost, accum, (k, d, g) = ctx.eval(z["poses"], per_point=True)
+    _check_against((z["d"], z["kstar"], z["grad"]), d, k, g, accum, z["accum"])
+    assert cost == accum[0]
+    # the skin() entry point (arbitrary query points) agrees with the resident pass
+    d2, k2, g2 = ctx.skin(z["poses"], z["points"])
+    assert np.array_equal(d2, d) and np.array_equal(k2, k) and np.array_equal(g2, g)
+
+
+def test_m64_parity_64k(m64, oracle_mod, ctx_factory):
+    from flash import synthetic
+    import flash
+    qt, qe = synthetic.perturbed_configuration(m64, 101)
+    for order in ("raster", "shuffled"):
+        pts = synthetic.depth_cloud(m64, qt, 65536 + 37, seed=102, order=order)
+        poses = flash.hull_poses(m64, qe)
+        om = oracle_mod.OracleModel.from_manipulator(m64)
+        ref = om.skin(poses, pts)
+        ref_acc = om.cost_accum(poses, pts)
+        for cull in (True, False):
+            ctx = ctx_factory(m64, cull=cull)
+            ctx.set_points(pts)
+            _, acc, (k, d, g) = ctx.eval(poses, per_point=True)
+            _check_against(ref, d, k, g, acc, ref_acc)
+
+
+def test_edge_cases(irb, oracle_mod, ctx_factory):
+    import flash
+    ctx = ctx_factory(irb)
+    poses = flash.hull_poses(irb, np.zeros(6))
+    om = oracle_mod.OracleModel.from_manipulator(irb)
+    # empty cloud: zero cost and wrenches
+    ctx.set_points(np.zeros((0, 3)))
+    cost, acc, _ = ctx.eval(poses)
+    assert cost == 0.0 and not acc.any()
+    # ragged sizes around wave/block boundaries, points exactly on vertices,
+    # hull centroids (deep inside), far field, and duplicates
+    verts = np.concatenate([s.hull.vertices @ p[:9].reshape(3, 3).T + p[9:] for s, p in zip(irb.surfaces, poses)])
+    cents = np.stack([(s.hull.vertices @ p[:9].reshape(3, 3).T + p[9:]).mean(0) for s, p in zip(irb.surfaces, poses)])
+    far = rng(5).normal(size=(50, 3)) * 1e3
+    special = np.concatenate([verts, cents, far, verts[:10]])
+    for n in (1, 2, 63, 64, 65, 255, 256, 257, 1000, len(special)):
+        pts = special[:n] if n <= len(special) else special
+        ctx.set_points(pts)
+        _, acc, (k, d, g) = ctx.eval(poses, per_point=True)
+        _check_against(om.skin(poses, pts), d, k, g, acc, om.cost_accum(poses, pts))
+
+
+def test_duplicate_hulls_first_index_wins(irb, ctx_factory):
+    from flash import Manipulator
+    s = irb.surfaces[3]
+    m = Manipulator(irb.mechanism, [s, s, s])
+    ctx = ctx_factory(m)
+    pose = np.concatenate([np.eye(3).ravel(), np.zeros(3)])
+    pts = s.hull.vertices.mean(0) + rng(6).normal(scale=0.3, size=(3000, 3))
+    d, k, _ = ctx.skin(np.stack([pose] * 3), pts)
+    assert (k == 0).all()
+
+
+def test_deterministic_and_resident(irb, ctx_factory):
+    import flash
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(irb, 7)
+    pts = synthetic.depth_cloud(irb, qt, 200000, seed=8)
+    ctx = ctx_factory(irb)
+    ctx.set_points(pts)
+    poses = flash.hull_poses(irb, qe)
+    a = ctx.eval(poses, per_point=True)
+    b = ctx.eval(poses, per_point=True)
+    assert a[0] == b[0] and np.array_equal(a[1], b[1])
+    for x, y in zip(a[2], b[2]):
+        assert np.array_equal(x, y)
+
+
+def test_full_size_properties(m64, ctx_factory):
+    """BASELINE config size (2^20 points, M64): culled == brute force bit for bit,
+    cost == Σ d², and Σ_k F_k == Σ_p 2 d ∇d (size-independent identities)."""
+    import flash
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(m64, 201)
+    pts = synthetic.depth_cloud(m64, qt, 1 << 20, seed=202)
+    poses = flash.hull_poses(m64, qe)
+    out = {}
+    for cull in (True, False):
+        ctx = ctx_factory(m64, cull=cull)
+        ctx.set_points(pts)
+        out[cull] = ctx.eval(poses, per_point=True)
+    (c1, a1, (k1, d1, g1)), (c0, a0, (k0, d0, g0)) = out[True], out[False]
+    assert np.array_equal(k1, k0) and np.array_equal(d1, d0) and np.array_equal(g1, g0)
+    assert np.array_equal(a1, a0)  # same grid, same fixed-order reduction
+    assert c1 == pytest.approx(np.dot(d1, d1), rel=1e-10)
+    F = a1[1:].reshape(-1, 6)[:, :3].sum(0)
+    assert np.allclose(F, (2 * d1[:, None] * g1).sum(0), rtol=1e-8, atol=1e-8)
+    assert np.allclose(np.linalg.norm(g1, axis=1), 1.0, atol=1e-12)
+
+
+def test_fp32_within_tolerance(m64, oracle_mod, ctx_factory):
+    """fp32 residual pass (BASELINE configs 3/5) vs the fp64 oracle."""
+    import flash
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(m64, 301)
+    pts = synthetic.depth_cloud(m64, qt, 50000, seed=302)
+    poses = flash.hull_poses(m64, qe)
+    od, ok, og = oracle_mod.OracleModel.from_manipulator(m64).skin(poses, pts)
+    ctx = ctx_factory(m64, precision=32)
+    ctx.set_points(pts)
+    cost, acc, (k, d, g) = ctx.eval(poses, per_point=True)
+    assert np.abs(d - od).max() < 2e-5
+    # k* may differ only where two hulls are within fp32 resolution of each other
+    mism = np.nonzero(k != ok)[0]
+    assert len(mism) <= 1e-3 * len(pts)
+    assert cost == pytest.approx(np.dot(od, od), rel=1e-4)
+
+
+def test_cost_functor_gradient_and_tracking(irb):
+    """CostFunctor value/gradient on the GPU vs central differences of the GPU
+    cost; estimate_state lowers the tracking cost (src/tracking.jl:8-27)."""
+    import flash
+    from flash import synthetic
+    from flash.gradientdescent import CostFunctor
+    from flash.tracking import NaiveSolver, estimate_state
+    qt, qe = synthetic.perturbed_configuration(irb, 401)
+    pts = synthetic.depth_cloud(irb, qt, 20000, seed=402)
+    cf = CostFunctor(irb, pts)
+    c, g = cf.value_and_gradient(qe)
+    h = 1e-6
+    for i in range(6):
+        xp, xm = qe.copy(), qe.copy()
+        xp[i] += h
+        xm[i] -= h
+        assert g[i] == pytest.approx((cf(xp) - cf(xm)) / (2 * h), rel=1e-5, abs=1e-6)
+    seen = []
+    x = estimate_state(irb, pts, qe, callback=lambda x, c: seen.append(c),
+                       solver=NaiveSolver(6, rate=0.5, max_step=0.05, iteration_limit=20))
+    assert seen[-1] < seen[0]
+    assert np.linalg.norm(x - qt) < np.linalg.norm(qe - qt) + 1e-9

@@ -1,0 +1,106 @@
+"""Pin the CPU oracle: independent numpy formulation, closed forms, the
+first-index tie rule, finite differences and the committed golden vectors."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, rng
+
+
+def _poses(manip, q):
+    import flash
+    return flash.hull_poses(manip, manip.mechanism.normalize(q))
+
+
+def test_oracle_matches_independent_numpy_irb140(irb, oracle_mod):
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(irb, 5)
+    pts = synthetic.depth_cloud(irb, qt, 6000, seed=6, order="shuffled")
+    om = oracle_mod.OracleModel.from_manipulator(irb)
+    poses = _poses(irb, qe)
+    d, k, g = om.skin(poses, pts, threads=1)
+    per = np.stack([oracle_mod.numpy_hull_sdf(*om.world_hull(poses, kk), pts) for kk in range(om.K)], 1)
+    assert np.abs(d - per.min(1)).max() < 1e-12
+    # k* attains the minimum; first index among (numerical) ties
+    assert np.abs(per[np.arange(len(pts)), k] - d).max() < 1e-12
+    assert (d < 0).any() and (d > 0).any()
+
+
+def test_oracle_matches_independent_numpy_m64_subset(m64, oracle_mod):
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(m64, 7)
+    pts = synthetic.depth_cloud(m64, qt, 1500, seed=8, order="shuffled")
+    om = oracle_mod.OracleModel.from_manipulator(m64)
+    poses = _poses(m64, qe)
+    d, k, _ = om.skin(poses, pts)
+    per = np.stack([oracle_mod.numpy_hull_sdf(*om.world_hull(poses, kk), pts) for kk in range(om.K)], 1)
+    assert np.abs(d - per.min(1)).max() < 1e-12
+
+
+def test_box_closed_form(oracle_mod):
+    """The table box (examples/irb_and_squishable.ipynb cell 3) is an exact box SDF."""
+    from flash import Models
+    from flash.geometry import quat_to_matrix
+    tab = Models.table()
+    r = rng(3)
+    qq = r.normal(size=4)
+    qq /= np.linalg.norm(qq)
+    R, t = quat_to_matrix(qq), np.array([0.4, -0.2, 0.6])
+    poses = np.concatenate([R.ravel(), t])[None]
+    pts = t + r.uniform(-0.5, 0.5, size=(4000, 3))
+    om = oracle_mod.OracleModel.from_manipulator(tab)
+    d, k, g = om.skin(poses, pts, threads=1)
+    loc = (pts - t) @ R  # box frame
+    qd = np.abs(loc) - np.array([0.25, 0.25, 0.05])
+    exact = np.linalg.norm(np.maximum(qd, 0), axis=1) + np.minimum(qd.max(1), 0)
+    assert np.abs(d - exact).max() < 1e-14
+    assert (k == 0).all()
+    assert np.allclose(np.linalg.norm(g, axis=1), 1.0)
+
+
+def test_first_index_wins_ties(irb, oracle_mod):
+    """Julia's left-fold `minimum` keeps the earlier surface (src/Flash.jl:267)."""
+    s = irb.surfaces[2]
+    h = (s.hull.vertices, s.hull.faces, s.hull.planes)
+    om = oracle_mod.OracleModel([h, h, h])
+    pose = np.concatenate([np.eye(3).ravel(), np.zeros(3)])
+    poses = np.stack([pose] * 3)
+    pts = s.hull.vertices.mean(0) + rng(4).normal(scale=0.2, size=(500, 3))
+    _, k, _ = om.skin(poses, pts)
+    assert (k == 0).all()
+
+
+def test_point_gradient_finite_differences(irb, oracle_mod):
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(irb, 9)
+    pts = synthetic.depth_cloud(irb, qt, 3000, seed=10, order="shuffled")
+    om = oracle_mod.OracleModel.from_manipulator(irb)
+    poses = _poses(irb, qe)
+    d, _, g = om.skin(poses, pts)
+    h = 1e-7
+    for ax in range(3):
+        e = np.zeros(3)
+        e[ax] = h
+        fd = (om.skin(poses, pts + e)[0] - om.skin(poses, pts - e)[0]) / (2 * h)
+        err = np.abs(fd - g[:, ax])
+        assert np.median(err) < 1e-8 and np.percentile(err, 99) < 1e-6
+    assert np.allclose(np.linalg.norm(g, axis=1), 1.0, atol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["c1_irb140", "m64_2k", "table_quat"])
+def test_oracle_reproduces_golden(name, oracle_mod):
+    from flash import Models
+    manip = {"c1_irb140": Models.irb140, "m64_2k": Models.arm_grid, "table_quat": Models.table}[name]()
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    import flash
+    poses = flash.hull_poses(manip, manip.mechanism.normalize(z["q"]))
+    assert np.array_equal(poses, z["poses"])
+    om = oracle_mod.OracleModel.from_manipulator(manip)
+    d, k, g = om.skin(poses, z["points"])
+    assert np.array_equal(k, z["kstar"])
+    assert np.array_equal(d, z["d"])
+    assert np.array_equal(g, z["grad"])
+    acc = om.cost_accum(poses, z["points"])
+    assert np.allclose(acc, z["accum"], rtol=1e-13, atol=1e-13)
+    assert acc[0] == pytest.approx(np.dot(d, d), rel=1e-12)

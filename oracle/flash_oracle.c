@@ -136,7 +136,10 @@ static void closest_on_triangle(const double* p, const double* v, double* q) {
 }
 
 /* Signed distance of p to one posed hull (faces [f0, f1)), with its unit
- * gradient. Restates ConvexSurface(x) (src/Flash.jl:238-243). */
+ * gradient. Restates ConvexSurface(x) (src/Flash.jl:238-243). The closest-
+ * feature scan visits only faces visible from p whose plane distance is below
+ * the best distance so far (neither can change the minimum, and the kernel
+ * prunes identically). */
 void oracle_hull_sdf(const double* p, int32_t f0, int32_t f1, const double* planes_w, const double* facex_w,
                      double* d, double* g) {
   double hmax = -INFINITY;
@@ -159,7 +162,7 @@ void oracle_hull_sdf(const double* p, int32_t f0, int32_t f1, const double* plan
   for (int f = f0; f < f1; ++f) {
     const double* pl = planes_w + 4 * f;
     const double h = fma(pl[0], p[0], fma(pl[1], p[1], fma(pl[2], p[2], -pl[3])));
-    if (h > 0) {
+    if (h > 0 && h * h < best2) {
       double q[3];
       closest_on_triangle(p, facex_w + FX * f + 12, q);
       const double dx = p[0] - q[0], dy = p[1] - q[1], dz = p[2] - q[2];
@@ -167,11 +170,15 @@ void oracle_hull_sdf(const double* p, int32_t f0, int32_t f1, const double* plan
       if (dist2 < best2) { best2 = dist2; qb[0] = q[0]; qb[1] = q[1]; qb[2] = q[2]; }
     }
   }
-  *d = sqrt(best2);
-  const double inv = 1.0 / *d;
-  g[0] = (p[0] - qb[0]) * inv;
-  g[1] = (p[1] - qb[1]) * inv;
-  g[2] = (p[2] - qb[2]) * inv;
+  if (best2 > 0) {
+    *d = sqrt(best2);
+    const double inv = 1.0 / *d;
+    g[0] = (p[0] - qb[0]) * inv;
+    g[1] = (p[1] - qb[1]) * inv;
+    g[2] = (p[2] - qb[2]) * inv;
+  } else {
+    *d = 0.0; /* p on the boundary: subgradient = normal of the max face */
+  }
 }
 
 /* Scene SDF: brute-force minimum over ALL surfaces in index order, strict <,

@@ -84,6 +84,8 @@ struct fsdf_ctx {
   bool profiling = false;
   std::vector<hipEvent_t> prof_ev;  // pairs
   size_t prof_used = 0;             // events recorded (2 per pass)
+  unsigned long long* d_stats = nullptr;  // fsdf_kernel_stats
+  bool stats_on = false;
 };
 
 static int fail(fsdf_ctx* c, int code, const char* fmt, ...) {
@@ -162,6 +164,7 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   dfree(c->d_grad);
   dfree(c->d_q);
   dfree(c->d_q64);
+  dfree(c->d_stats);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (int i = 0; i < kPoseRing; ++i) {
     if (c->pose_ev[i]) (void)hipEventDestroy(c->pose_ev[i]);
@@ -396,6 +399,7 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
   out.d = d_d;
   out.grad = d_grad;
   out.perm = d_perm;
+  out.stats = c->stats_on ? c->d_stats : nullptr;
   if (n > 0) {
     const bool prof = c->profiling && c->prof_used + 2 <= c->prof_ev.size();
     if (prof) HIPCHECK(c, hipEventRecord(c->prof_ev[c->prof_used], c->stream));
@@ -529,5 +533,20 @@ extern "C" int fsdf_pass_time(fsdf_ctx* c, double* total_ms, int64_t* launches) 
   *total_ms = t;
   *launches = (int64_t)(c->prof_used / 2);
   c->prof_used = 0;
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_kernel_stats(fsdf_ctx* c, int32_t enable, uint64_t* counters) {
+  if (!c) return FSDF_ERR_ARG;
+  HIPCHECK(c, hipSetDevice(c->device));
+  if (!c->d_stats) HIPCHECK(c, hipMalloc(&c->d_stats, 8 * sizeof(unsigned long long)));
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  if (enable) {
+    HIPCHECK(c, hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long)));
+    c->stats_on = true;
+    return FSDF_OK;
+  }
+  c->stats_on = false;
+  if (counters) HIPCHECK(c, hipMemcpy(counters, c->d_stats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return FSDF_OK;
 }

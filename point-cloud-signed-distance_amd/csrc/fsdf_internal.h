@@ -49,6 +49,7 @@ struct PassOutputs {
   double* d = nullptr;         // optional
   double* grad = nullptr;      // optional [n][3]
   const int64_t* perm = nullptr;  // optional: resident index -> caller index
+  unsigned long long* stats = nullptr;  // optional kernel counters (fsdf_debug_stats)
 };
 
 // precision: 64 or 32. Points are AoS of the matching precision.

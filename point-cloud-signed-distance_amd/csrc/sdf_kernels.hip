@@ -181,10 +181,12 @@ __device__ __forceinline__ void closest_on_triangle(T px, T py, T pz, const T* _
 template <typename T>
 __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int f0, int f1, const T* __restrict__ planes,
                                          const T* __restrict__ facex, bool active, T& d, T& gx, T& gy,
-                                         T& gz) {
+                                         T& gz, unsigned long long* __restrict__ stats) {
   T hmax = -tinf<T>();
   int fs = f0;
-#pragma unroll 4
+  // 8 planes per trip: the wave-uniform plane rows arrive by scalar loads
+  // (s_load_dwordx8), issued a whole trip ahead of the VALU that consumes them.
+#pragma unroll 8
   for (int f = f0; f < f1; ++f) {
     const T* pl = planes + 4 * f;
     const T h = mfma_(pl[0], px, mfma_(pl[1], py, mfma_(pl[2], pz, -pl[3])));
@@ -204,15 +206,21 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int f0, int f1, const
     slow = !(s0 >= (T)0 && s1 >= (T)0 && s2 >= (T)0);
   }
   slow = slow && active;
-  if (__any(slow)) {
+  const uint64_t slow_mask = __ballot(slow);
+  if (slow_mask) {
+    if (stats && (threadIdx.x & 63) == 0) {
+      atomicAdd(stats + 2, 1ull);
+      atomicAdd(stats + 4, (unsigned long long)__builtin_popcountll(slow_mask));
+    }
     // Closest feature over the faces visible from p (h_f > 0): the closest
-    // boundary point of a convex polytope lies on one of them.
+    // boundary point of a convex polytope lies on one of them; a face whose
+    // plane distance already exceeds the best distance cannot improve it.
     T best2 = tinf<T>();
     T qbx = (T)0, qby = (T)0, qbz = (T)0;
     for (int f = f0; f < f1; ++f) {
       const T* pl = planes + 4 * f;
       const T h = mfma_(pl[0], px, mfma_(pl[1], py, mfma_(pl[2], pz, -pl[3])));
-      if (slow && h > (T)0) {
+      if (slow && h > (T)0 && h * h < best2) {
         T qx, qy, qz;
         closest_on_triangle(px, py, pz, facex + kFaceX * f + 12, qx, qy, qz);
         const T dx = px - qx, dy = py - qy, dz = pz - qz;
@@ -221,9 +229,14 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int f0, int f1, const
       }
     }
     if (slow) {
-      d = tsqrt(best2);
-      const T inv = (T)1 / d;
-      gx = (px - qbx) * inv; gy = (py - qby) * inv; gz = (pz - qbz) * inv;
+      if (best2 > (T)0) {
+        d = tsqrt(best2);
+        const T inv = (T)1 / d;
+        gx = (px - qbx) * inv; gy = (py - qby) * inv; gz = (pz - qbz) * inv;
+      } else {
+        // p on the boundary (a vertex/edge): d = 0, subgradient = face normal
+        d = (T)0;
+      }
     }
   }
 }
@@ -259,7 +272,11 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(const T* __restrict__ pts,
     const int64_t ii = valid ? i : n - 1;
     const T px = pts[3 * ii + 0], py = pts[3 * ii + 1], pz = pts[3 * ii + 2];
 
-    float ub = __builtin_huge_valf();
+    // Phase A (fp32, exact-safe): per hull lower bound lb_k = |p-c_k| - r_k
+    // (sphere around the hull), upper bound ub = min_k |p-c_k| (c_k is inside
+    // its hull), and the best-first seed hull argmin_k lb_k.
+    float ub = __builtin_huge_valf(), lbmin = __builtin_huge_valf();
+    int kseed = 0;
     float pxf = 0.f, pyf = 0.f, pzf = 0.f, pmag = 0.f;
     if (CULL) {
       pxf = (float)px; pyf = (float)py; pzf = (float)pz;
@@ -267,32 +284,74 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(const T* __restrict__ pts,
       for (int k = 0; k < K; ++k) {
         const float* sp = spheres + 4 * k;
         const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
-        ub = fminf(ub, __builtin_sqrtf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz))));
+        const float dist = __builtin_sqrtf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)));
+        ub = fminf(ub, dist);
+        const float lb = dist - sp[3];
+        if (lb < lbmin) { lbmin = lb; kseed = k; }
       }
     }
 
     T best = tinf<T>();
-    int bk = 0;
+    int bk = 0x7fffffff;
     T gx = (T)0, gy = (T)0, gz = (T)0;
-    for (int k = 0; k < K; ++k) {
-      bool need = valid;
-      if (CULL) {
-        const float* sp = spheres + 4 * k;
-        const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
-        const float dist = __builtin_sqrtf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)));
-        const float lb = dist - sp[3];
-        const float bf = fminf(ub, (float)best);
-        const float mrg = 1e-5f * (1.0f + pmag + fabsf(sp[0]) + fabsf(sp[1]) + fabsf(sp[2]) + sp[3] + dist +
-                                   fabsf(bf));
-        need = valid && (lb <= bf + mrg);
-      }
-      if (!__any(need)) continue;
+    // hull k is needed by a lane unless its lower bound exceeds min(ub, best)
+    // by more than the fp32 rounding margin
+    auto needs = [&](int k) -> bool {
+      if (!CULL) return valid;
+      const float* sp = spheres + 4 * k;
+      const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
+      const float dist = __builtin_sqrtf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)));
+      const float lb = dist - sp[3];
+      const float bf = fminf(ub, (float)best);
+      const float mrg =
+          1e-5f * (1.0f + pmag + fabsf(sp[0]) + fabsf(sp[1]) + fabsf(sp[2]) + sp[3] + dist + fabsf(bf));
+      return valid && (lb <= bf + mrg);
+    };
+    // evaluations may run out of index order: ties keep the smaller k
+    auto evaluate = [&](int k, bool need) {
       const int f0 = __builtin_amdgcn_readfirstlane(face_off[k]);
       const int f1 = __builtin_amdgcn_readfirstlane(face_off[k + 1]);
       T dk, hx, hy, hz;
-      hull_sdf<T>(px, py, pz, f0, f1, planes, facex, need, dk, hx, hy, hz);
-      if (need && dk < best) { best = dk; bk = k; gx = hx; gy = hy; gz = hz; }
+      hull_sdf<T>(px, py, pz, f0, f1, planes, facex, need, dk, hx, hy, hz, out.stats);
+      if (out.stats) {
+        const uint64_t nm = __ballot(need);
+        if (lane == 0) {
+          atomicAdd(out.stats + 1, 1ull);
+          atomicAdd(out.stats + 3, (unsigned long long)__builtin_popcountll(nm));
+        }
+      }
+      if (need && (dk < best || (dk == best && k < bk))) { best = dk; bk = k; gx = hx; gy = hy; gz = hz; }
+    };
+    uint64_t done[SLOTS];
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) done[s] = 0;
+    if (CULL) {
+      // Phase B: each lane's seed hull first (one evaluation per distinct seed
+      // in the wave) so that `best` is tight before the sweep.
+      uint64_t pend = __ballot(valid);
+      while (pend) {
+        const int kk = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(pend), 64));
+        pend &= ~__ballot(valid && kseed == kk);
+        evaluate(kk, needs(kk));
+#pragma unroll
+        for (int s = 0; s < SLOTS; ++s)
+          if ((kk >> 6) == s) done[s] |= 1ull << (kk & 63);
+        if (out.stats && lane == 0) atomicAdd(out.stats + 5, 1ull);
+      }
     }
+    // Phase C: sweep the remaining hulls in index order.
+    for (int k = 0; k < K; ++k) {
+      bool skip = false;
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s)
+        if ((k >> 6) == s) skip = (done[s] >> (k & 63)) & 1ull;
+      if (skip) continue;
+      const bool need = needs(k);
+      if (!__any(need)) continue;
+      evaluate(k, need);
+    }
+    if (out.stats && lane == 0) atomicAdd(out.stats + 0, 1ull);
+    if (!valid) bk = 0;
 
     // contributions: c += d^2; F_k += 2 d g; M_k += 2 d (p x g)
     double cF[3] = {0.0, 0.0, 0.0}, cM[3] = {0.0, 0.0, 0.0};

@@ -57,6 +57,7 @@ _PROTOS = {
     "fsdf_synchronize": (c_int32, [c_void_p]),
     "fsdf_profile_pass": (c_int32, [c_void_p, c_int32]),
     "fsdf_pass_time": (c_int32, [c_void_p, POINTER(c_double), POINTER(c_int64)]),
+    "fsdf_kernel_stats": (c_int32, [c_void_p, c_int32, c_void_p]),
 }
 SYMBOLS = tuple(_PROTOS)
 
@@ -211,3 +212,11 @@ class Context:
         ms, n = c_double(0.0), c_int64(0)
         check(self._lib.fsdf_pass_time(self._ctx, ctypes.byref(ms), ctypes.byref(n)), self._ctx, "pass_time")
         return ms.value, n.value
+
+    STAT_NAMES = ("wave_iters", "hull_evals", "scans", "lane_needs", "scan_lanes", "seed_evals")
+
+    def kernel_stats(self, enable: bool):
+        """enable=True: start counting; enable=False: stop, return the counters."""
+        out = np.zeros(8, np.uint64)
+        check(self._lib.fsdf_kernel_stats(self._ctx, int(enable), ptr(out)), self._ctx, "kernel_stats")
+        return None if enable else dict(zip(self.STAT_NAMES, (int(v) for v in out[:6])))

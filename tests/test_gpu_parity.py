@@ -97,6 +97,7 @@ def test_edge_cases(irb, oracle_mod, ctx_factory):
     cents = np.stack([(s.hull.vertices @ p[:9].reshape(3, 3).T + p[9:]).mean(0) for s, p in zip(irb.surfaces, poses)])
     far = rng(5).normal(size=(50, 3)) * 1e3
     special = np.concatenate([verts, cents, far, verts[:10]])
+    assert np.isfinite(special).all()
     for n in (1, 2, 63, 64, 65, 255, 256, 257, 1000, len(special)):
         pts = special[:n] if n <= len(special) else special
         ctx.set_points(pts)

@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Pass-kernel diagnostics on the GPU: mean kernel time (HIP events) and the
+kernel work counters (fsdf_kernel_stats) for M64 at 2^20 points, across
+cloud orders, culling and precision. One process, variants interleaved.
+
+    python tools/profile_pass.py [--points N] [--reps R] [--json out.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "point-cloud-signed-distance_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--points", type=int, default=1 << 20)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--variants", default="all")
+    args = ap.parse_args()
+    import flash
+    from flash import Models, synthetic, _lib
+
+    m = Models.arm_grid()
+    qt, qe = synthetic.perturbed_configuration(m, 1234)
+    poses = flash.hull_poses(m, qe)
+    clouds = {o: synthetic.depth_cloud(m, qt, args.points, seed=1234 + 17, order=o) for o in ("raster", "shuffled")}
+    hulls = [(s.hull.vertices, s.hull.faces, s.hull.planes) for s in m.surfaces]
+    variants = [("raster", True, 64), ("shuffled", True, 64), ("raster", False, 64), ("raster", True, 32)]
+    if args.variants != "all":
+        variants = [v for v in variants if f"{v[0]}-{int(v[1])}-{v[2]}" in args.variants.split(",")]
+    ctxs = {}
+    for order, cull, prec in variants:
+        c = _lib.Context(device=0, precision=prec, cull=cull)
+        c.set_model(hulls)
+        c.set_points(clouds[order])
+        c.eval(poses)  # warm
+        ctxs[(order, cull, prec)] = c
+    times = {v: [] for v in variants}
+    for _ in range(args.rounds):
+        for v in variants:
+            c = ctxs[v]
+            c.profile_pass(True)
+            for _ in range(args.reps):
+                c.eval(poses)
+            ms, n = c.pass_time()
+            times[v].append(ms / n)
+    res = []
+    for v in variants:
+        c = ctxs[v]
+        c.kernel_stats(True)
+        c.eval(poses)
+        st = c.kernel_stats(False)
+        w = st["wave_iters"]
+        ms = float(np.median(times[v]))
+        row = {"order": v[0], "cull": v[1], "precision": v[2], "pass_ms_median": ms,
+               "pass_ms_min": float(np.min(times[v])), "Mevals_per_s": args.points / ms / 1e3,
+               "hull_evals_per_wave": st["hull_evals"] / w, "seed_evals_per_wave": st["seed_evals"] / w,
+               "scans_per_wave": st["scans"] / w, "lane_need_frac": st["lane_needs"] / max(st["hull_evals"] * 64, 1),
+               "scan_lane_frac": st["scan_lanes"] / max(st["scans"] * 64, 1), **st}
+        res.append(row)
+        print(json.dumps(row), flush=True)
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -56,10 +56,13 @@ static inline void cross3(const double* a, const double* b, double* o) {
 }
 static inline double dot3(const double* a, const double* b) { return fma(a[0], b[0], fma(a[1], b[1], a[2] * b[2])); }
 
-/* World-frame planes and per-face records for every hull (src/Flash.jl:248:
- * the surface pose is transform_to_root of the geometry frame). */
-void oracle_pose_model(int32_t F, const double* verts_l, const int32_t* faces, const double* planes_l,
-                       const int32_t* face_hull, const double* poses, double* planes_w, double* facex_w) {
+/* World-frame planes, per-face records, vertices and certificate scales for
+ * every hull (src/Flash.jl:248: the surface pose is transform_to_root of the
+ * geometry frame). Same formulas as pose_kernel. */
+void oracle_pose_model(int32_t F, int32_t V, int32_t K, const double* verts_l, const int32_t* faces,
+                       const double* planes_l, const int32_t* face_hull, const int32_t* vert_hull,
+                       const int32_t* vert_off, const double* poses, double* planes_w, double* facex_w,
+                       double* verts_w, double* hscale) {
   for (int f = 0; f < F; ++f) {
     const double* P = poses + 12 * face_hull[f];
     const double* pl = planes_l + 4 * f;
@@ -88,7 +91,34 @@ void oracle_pose_model(int32_t F, const double* verts_l, const int32_t* faces, c
     fx[18] = c[0]; fx[19] = c[1]; fx[20] = c[2];
     fx[21] = 0; fx[22] = 0; fx[23] = 0;
   }
+  for (int v = 0; v < V; ++v) {
+    double* o = verts_w + 4 * v;
+    xf_point(poses + 12 * vert_hull[v], verts_l + 3 * v, o);
+    o[3] = 0;
+  }
+  for (int k = 0; k < K; ++k) {
+    double sc = 0;
+    for (int v = vert_off[k]; v < vert_off[k + 1]; ++v) {
+      double w[3];
+      xf_point(poses + 12 * k, verts_l + 3 * v, w);
+      const double l1 = fabs(w[0]) + fabs(w[1]) + fabs(w[2]);
+      sc = l1 > sc ? l1 : sc;
+    }
+    hscale[k] = sc;
+  }
 }
+
+/* The posed model as the kernel sees it. */
+typedef struct {
+  int32_t K;
+  const int32_t* face_off;
+  const int32_t* vert_off;
+  const int32_t* nbr;
+  const double* planes_w;
+  const double* facex_w;
+  const double* verts_w;
+  const double* hscale;
+} oracle_posed;
 
 /* Closest point on triangle v = (a, b, c) to p, Voronoi-region walk. */
 static void closest_on_triangle(const double* p, const double* v, double* q) {
@@ -135,47 +165,90 @@ static void closest_on_triangle(const double* p, const double* v, double* q) {
   q[2] = fma(ww, acz, fma(vv, abz, az));
 }
 
-/* Signed distance of p to one posed hull (faces [f0, f1)), with its unit
- * gradient. Restates ConvexSurface(x) (src/Flash.jl:238-243). The closest-
- * feature scan visits only faces visible from p whose plane distance is below
- * the best distance so far (neither can change the minimum, and the kernel
- * prunes identically). */
-void oracle_hull_sdf(const double* p, int32_t f0, int32_t f1, const double* planes_w, const double* facex_w,
-                     double* d, double* g) {
+static inline double plane_value(const double* pl, const double* p) {
+  return fma(pl[0], p[0], fma(pl[1], p[1], fma(pl[2], p[2], -pl[3])));
+}
+
+static inline double dist2_to(const double* p, const double* q) {
+  const double dx = p[0] - q[0], dy = p[1] - q[1], dz = p[2] - q[2];
+  return fma(dx, dx, fma(dy, dy, dz * dz));
+}
+
+/* GJK's termination test as an optimality certificate: q is the closest point
+ * of conv(V) to p iff max_v (p-q)·v <= (p-q)·q (within rounding tolerance). */
+static int certified(const double* p, const double* q, int v0, int v1, const double* verts, double scale) {
+  const double wx = p[0] - q[0], wy = p[1] - q[1], wz = p[2] - q[2];
+  const double wq = fma(wx, q[0], fma(wy, q[1], wz * q[2]));
+  double smax = -INFINITY;
+  for (int v = v0; v < v1; ++v) {
+    const double* vv = verts + 4 * v;
+    const double sv = fma(vv[0], wx, fma(vv[1], wy, vv[2] * wz));
+    smax = sv > smax ? sv : smax;
+  }
+  const double tol = 1e-13 * ((fabs(wx) + fabs(wy)) + fabs(wz)) * scale;
+  return smax <= wq + tol;
+}
+
+/* Signed distance of p to posed hull k, with its unit gradient. Restates
+ * ConvexSurface(x) (src/Flash.jl:238-243) as the exact polytope SDF:
+ *   inside / on the surface: max_f h_f (first max face's normal);
+ *   outside: h_{f*} when p projects into triangle f*; else the closest point on
+ *   triangle f*, then on its neighbours across violated edges, each candidate
+ *   certified by the support test; uncertified -> exhaustive scan of the
+ *   visible faces whose plane distance is below the best so far. */
+void oracle_hull_sdf(const oracle_posed* m, int32_t k, const double* p, double* d, double* g) {
+  const int f0 = m->face_off[k], f1 = m->face_off[k + 1];
   double hmax = -INFINITY;
   int fs = f0;
   for (int f = f0; f < f1; ++f) {
-    const double* pl = planes_w + 4 * f;
-    const double h = fma(pl[0], p[0], fma(pl[1], p[1], fma(pl[2], p[2], -pl[3])));
+    const double h = plane_value(m->planes_w + 4 * f, p);
     if (h > hmax) { hmax = h; fs = f; }
   }
-  const double* pls = planes_w + 4 * fs;
+  const double* pls = m->planes_w + 4 * fs;
   *d = hmax;
   g[0] = pls[0]; g[1] = pls[1]; g[2] = pls[2];
   if (!(hmax > 0)) return;
-  const double* fx = facex_w + FX * fs;
-  const double s0 = fma(fx[0], p[0], fma(fx[1], p[1], fma(fx[2], p[2], -fx[3])));
-  const double s1 = fma(fx[4], p[0], fma(fx[5], p[1], fma(fx[6], p[2], -fx[7])));
-  const double s2 = fma(fx[8], p[0], fma(fx[9], p[1], fma(fx[10], p[2], -fx[11])));
-  if (s0 >= 0 && s1 >= 0 && s2 >= 0) return;
-  double best2 = INFINITY, qb[3] = {0, 0, 0};
-  for (int f = f0; f < f1; ++f) {
-    const double* pl = planes_w + 4 * f;
-    const double h = fma(pl[0], p[0], fma(pl[1], p[1], fma(pl[2], p[2], -pl[3])));
-    if (h > 0 && h * h < best2) {
-      double q[3];
-      closest_on_triangle(p, facex_w + FX * f + 12, q);
-      const double dx = p[0] - q[0], dy = p[1] - q[1], dz = p[2] - q[2];
-      const double dist2 = fma(dx, dx, fma(dy, dy, dz * dz));
-      if (dist2 < best2) { best2 = dist2; qb[0] = q[0]; qb[1] = q[1]; qb[2] = q[2]; }
+  const double* fx = m->facex_w + FX * fs;
+  const double s[3] = {fma(fx[0], p[0], fma(fx[1], p[1], fma(fx[2], p[2], -fx[3]))),
+                       fma(fx[4], p[0], fma(fx[5], p[1], fma(fx[6], p[2], -fx[7]))),
+                       fma(fx[8], p[0], fma(fx[9], p[1], fma(fx[10], p[2], -fx[11])))};
+  if (s[0] >= 0 && s[1] >= 0 && s[2] >= 0) return;
+  const int v0 = m->vert_off[k], v1 = m->vert_off[k + 1];
+  const double scale = m->hscale[k];
+  double q[3];
+  closest_on_triangle(p, fx + 12, q);
+  double best2 = dist2_to(p, q);
+  if (!certified(p, q, v0, v1, m->verts_w, scale)) {
+    for (int e = 0; e < 3; ++e) {
+      if (s[e] < 0) {
+        const int gf = m->nbr[3 * fs + e];
+        double c[3];
+        closest_on_triangle(p, m->facex_w + FX * gf + 12, c);
+        const double d2 = dist2_to(p, c);
+        if (d2 < best2) { best2 = d2; q[0] = c[0]; q[1] = c[1]; q[2] = c[2]; }
+      }
+    }
+    if (!certified(p, q, v0, v1, m->verts_w, scale)) {
+      double b2 = INFINITY, b[3] = {0, 0, 0};
+      for (int f = f0; f < f1; ++f) {
+        const double h = plane_value(m->planes_w + 4 * f, p);
+        if (h > 0 && h * h < b2) {
+          double c[3];
+          closest_on_triangle(p, m->facex_w + FX * f + 12, c);
+          const double d2 = dist2_to(p, c);
+          if (d2 < b2) { b2 = d2; b[0] = c[0]; b[1] = c[1]; b[2] = c[2]; }
+        }
+      }
+      best2 = b2;
+      q[0] = b[0]; q[1] = b[1]; q[2] = b[2];
     }
   }
   if (best2 > 0) {
     *d = sqrt(best2);
     const double inv = 1.0 / *d;
-    g[0] = (p[0] - qb[0]) * inv;
-    g[1] = (p[1] - qb[1]) * inv;
-    g[2] = (p[2] - qb[2]) * inv;
+    g[0] = (p[0] - q[0]) * inv;
+    g[1] = (p[1] - q[1]) * inv;
+    g[2] = (p[2] - q[2]) * inv;
   } else {
     *d = 0.0; /* p on the boundary: subgradient = normal of the max face */
   }
@@ -183,13 +256,12 @@ void oracle_hull_sdf(const double* p, int32_t f0, int32_t f1, const double* plan
 
 /* Scene SDF: brute-force minimum over ALL surfaces in index order, strict <,
  * i.e. exactly the reference's `minimum(s(x) for s in all_surfaces)`. */
-static void skin_one(const double* p, int32_t K, const int32_t* face_off, const double* planes_w,
-                     const double* facex_w, double* d, int32_t* k, double* g) {
+static void skin_one(const oracle_posed* m, const double* p, double* d, int32_t* k, double* g) {
   double best = INFINITY, gb[3] = {0, 0, 0};
   int32_t bk = 0;
-  for (int32_t kk = 0; kk < K; ++kk) {
+  for (int32_t kk = 0; kk < m->K; ++kk) {
     double dk, gk[3];
-    oracle_hull_sdf(p, face_off[kk], face_off[kk + 1], planes_w, facex_w, &dk, gk);
+    oracle_hull_sdf(m, kk, p, &dk, gk);
     if (dk < best) { best = dk; bk = kk; gb[0] = gk[0]; gb[1] = gk[1]; gb[2] = gk[2]; }
   }
   *d = best;
@@ -198,8 +270,8 @@ static void skin_one(const double* p, int32_t K, const int32_t* face_off, const 
 }
 
 /* Per-point skin over a cloud. Any output may be NULL. threads <= 0: all. */
-void oracle_skin(const double* pts, int64_t n, int32_t K, const int32_t* face_off, const double* planes_w,
-                 const double* facex_w, double* d_out, int32_t* k_out, double* g_out, int32_t threads) {
+void oracle_skin(const oracle_posed* m, const double* pts, int64_t n, double* d_out, int32_t* k_out,
+                 double* g_out, int32_t threads) {
 #ifdef _OPENMP
   if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(dynamic, 256)
@@ -207,7 +279,7 @@ void oracle_skin(const double* pts, int64_t n, int32_t K, const int32_t* face_of
   for (int64_t i = 0; i < n; ++i) {
     double d, g[3];
     int32_t k;
-    skin_one(pts + 3 * i, K, face_off, planes_w, facex_w, &d, &k, g);
+    skin_one(m, pts + 3 * i, &d, &k, g);
     if (d_out) d_out[i] = d;
     if (k_out) k_out[i] = k;
     if (g_out) { g_out[3 * i] = g[0]; g_out[3 * i + 1] = g[1]; g_out[3 * i + 2] = g[2]; }
@@ -218,15 +290,14 @@ void oracle_skin(const double* pts, int64_t n, int32_t K, const int32_t* face_of
 /* cost = Σ d*² and the per-hull wrench sums (layout of include/flashsdf.h):
  * accum[0] = Σ d², accum[1+6k..] = Σ 2d∇d, Σ 2d (p×∇d) over points with k*=k.
  * Serial in point order (the reference's `sum` is pairwise; both agree to
- * rounding, compared at 1e-6 relative). */
-void oracle_cost_accum(const double* pts, int64_t n, int32_t K, const int32_t* face_off, const double* planes_w,
-                       const double* facex_w, double* accum) {
-  memset(accum, 0, sizeof(double) * (size_t)(1 + 6 * K));
+ * rounding, compared at 1e-9 relative). */
+void oracle_cost_accum(const oracle_posed* m, const double* pts, int64_t n, double* accum) {
+  memset(accum, 0, sizeof(double) * (size_t)(1 + 6 * m->K));
   for (int64_t i = 0; i < n; ++i) {
     const double* p = pts + 3 * i;
     double d, g[3];
     int32_t k;
-    skin_one(p, K, face_off, planes_w, facex_w, &d, &k, g);
+    skin_one(m, p, &d, &k, g);
     accum[0] = fma(d, d, accum[0]);
     const double w = 2.0 * d;
     double* a = accum + 1 + 6 * k;

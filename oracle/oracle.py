@@ -32,17 +32,21 @@ def build():
     subprocess.run(["make", "-C", HERE], check=True, stdout=subprocess.DEVNULL)
 
 
+class Posed(ctypes.Structure):
+    _fields_ = [("K", c_int32), ("face_off", c_void_p), ("vert_off", c_void_p), ("nbr", c_void_p),
+                ("planes_w", c_void_p), ("facex_w", c_void_p), ("verts_w", c_void_p), ("hscale", c_void_p)]
+
+
 def load():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB):
             build()
         lib = ctypes.CDLL(LIB)
-        lib.oracle_pose_model.argtypes = [c_int32] + [c_void_p] * 7
-        lib.oracle_hull_sdf.argtypes = [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]
-        lib.oracle_skin.argtypes = [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                    c_void_p, c_int32]
-        lib.oracle_cost_accum.argtypes = [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]
+        lib.oracle_pose_model.argtypes = [c_int32, c_int32, c_int32] + [c_void_p] * 11
+        lib.oracle_hull_sdf.argtypes = [ctypes.POINTER(Posed), c_int32, c_void_p, c_void_p, c_void_p]
+        lib.oracle_skin.argtypes = [ctypes.POINTER(Posed), c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int32]
+        lib.oracle_cost_accum.argtypes = [ctypes.POINTER(Posed), c_void_p, c_int64, c_void_p]
         lib.oracle_max_threads.restype = c_int32
         _lib = lib
     return _lib
@@ -52,25 +56,45 @@ def _p(a):
     return None if a is None else c_void_p(a.ctypes.data)
 
 
+def face_neighbours(faces, fbase):
+    """Face across edge i (v_i -> v_{i+1}) of every face (global ids), like fsdf_set_model."""
+    owner = {}
+    for f, (a, b, c) in enumerate(faces):
+        for e, (u, v) in enumerate(((a, b), (b, c), (c, a))):
+            owner[(int(u), int(v))] = f
+    nb = np.empty((len(faces), 3), np.int32)
+    for f, (a, b, c) in enumerate(faces):
+        for e, (u, v) in enumerate(((a, b), (b, c), (c, a))):
+            nb[f, e] = fbase + owner.get((int(v), int(u)), f)
+    return nb
+
+
 class OracleModel:
     def __init__(self, hulls):
         """hulls: list of (vertices, faces, planes) in local frames."""
-        V, Fc, P, FH, off = [], [], [], [], [0]
+        V, Fc, P, FH, VH, NB, off, voff = [], [], [], [], [], [], [0], [0]
         vbase = 0
         for k, (v, f, p) in enumerate(hulls):
             V.append(np.asarray(v, np.float64))
             Fc.append(np.asarray(f, np.int32) + vbase)
             P.append(np.asarray(p, np.float64))
             FH.append(np.full(len(f), k, np.int32))
+            VH.append(np.full(len(v), k, np.int32))
+            NB.append(face_neighbours(np.asarray(f), off[-1]))
             off.append(off[-1] + len(f))
+            voff.append(voff[-1] + len(v))
             vbase += len(v)
         self.K = len(hulls)
         self.verts_l = np.ascontiguousarray(np.concatenate(V))
         self.faces = np.ascontiguousarray(np.concatenate(Fc))
         self.planes_l = np.ascontiguousarray(np.concatenate(P))
         self.face_hull = np.ascontiguousarray(np.concatenate(FH))
+        self.vert_hull = np.ascontiguousarray(np.concatenate(VH))
+        self.nbr = np.ascontiguousarray(np.concatenate(NB))
         self.face_off = np.asarray(off, np.int32)
+        self.vert_off = np.asarray(voff, np.int32)
         self.F = len(self.face_hull)
+        self.V = len(self.vert_hull)
         self.hulls = hulls
 
     @staticmethod
@@ -78,28 +102,35 @@ class OracleModel:
         return OracleModel([(s.hull.vertices, s.hull.faces, s.hull.planes) for s in manip.convex_surfaces()])
 
     def pose(self, poses):
+        """World-frame model arrays for `poses` ([K,12])."""
         poses = np.ascontiguousarray(poses, np.float64).reshape(self.K, 12)
         pw = np.empty((self.F, 4))
         fx = np.empty((self.F, FX))
-        load().oracle_pose_model(self.F, _p(self.verts_l), _p(self.faces), _p(self.planes_l), _p(self.face_hull),
-                                 _p(poses), _p(pw), _p(fx))
-        return pw, fx
+        vw = np.empty((self.V, 4))
+        hs = np.empty(self.K)
+        load().oracle_pose_model(self.F, self.V, self.K, _p(self.verts_l), _p(self.faces), _p(self.planes_l),
+                                 _p(self.face_hull), _p(self.vert_hull), _p(self.vert_off), _p(poses), _p(pw),
+                                 _p(fx), _p(vw), _p(hs))
+        arrays = (pw, fx, vw, hs)
+        st = Posed(self.K, self.face_off.ctypes.data, self.vert_off.ctypes.data, self.nbr.ctypes.data,
+                   pw.ctypes.data, fx.ctypes.data, vw.ctypes.data, hs.ctypes.data)
+        return st, arrays
 
     def skin(self, poses, pts, threads: int = 0):
         pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
-        pw, fx = self.pose(poses)
+        st, _keep = self.pose(poses)
         n = len(pts)
         d = np.empty(n)
         k = np.empty(n, np.int32)
         g = np.empty((n, 3))
-        load().oracle_skin(_p(pts), n, self.K, _p(self.face_off), _p(pw), _p(fx), _p(d), _p(k), _p(g), threads)
+        load().oracle_skin(ctypes.byref(st), _p(pts), n, _p(d), _p(k), _p(g), threads)
         return d, k, g
 
     def cost_accum(self, poses, pts):
         pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
-        pw, fx = self.pose(poses)
+        st, _keep = self.pose(poses)
         acc = np.empty(1 + 6 * self.K)
-        load().oracle_cost_accum(_p(pts), len(pts), self.K, _p(self.face_off), _p(pw), _p(fx), _p(acc))
+        load().oracle_cost_accum(ctypes.byref(st), _p(pts), len(pts), _p(acc))
         return acc
 
     def world_hull(self, poses, k):

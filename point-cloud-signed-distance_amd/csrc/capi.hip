@@ -14,6 +14,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -55,6 +57,9 @@ struct fsdf_ctx {
   int32_t* d_face_hull = nullptr;
   double* d_sphere_l = nullptr;
   int32_t* d_face_off = nullptr;
+  int32_t* d_vert_hull = nullptr;
+  int32_t* d_vert_off = nullptr;
+  int32_t* d_face_nbr = nullptr;
   // posed model
   fsdf::PosedModel pm;
   // poses: pinned ring + device copy
@@ -113,6 +118,11 @@ static void free_model(fsdf_ctx* c) {
   dfree(c->d_face_hull);
   dfree(c->d_sphere_l);
   dfree(c->d_face_off);
+  dfree(c->d_vert_hull);
+  dfree(c->d_vert_off);
+  dfree(c->d_face_nbr);
+  dfree(c->pm.verts_w);
+  dfree(c->pm.hscale_w);
   dfree(c->pm.planes_w);
   dfree(c->pm.facex_w);
   dfree(c->pm.spheres_w);
@@ -209,8 +219,9 @@ extern "C" int fsdf_set_model(fsdf_ctx* c, const fsdf_hull* hulls, int32_t K) {
   if (!hulls || K < 1) return fail(c, FSDF_ERR_ARG, "set_model: need at least one hull");
   if (K > fsdf::kMaxHulls) return fail(c, FSDF_ERR_ARG, "set_model: %d hulls exceeds the limit %d", K, fsdf::kMaxHulls);
   std::vector<double> verts, planes, sph;
-  std::vector<int32_t> faces, face_hull, face_off;
+  std::vector<int32_t> faces, face_hull, face_off, vert_hull, vert_off, face_nbr;
   face_off.push_back(0);
+  vert_off.push_back(0);
   for (int k = 0; k < K; ++k) {
     const fsdf_hull& h = hulls[k];
     if (h.n_vertices < 4 || h.n_faces < 4 || !h.vertices || !h.faces)
@@ -225,6 +236,8 @@ extern "C" int fsdf_set_model(fsdf_ctx* c, const fsdf_hull* hulls, int32_t K) {
         cen[j] += v;
       }
     for (int j = 0; j < 3; ++j) cen[j] /= h.n_vertices;
+    for (int i = 0; i < h.n_vertices; ++i) vert_hull.push_back(k);
+    vert_off.push_back((int32_t)vert_hull.size());
     double r2 = 0;
     for (int i = 0; i < h.n_vertices; ++i) {
       double s = 0;
@@ -266,6 +279,20 @@ extern "C" int fsdf_set_model(fsdf_ctx* c, const fsdf_hull* hulls, int32_t K) {
       for (int j = 0; j < 4; ++j) planes.push_back(pl[j]);
       face_hull.push_back(k);
     }
+    // face adjacency across each edge v_i -> v_{i+1} (the twin edge's face);
+    // an open mesh edge points back at its own face (the certificate then
+    // simply fails over to the exhaustive scan)
+    {
+      const int fbase = face_off.back();
+      std::map<std::pair<int, int>, int> owner;
+      for (int f = 0; f < h.n_faces; ++f)
+        for (int e = 0; e < 3; ++e) owner[{h.faces[3 * f + e], h.faces[3 * f + (e + 1) % 3]}] = f;
+      for (int f = 0; f < h.n_faces; ++f)
+        for (int e = 0; e < 3; ++e) {
+          auto it = owner.find({h.faces[3 * f + (e + 1) % 3], h.faces[3 * f + e]});
+          face_nbr.push_back(fbase + (it == owner.end() ? f : it->second));
+        }
+    }
     face_off.push_back((int32_t)(face_hull.size()));
   }
   HIPCHECK(c, hipSetDevice(c->device));
@@ -279,6 +306,11 @@ extern "C" int fsdf_set_model(fsdf_ctx* c, const fsdf_hull* hulls, int32_t K) {
   HIPCHECK(c, dalloc(&c->d_face_hull, face_hull.size() * sizeof(int32_t)));
   HIPCHECK(c, dalloc(&c->d_sphere_l, sph.size() * sizeof(double)));
   HIPCHECK(c, dalloc(&c->d_face_off, face_off.size() * sizeof(int32_t)));
+  HIPCHECK(c, dalloc(&c->d_vert_hull, vert_hull.size() * sizeof(int32_t)));
+  HIPCHECK(c, dalloc(&c->d_vert_off, vert_off.size() * sizeof(int32_t)));
+  HIPCHECK(c, dalloc(&c->d_face_nbr, face_nbr.size() * sizeof(int32_t)));
+  HIPCHECK(c, dalloc((char**)&c->pm.verts_w, (size_t)V * 4 * tsz));
+  HIPCHECK(c, dalloc((char**)&c->pm.hscale_w, (size_t)K * tsz));
   HIPCHECK(c, dalloc((char**)&c->pm.planes_w, (size_t)F * 4 * tsz));
   HIPCHECK(c, dalloc((char**)&c->pm.facex_w, (size_t)F * fsdf::kFaceX * tsz));
   HIPCHECK(c, dalloc(&c->pm.spheres_w, (size_t)K * 4 * sizeof(float)));
@@ -290,6 +322,9 @@ extern "C" int fsdf_set_model(fsdf_ctx* c, const fsdf_hull* hulls, int32_t K) {
   HIPCHECK(c, hipMemcpy(c->d_face_hull, face_hull.data(), face_hull.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   HIPCHECK(c, hipMemcpy(c->d_sphere_l, sph.data(), sph.size() * sizeof(double), hipMemcpyHostToDevice));
   HIPCHECK(c, hipMemcpy(c->d_face_off, face_off.data(), face_off.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHECK(c, hipMemcpy(c->d_vert_hull, vert_hull.data(), vert_hull.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHECK(c, hipMemcpy(c->d_vert_off, vert_off.data(), vert_off.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHECK(c, hipMemcpy(c->d_face_nbr, face_nbr.data(), face_nbr.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   for (int i = 0; i < kPoseRing; ++i) {
     if (c->h_poses[i]) (void)hipHostFree(c->h_poses[i]);
     c->h_poses[i] = nullptr;
@@ -305,6 +340,9 @@ extern "C" int fsdf_set_model(fsdf_ctx* c, const fsdf_hull* hulls, int32_t K) {
   c->lm.face_hull = c->d_face_hull;
   c->lm.sphere_l = c->d_sphere_l;
   c->lm.face_off = c->d_face_off;
+  c->lm.vert_hull = c->d_vert_hull;
+  c->lm.vert_off = c->d_vert_off;
+  c->lm.face_nbr = c->d_face_nbr;
   return FSDF_OK;
 }
 

@@ -9,11 +9,16 @@
 //     face_hull [F]     i32     owning hull of each face
 //     sphere_l  [K][4]  f64     vertex centroid (inside the hull) + radius
 //     face_off  [K+1]   i32     faces of hull k are [face_off[k], face_off[k+1])
+//     vert_hull [V]     i32     owning hull of each vertex
+//     vert_off  [K+1]   i32     vertices of hull k are [vert_off[k], vert_off[k+1])
+//     face_nbr  [F][3]  i32     face across edge i (v_i -> v_{i+1}) of each face
 //
 //   posed model (rewritten by every evaluation; T = double or float)
 //     planes_w  [F][4]  T       world plane
 //     facex_w   [F][24] T       3 inward edge planes (m_i, o_i) then a, b, c
 //     spheres_w [K][4]  f32     world centroid + radius (culling only)
+//     verts_w   [V][4]  T       world vertices (support/optimality certificate)
+//     hscale_w  [K]     T       max_v |v|_1 over the hull's world vertices
 //
 //   per-block partial sums  partials [1+6K][nblocks] f64 (column = block)
 #pragma once
@@ -35,12 +40,17 @@ struct LocalModel {
   const int32_t* face_hull = nullptr;
   const double* sphere_l = nullptr;
   const int32_t* face_off = nullptr;
+  const int32_t* vert_hull = nullptr;
+  const int32_t* vert_off = nullptr;
+  const int32_t* face_nbr = nullptr;
 };
 
 struct PosedModel {
   void* planes_w = nullptr;   // T
   void* facex_w = nullptr;    // T
   float* spheres_w = nullptr;
+  void* verts_w = nullptr;    // T
+  void* hscale_w = nullptr;   // T
 };
 
 struct PassOutputs {

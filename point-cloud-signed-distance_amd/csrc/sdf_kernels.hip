@@ -73,7 +73,8 @@ __device__ __forceinline__ double dot3(const double* a, const double* b) {
 template <typename T>
 __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const double* __restrict__ poses,
                                                       T* __restrict__ planes_w, T* __restrict__ facex_w,
-                                                      float* __restrict__ spheres_w) {
+                                                      float* __restrict__ spheres_w, T* __restrict__ verts_w,
+                                                      T* __restrict__ hscale_w) {
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid < lm.F) {
     const int f = tid;
@@ -109,11 +110,16 @@ __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const doubl
     fx[15] = (T)b[0]; fx[16] = (T)b[1]; fx[17] = (T)b[2];
     fx[18] = (T)c[0]; fx[19] = (T)c[1]; fx[20] = (T)c[2];
     fx[21] = (T)0; fx[22] = (T)0; fx[23] = (T)0;
-  } else if (tid < lm.F + lm.K) {
-    const int k = tid - lm.F;
-    double P[12];
-#pragma unroll
-    for (int i = 0; i < 12; ++i) P[i] = poses[12 * k + i];
+  } else if (tid < lm.F + lm.V) {
+    const int v = tid - lm.F;
+    const double* P = poses + 12 * lm.vert_hull[v];
+    double w[3];
+    xf_point(P, lm.verts_l + 3 * v, w);
+    T* o = verts_w + 4 * v;
+    o[0] = (T)w[0]; o[1] = (T)w[1]; o[2] = (T)w[2]; o[3] = (T)0;
+  } else if (tid < lm.F + lm.V + lm.K) {
+    const int k = tid - lm.F - lm.V;
+    const double* P = poses + 12 * k;
     double cw[3];
     xf_point(P, lm.sphere_l + 4 * k, cw);
     spheres_w[4 * k + 0] = (float)cw[0];
@@ -121,6 +127,15 @@ __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const doubl
     spheres_w[4 * k + 2] = (float)cw[2];
     // radius was rounded up to float on the host (exact-safe)
     spheres_w[4 * k + 3] = (float)lm.sphere_l[4 * k + 3];
+    // scale of the optimality certificate: max_v |v|_1 of the world vertices
+    T sc = (T)0;
+    for (int v = lm.vert_off[k]; v < lm.vert_off[k + 1]; ++v) {
+      double w[3];
+      xf_point(P, lm.verts_l + 3 * v, w);
+      const T l1 = (T)fabs(w[0]) + (T)fabs(w[1]) + (T)fabs(w[2]);
+      sc = l1 > sc ? l1 : sc;
+    }
+    hscale_w[k] = sc;
   }
 }
 
@@ -173,70 +188,153 @@ __device__ __forceinline__ void closest_on_triangle(T px, T py, T pz, const T* _
   qz = mfma_(w_, acz, mfma_(v_, abz, az));
 }
 
+// Posed model as the pass kernel sees it (device pointers, world frame).
+template <typename T>
+struct PassModel {
+  int K;
+  const int32_t* __restrict__ face_off;
+  const int32_t* __restrict__ vert_off;
+  const int32_t* __restrict__ nbr;
+  const T* __restrict__ planes;
+  const T* __restrict__ facex;
+  const T* __restrict__ verts;
+  const T* __restrict__ hscale;
+  const float* __restrict__ spheres;
+};
+
+template <typename T>
+__device__ __forceinline__ T plane_value(const T* __restrict__ pl, T px, T py, T pz) {
+  return mfma_(pl[0], px, mfma_(pl[1], py, mfma_(pl[2], pz, -pl[3])));
+}
+
+// Optimality certificate of a candidate closest point q of hull k (the GJK
+// termination test): q is the closest point of conv(V) to p iff
+// max_v (p-q)·v <= (p-q)·q; accepted within a rounding tolerance.
+template <typename T>
+__device__ __forceinline__ bool certified(T px, T py, T pz, T qx, T qy, T qz, int v0, int v1,
+                                          const T* __restrict__ verts, T scale) {
+  const T wx = px - qx, wy = py - qy, wz = pz - qz;
+  const T wq = mfma_(wx, qx, mfma_(wy, qy, wz * qz));
+  T smax = -tinf<T>();
+#pragma unroll 4
+  for (int v = v0; v < v1; ++v) {
+    const T* vv = verts + 4 * v;
+    const T sv = mfma_(vv[0], wx, mfma_(vv[1], wy, vv[2] * wz));
+    smax = sv > smax ? sv : smax;
+  }
+  const T tol = (T)1e-13 * ((fabs(wx) + fabs(wy)) + fabs(wz)) * scale;
+  return smax <= wq + tol;
+}
+
 // ---------------------------------------------------------------------------
-// Exact signed distance of p to posed hull with faces [f0, f1).
-// `active`: this lane's result is used (controls only the wave-uniform branch
-// into the closest-feature scan). Result gradient is world-frame, unit length.
+// Exact signed distance of p to posed hull k, with its unit gradient.
+//   inside / on the surface: max_f h_f, gradient n_{f*} (first max face);
+//   outside: if the projection on f* lies in triangle f*, d = h_{f*};
+//     otherwise the closest point is searched locally (triangle f*, then the
+//     neighbours across its violated edges), certified optimal by the support
+//     test over the hull's vertices, and only uncertified lanes fall back to the
+//     exhaustive scan of the visible faces.
+// `active`: this lane's result is used (gates the wave-uniform slow branches).
 // ---------------------------------------------------------------------------
 template <typename T>
-__device__ __forceinline__ void hull_sdf(T px, T py, T pz, int f0, int f1, const T* __restrict__ planes,
-                                         const T* __restrict__ facex, bool active, T& d, T& gx, T& gy,
-                                         T& gz, unsigned long long* __restrict__ stats) {
-  T hmax = -tinf<T>();
-  int fs = f0;
-  // 8 planes per trip: the wave-uniform plane rows arrive by scalar loads
-  // (s_load_dwordx8), issued a whole trip ahead of the VALU that consumes them.
-#pragma unroll 8
-  for (int f = f0; f < f1; ++f) {
-    const T* pl = planes + 4 * f;
-    const T h = mfma_(pl[0], px, mfma_(pl[1], py, mfma_(pl[2], pz, -pl[3])));
-    if (h > hmax) { hmax = h; fs = f; }
+__device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassModel<T>& m, bool active, T& d,
+                                         T& gx, T& gy, T& gz, unsigned long long* __restrict__ stats) {
+  const int f0 = __builtin_amdgcn_readfirstlane(m.face_off[k]);
+  const int f1 = __builtin_amdgcn_readfirstlane(m.face_off[k + 1]);
+  // two independent running maxima (even / odd faces) shorten the serial
+  // compare chain; merged with the first-index rule, identical to one chain
+  T hA = -tinf<T>(), hB = -tinf<T>();
+  int iA = f0, iB = f0;
+  int f = f0;
+#pragma unroll 4
+  for (; f + 1 < f1; f += 2) {
+    const T ha = plane_value(m.planes + 4 * f, px, py, pz);
+    const T hb = plane_value(m.planes + 4 * f + 4, px, py, pz);
+    if (ha > hA) { hA = ha; iA = f; }
+    if (hb > hB) { hB = hb; iB = f + 1; }
   }
-  const T* pls = planes + 4 * fs;
+  if (f < f1) {
+    const T ha = plane_value(m.planes + 4 * f, px, py, pz);
+    if (ha > hA) { hA = ha; iA = f; }
+  }
+  if (hB > hA || (hB == hA && iB < iA)) { hA = hB; iA = iB; }
+  const T hmax = hA;
+  const int fs = iA;
+  const T* pls = m.planes + 4 * fs;
   d = hmax;
   gx = pls[0]; gy = pls[1]; gz = pls[2];
   bool slow = false;
+  T s0 = (T)0, s1 = (T)0, s2 = (T)0;
   if (hmax > (T)0) {
     // Fast path: the projection of p on the max-violated face lies inside that
     // triangle => it is the closest point and the distance equals hmax.
-    const T* fx = facex + kFaceX * fs;
-    const T s0 = mfma_(fx[0], px, mfma_(fx[1], py, mfma_(fx[2], pz, -fx[3])));
-    const T s1 = mfma_(fx[4], px, mfma_(fx[5], py, mfma_(fx[6], pz, -fx[7])));
-    const T s2 = mfma_(fx[8], px, mfma_(fx[9], py, mfma_(fx[10], pz, -fx[11])));
+    const T* fx = m.facex + kFaceX * fs;
+    s0 = mfma_(fx[0], px, mfma_(fx[1], py, mfma_(fx[2], pz, -fx[3])));
+    s1 = mfma_(fx[4], px, mfma_(fx[5], py, mfma_(fx[6], pz, -fx[7])));
+    s2 = mfma_(fx[8], px, mfma_(fx[9], py, mfma_(fx[10], pz, -fx[11])));
     slow = !(s0 >= (T)0 && s1 >= (T)0 && s2 >= (T)0);
   }
   slow = slow && active;
   const uint64_t slow_mask = __ballot(slow);
-  if (slow_mask) {
-    if (stats && (threadIdx.x & 63) == 0) {
-      atomicAdd(stats + 2, 1ull);
-      atomicAdd(stats + 4, (unsigned long long)__builtin_popcountll(slow_mask));
-    }
-    // Closest feature over the faces visible from p (h_f > 0): the closest
-    // boundary point of a convex polytope lies on one of them; a face whose
-    // plane distance already exceeds the best distance cannot improve it.
-    T best2 = tinf<T>();
-    T qbx = (T)0, qby = (T)0, qbz = (T)0;
-    for (int f = f0; f < f1; ++f) {
-      const T* pl = planes + 4 * f;
-      const T h = mfma_(pl[0], px, mfma_(pl[1], py, mfma_(pl[2], pz, -pl[3])));
-      if (slow && h > (T)0 && h * h < best2) {
-        T qx, qy, qz;
-        closest_on_triangle(px, py, pz, facex + kFaceX * f + 12, qx, qy, qz);
-        const T dx = px - qx, dy = py - qy, dz = pz - qz;
-        const T dist2 = mfma_(dx, dx, mfma_(dy, dy, dz * dz));
-        if (dist2 < best2) { best2 = dist2; qbx = qx; qby = qy; qbz = qz; }
+  if (!slow_mask) return;
+  if (stats && (threadIdx.x & 63) == 0) {
+    atomicAdd(stats + 2, 1ull);
+    atomicAdd(stats + 4, (unsigned long long)__builtin_popcountll(slow_mask));
+  }
+  const int v0 = __builtin_amdgcn_readfirstlane(m.vert_off[k]);
+  const int v1 = __builtin_amdgcn_readfirstlane(m.vert_off[k + 1]);
+  const T scale = m.hscale[k];
+  // stage A: closest point on triangle f*
+  T qx, qy, qz;
+  closest_on_triangle(px, py, pz, m.facex + kFaceX * fs + 12, qx, qy, qz);
+  T ex = px - qx, ey = py - qy, ez = pz - qz;
+  T best2 = mfma_(ex, ex, mfma_(ey, ey, ez * ez));
+  bool todo = slow && !certified(px, py, pz, qx, qy, qz, v0, v1, m.verts, scale);
+  if (__any(todo)) {
+    // stage B: the neighbours across the violated edges of f*
+    if (stats && (threadIdx.x & 63) == 0) atomicAdd(stats + 6, 1ull);
+    const T sv[3] = {s0, s1, s2};
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      if (todo && sv[e] < (T)0) {
+        const int g = m.nbr[3 * fs + e];
+        T cx, cy, cz;
+        closest_on_triangle(px, py, pz, m.facex + kFaceX * g + 12, cx, cy, cz);
+        const T dx = px - cx, dy = py - cy, dz = pz - cz;
+        const T d2 = mfma_(dx, dx, mfma_(dy, dy, dz * dz));
+        if (d2 < best2) { best2 = d2; qx = cx; qy = cy; qz = cz; }
       }
     }
-    if (slow) {
-      if (best2 > (T)0) {
-        d = tsqrt(best2);
-        const T inv = (T)1 / d;
-        gx = (px - qbx) * inv; gy = (py - qby) * inv; gz = (pz - qbz) * inv;
-      } else {
-        // p on the boundary (a vertex/edge): d = 0, subgradient = face normal
-        d = (T)0;
+    todo = todo && !certified(px, py, pz, qx, qy, qz, v0, v1, m.verts, scale);
+    const uint64_t scan_mask = __ballot(todo);
+    if (scan_mask) {
+      // stage C: exhaustive scan of the visible faces (the closest boundary
+      // point of a convex polytope lies on one of them); a face whose plane
+      // distance already exceeds the best distance cannot improve it.
+      if (stats && (threadIdx.x & 63) == 0) atomicAdd(stats + 7, (unsigned long long)__builtin_popcountll(scan_mask));
+      T b2 = tinf<T>();
+      T bx = (T)0, by = (T)0, bz = (T)0;
+      for (int ff = f0; ff < f1; ++ff) {
+        const T h = plane_value(m.planes + 4 * ff, px, py, pz);
+        if (todo && h > (T)0 && h * h < b2) {
+          T cx, cy, cz;
+          closest_on_triangle(px, py, pz, m.facex + kFaceX * ff + 12, cx, cy, cz);
+          const T dx = px - cx, dy = py - cy, dz = pz - cz;
+          const T d2 = mfma_(dx, dx, mfma_(dy, dy, dz * dz));
+          if (d2 < b2) { b2 = d2; bx = cx; by = cy; bz = cz; }
+        }
       }
+      if (todo) { best2 = b2; qx = bx; qy = by; qz = bz; }
+    }
+  }
+  if (slow) {
+    if (best2 > (T)0) {
+      d = tsqrt(best2);
+      const T inv = (T)1 / d;
+      gx = (px - qx) * inv; gy = (py - qy) * inv; gz = (pz - qz) * inv;
+    } else {
+      // p on the boundary (a vertex/edge): d = 0, subgradient = face normal
+      d = (T)0;
     }
   }
 }
@@ -251,11 +349,10 @@ __device__ __forceinline__ double wave_sum(double v) {
 // Residual pass.
 // ---------------------------------------------------------------------------
 template <typename T, int SLOTS, bool CULL>
-__global__ __launch_bounds__(kBlock) void pass_kernel(const T* __restrict__ pts, int64_t n, int K,
-                                                      const int32_t* __restrict__ face_off,
-                                                      const T* __restrict__ planes,
-                                                      const T* __restrict__ facex,
-                                                      const float* __restrict__ spheres, PassOutputs out) {
+__global__ __launch_bounds__(kBlock) void pass_kernel(const T* __restrict__ pts, int64_t n, PassModel<T> m,
+                                                      PassOutputs out) {
+  const int K = m.K;
+  const float* __restrict__ spheres = m.spheres;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   double accF[SLOTS][3], accM[SLOTS][3];
@@ -309,10 +406,8 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(const T* __restrict__ pts,
     };
     // evaluations may run out of index order: ties keep the smaller k
     auto evaluate = [&](int k, bool need) {
-      const int f0 = __builtin_amdgcn_readfirstlane(face_off[k]);
-      const int f1 = __builtin_amdgcn_readfirstlane(face_off[k + 1]);
       T dk, hx, hy, hz;
-      hull_sdf<T>(px, py, pz, f0, f1, planes, facex, need, dk, hx, hy, hz, out.stats);
+      hull_sdf<T>(px, py, pz, k, m, need, dk, hx, hy, hz, out.stats);
       if (out.stats) {
         const uint64_t nm = __ballot(need);
         if (lane == 0) {
@@ -454,14 +549,15 @@ int pass_blocks(int64_t n) {
 
 hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_poses, const PosedModel& pm,
                        hipStream_t s) {
-  const int total = lm.F + lm.K;
+  const int total = lm.F + lm.V + lm.K;
   const int grid = (total + kBlock - 1) / kBlock;
   if (precision == 64) {
     hipLaunchKernelGGL(pose_kernel<double>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses,
-                       (double*)pm.planes_w, (double*)pm.facex_w, pm.spheres_w);
+                       (double*)pm.planes_w, (double*)pm.facex_w, pm.spheres_w, (double*)pm.verts_w,
+                       (double*)pm.hscale_w);
   } else {
     hipLaunchKernelGGL(pose_kernel<float>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses, (float*)pm.planes_w,
-                       (float*)pm.facex_w, pm.spheres_w);
+                       (float*)pm.facex_w, pm.spheres_w, (float*)pm.verts_w, (float*)pm.hscale_w);
   }
   return hipGetLastError();
 }
@@ -469,18 +565,23 @@ hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_pose
 template <typename T, bool CULL>
 static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void* d_pts, int64_t n, int nblocks,
                           const PassOutputs& out, hipStream_t s) {
+  PassModel<T> m;
+  m.K = lm.K;
+  m.face_off = lm.face_off;
+  m.vert_off = lm.vert_off;
+  m.nbr = lm.face_nbr;
+  m.planes = (const T*)pm.planes_w;
+  m.facex = (const T*)pm.facex_w;
+  m.verts = (const T*)pm.verts_w;
+  m.hscale = (const T*)pm.hscale_w;
+  m.spheres = pm.spheres_w;
   const T* pts = (const T*)d_pts;
-  const T* planes = (const T*)pm.planes_w;
-  const T* facex = (const T*)pm.facex_w;
   if (lm.K <= 64)
-    hipLaunchKernelGGL((pass_kernel<T, 1, CULL>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, lm.K, lm.face_off,
-                       planes, facex, pm.spheres_w, out);
+    hipLaunchKernelGGL((pass_kernel<T, 1, CULL>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, m, out);
   else if (lm.K <= 128)
-    hipLaunchKernelGGL((pass_kernel<T, 2, CULL>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, lm.K, lm.face_off,
-                       planes, facex, pm.spheres_w, out);
+    hipLaunchKernelGGL((pass_kernel<T, 2, CULL>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, m, out);
   else
-    hipLaunchKernelGGL((pass_kernel<T, 4, CULL>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, lm.K, lm.face_off,
-                       planes, facex, pm.spheres_w, out);
+    hipLaunchKernelGGL((pass_kernel<T, 4, CULL>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, m, out);
 }
 
 hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const void* d_pts,

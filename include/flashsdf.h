@@ -140,9 +140,9 @@ int fsdf_pass_time(fsdf_ctx* ctx, double* total_ms_out, int64_t* launches_out);
 /* Kernel work counters (diagnostics). enable=1 zeroes and starts counting in
  * every following pass; enable=0 stops and writes the 8 counters:
  *   [0] wave-iterations (64 points each)  [1] hull evaluations (per wave)
- *   [2] closest-feature scans (per wave)  [3] lane-needs summed over evaluations
- *   [4] lanes in closest-feature scans    [5] best-first seed evaluations
- *   [6..7] reserved (0) */
+ *   [2] slow-path entries (per wave)      [3] lane-needs summed over evaluations
+ *   [4] lanes on the slow path            [5] best-first seed evaluations
+ *   [6] waves reaching stage B (neighbours) [7] lanes in the exhaustive scan */
 int fsdf_kernel_stats(fsdf_ctx* ctx, int32_t enable, uint64_t* counters_out);
 
 #ifdef __cplusplus

@@ -368,7 +368,6 @@ static int adopt_points_device(fsdf_ctx* c, const double* d_src, int64_t n, void
 static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool device_src) {
   if (!c) return FSDF_ERR_ARG;
   if (n < 0 || (n > 0 && !src)) return fail(c, FSDF_ERR_ARG, "set_points: bad buffer (n=%lld)", (long long)n);
-  if (c->sort_points) return fail(c, FSDF_ERR_ARG, "set_points: sort_points is not available in this build");
   HIPCHECK(c, hipSetDevice(c->device));
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   c->n = 0;
@@ -383,7 +382,26 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
     }
     d_src = staging;
   }
-  int rc = adopt_points_device(c, d_src, n, &c->d_pts, &c->pts_cap);
+  int rc = FSDF_OK;
+  dfree(c->d_perm);
+  if (c->sort_points && n > 0) {
+    // spatially coherent resident order + permutation back to caller order
+    const size_t tsz = c->precision == 64 ? sizeof(double) : sizeof(float);
+    if (c->pts_cap < n) {
+      dfree(c->d_pts);
+      c->pts_cap = 0;
+      hipError_t e = hipMalloc(&c->d_pts, (size_t)n * 3 * tsz);
+      if (e == hipSuccess) c->pts_cap = n;
+      else rc = fail(c, FSDF_ERR_HIP, "set_points: %s", hipGetErrorString(e));
+    }
+    if (rc == FSDF_OK) {
+      hipError_t e = hipMalloc(&c->d_perm, (size_t)n * sizeof(int64_t));
+      if (e == hipSuccess) e = fsdf::sort_points_morton(d_src, n, c->precision, c->d_pts, c->d_perm, c->stream);
+      if (e != hipSuccess) rc = fail(c, FSDF_ERR_HIP, "set_points (sort): %s", hipGetErrorString(e));
+    }
+  } else {
+    rc = adopt_points_device(c, d_src, n, &c->d_pts, &c->pts_cap);
+  }
   if (rc == FSDF_OK) {
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) rc = fail(c, FSDF_ERR_HIP, "set_points: %s", hipGetErrorString(e));

@@ -77,4 +77,9 @@ hipError_t launch_to_f32(const double* src, float* dst, int64_t count, hipStream
 
 int pass_blocks(int64_t n);
 
+// Morton-order the f64 AoS cloud d_src into d_dst (context precision) and write
+// the permutation d_perm[resident i] = caller index. Synchronizes `s`.
+hipError_t sort_points_morton(const double* d_src, int64_t n, int precision, void* d_dst, int64_t* d_perm,
+                              hipStream_t s);
+
 }  // namespace fsdf

@@ -369,40 +369,43 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(const T* __restrict__ pts,
     const int64_t ii = valid ? i : n - 1;
     const T px = pts[3 * ii + 0], py = pts[3 * ii + 1], pz = pts[3 * ii + 2];
 
-    // Phase A (fp32, exact-safe): per hull lower bound lb_k = |p-c_k| - r_k
-    // (sphere around the hull), upper bound ub = min_k |p-c_k| (c_k is inside
-    // its hull), and the best-first seed hull argmin_k lb_k.
-    float ub = __builtin_huge_valf(), lbmin = __builtin_huge_valf();
+    // Phase A (fp32, exact-safe): with c_k inside hull k and r_k its bounding
+    // radius, d_k(p) >= |p-c_k| - r_k (lower bound) and d_k(p) <= |p-c_k|
+    // (upper bound). ub = min_k |p-c_k|; the best-first seed is the hull of
+    // least power distance |p-c_k|^2 - r_k^2 (a heuristic: any seed is exact).
+    float ub2 = __builtin_huge_valf(), pw_min = __builtin_huge_valf(), smax = 0.f;
     int kseed = 0;
-    float pxf = 0.f, pyf = 0.f, pzf = 0.f, pmag = 0.f;
+    float pxf = 0.f, pyf = 0.f, pzf = 0.f;
     if (CULL) {
       pxf = (float)px; pyf = (float)py; pzf = (float)pz;
-      pmag = fabsf(pxf) + fabsf(pyf) + fabsf(pzf);
       for (int k = 0; k < K; ++k) {
         const float* sp = spheres + 4 * k;
         const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
-        const float dist = __builtin_sqrtf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)));
-        ub = fminf(ub, dist);
-        const float lb = dist - sp[3];
-        if (lb < lbmin) { lbmin = lb; kseed = k; }
+        const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
+        ub2 = fminf(ub2, dist2);
+        const float pwr = __builtin_fmaf(-sp[3], sp[3], dist2);
+        if (pwr < pw_min) { pw_min = pwr; kseed = k; }
+        smax = fmaxf(smax, fabsf(sp[0]) + fabsf(sp[1]) + fabsf(sp[2]) + 2.0f * sp[3]);
       }
     }
+    const float ub = __builtin_sqrtf(ub2);
+    // one rounding margin per lane, >= 1e-5 x every magnitude in the test below
+    const float mrg = 1e-5f * (1.0f + fabsf(pxf) + fabsf(pyf) + fabsf(pzf) + smax + 2.0f * ub);
 
     T best = tinf<T>();
     int bk = 0x7fffffff;
     T gx = (T)0, gy = (T)0, gz = (T)0;
     // hull k is needed by a lane unless its lower bound exceeds min(ub, best)
     // by more than the fp32 rounding margin
+    // hull k is needed by a lane unless |p-c_k| - r_k > min(ub, best) + mrg,
+    // tested without a sqrt: |p-c_k|^2 <= (min(ub, best) + mrg + r_k)^2
     auto needs = [&](int k) -> bool {
       if (!CULL) return valid;
       const float* sp = spheres + 4 * k;
       const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
-      const float dist = __builtin_sqrtf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)));
-      const float lb = dist - sp[3];
-      const float bf = fminf(ub, (float)best);
-      const float mrg =
-          1e-5f * (1.0f + pmag + fabsf(sp[0]) + fabsf(sp[1]) + fabsf(sp[2]) + sp[3] + dist + fabsf(bf));
-      return valid && (lb <= bf + mrg);
+      const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
+      const float t = fminf(ub, (float)best) + mrg + sp[3];
+      return valid && t >= 0.0f && dist2 <= t * t;
     };
     // evaluations may run out of index order: ties keep the smaller k
     auto evaluate = [&](int k, bool need) {

@@ -213,10 +213,11 @@ class Context:
         check(self._lib.fsdf_pass_time(self._ctx, ctypes.byref(ms), ctypes.byref(n)), self._ctx, "pass_time")
         return ms.value, n.value
 
-    STAT_NAMES = ("wave_iters", "hull_evals", "scans", "lane_needs", "scan_lanes", "seed_evals")
+    STAT_NAMES = ("wave_iters", "hull_evals", "slow_waves", "lane_needs", "slow_lanes", "seed_evals",
+                  "stageB_waves", "full_scan_lanes")
 
     def kernel_stats(self, enable: bool):
         """enable=True: start counting; enable=False: stop, return the counters."""
         out = np.zeros(8, np.uint64)
         check(self._lib.fsdf_kernel_stats(self._ctx, int(enable), ptr(out)), self._ctx, "kernel_stats")
-        return None if enable else dict(zip(self.STAT_NAMES, (int(v) for v in out[:6])))
+        return None if enable else dict(zip(self.STAT_NAMES, (int(v) for v in out[:8])))

@@ -23,8 +23,8 @@ def ctx_factory():
     from flash import _lib
     made = []
 
-    def make(manip, precision=64, cull=True):
-        c = _lib.Context(device=0, precision=precision, cull=cull)
+    def make(manip, precision=64, cull=True, sort_points=False):
+        c = _lib.Context(device=0, precision=precision, cull=cull, sort_points=sort_points)
         c.set_model([(s.hull.vertices, s.hull.faces, s.hull.planes) for s in manip.convex_surfaces()])
         made.append(c)
         return c
@@ -193,3 +193,28 @@ def test_cost_functor_gradient_and_tracking(irb):
                        solver=NaiveSolver(6, rate=0.5, max_step=0.05, iteration_limit=20))
     assert seen[-1] < seen[0]
     assert np.linalg.norm(x - qt) < np.linalg.norm(qe - qt) + 1e-9
+
+
+def test_sort_points_preserves_caller_order(m64, oracle_mod, ctx_factory):
+    """sort_points (device Morton order) changes only speed: per-point outputs
+    come back in caller order, bit-identical to the oracle."""
+    import flash
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(m64, 501)
+    pts = synthetic.depth_cloud(m64, qt, 30011, seed=502, order="shuffled")
+    poses = flash.hull_poses(m64, qe)
+    om = oracle_mod.OracleModel.from_manipulator(m64)
+    ref, ref_acc = om.skin(poses, pts), om.cost_accum(poses, pts)
+    for precision in (64, 32):
+        ctx = ctx_factory(m64, precision=precision, sort_points=True)
+        ctx.set_points(pts)
+        _, acc, (k, d, g) = ctx.eval(poses, per_point=True)
+        if precision == 64:
+            _check_against(ref, d, k, g, acc, ref_acc)
+        else:
+            assert np.abs(d - ref[0]).max() < 2e-5
+    # a second frame replaces the permutation
+    pts2 = pts[::-1].copy()
+    ctx.set_points(pts2)
+    _, _, (k2, d2, _) = ctx.eval(poses, per_point=True)
+    assert np.abs(d2 - ref[0][::-1]).max() < 2e-5

@@ -32,16 +32,21 @@ def main():
     poses = flash.hull_poses(m, qe)
     clouds = {o: synthetic.depth_cloud(m, qt, args.points, seed=1234 + 17, order=o) for o in ("raster", "shuffled")}
     hulls = [(s.hull.vertices, s.hull.faces, s.hull.planes) for s in m.surfaces]
-    variants = [("raster", True, 64), ("shuffled", True, 64), ("raster", False, 64), ("raster", True, 32)]
+    variants = [("raster", True, 64, False), ("shuffled", True, 64, False), ("shuffled", True, 64, True),
+                ("raster", True, 64, True), ("raster", False, 64, False), ("raster", True, 32, False)]
     if args.variants != "all":
-        variants = [v for v in variants if f"{v[0]}-{int(v[1])}-{v[2]}" in args.variants.split(",")]
-    ctxs = {}
-    for order, cull, prec in variants:
-        c = _lib.Context(device=0, precision=prec, cull=cull)
+        variants = [v for v in variants if f"{v[0]}-{int(v[1])}-{v[2]}-{int(v[3])}" in args.variants.split(",")]
+    ctxs, setup_ms = {}, {}
+    import time
+    for order, cull, prec, srt in variants:
+        c = _lib.Context(device=0, precision=prec, cull=cull, sort_points=srt)
         c.set_model(hulls)
         c.set_points(clouds[order])
+        t = time.perf_counter()
+        c.set_points(clouds[order])
+        setup_ms[(order, cull, prec, srt)] = (time.perf_counter() - t) * 1e3
         c.eval(poses)  # warm
-        ctxs[(order, cull, prec)] = c
+        ctxs[(order, cull, prec, srt)] = c
     times = {v: [] for v in variants}
     for _ in range(args.rounds):
         for v in variants:
@@ -59,11 +64,13 @@ def main():
         st = c.kernel_stats(False)
         w = st["wave_iters"]
         ms = float(np.median(times[v]))
-        row = {"order": v[0], "cull": v[1], "precision": v[2], "pass_ms_median": ms,
+        row = {"order": v[0], "cull": v[1], "precision": v[2], "sort_points": v[3], "set_points_ms": setup_ms[v],
+               "pass_ms_median": ms,
                "pass_ms_min": float(np.min(times[v])), "Mevals_per_s": args.points / ms / 1e3,
                "hull_evals_per_wave": st["hull_evals"] / w, "seed_evals_per_wave": st["seed_evals"] / w,
-               "scans_per_wave": st["scans"] / w, "lane_need_frac": st["lane_needs"] / max(st["hull_evals"] * 64, 1),
-               "scan_lane_frac": st["scan_lanes"] / max(st["scans"] * 64, 1), **st}
+               "slow_per_wave": st["slow_waves"] / w, "lane_need_frac": st["lane_needs"] / max(st["hull_evals"] * 64, 1),
+               "slow_lane_frac": st["slow_lanes"] / max(st["slow_waves"] * 64, 1),
+               "full_scan_lane_frac_of_slow": st["full_scan_lanes"] / max(st["slow_lanes"], 1), **st}
         res.append(row)
         print(json.dumps(row), flush=True)
     if args.json:

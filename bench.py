@@ -43,7 +43,9 @@ def parse():
     p.add_argument("--points", type=int, default=1 << 20, help="points per GPU")
     p.add_argument("--precision", type=int, default=64, choices=(64, 32))
     p.add_argument("--no-cull", action="store_true")
-    p.add_argument("--order", default="raster", choices=("raster", "shuffled"))
+    p.add_argument("--order", default="shuffled", choices=("raster", "shuffled"),
+                   help="input order of the synthetic cloud (shuffled = adversarial)")
+    p.add_argument("--no-sort", action="store_true", help="keep the input order resident (no Morton sort)")
     p.add_argument("--no-per-point", action="store_true", help="reduction-only pass (no per-point outputs)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of the CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -96,11 +98,15 @@ def main():
     q_alt = q_eval + 1e-3  # alternate between two configurations step to step
     poses = [flash.hull_poses(m64, q_eval), flash.hull_poses(m64, q_alt)]
 
-    ctx = m64.engine(device=local, precision=args.precision, cull=not args.no_cull)
+    ctx = m64.engine(device=local, precision=args.precision, cull=not args.no_cull, sort_points=not args.no_sort)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
     d_pts = torch.as_tensor(pts, device=dev)
-    ctx.set_points_device(d_pts.data_ptr(), len(pts))
+    torch.cuda.synchronize()
+    ctx.set_points_device(d_pts.data_ptr(), len(pts))  # first upload (allocations)
+    t_set = time.perf_counter()
+    ctx.set_points_device(d_pts.data_ptr(), len(pts))  # once per frame: copy (+ Morton sort)
+    set_points_ms = (time.perf_counter() - t_set) * 1e3
     del d_pts
     n = len(pts)
     accum = torch.zeros(1 + 6 * ctx.K, dtype=torch.float64, device=dev)
@@ -167,7 +173,9 @@ def main():
                 "workload": "M64: 8 IRB140 arms (7 link hulls + ATI hull each) on a 2x4 grid, 64 convex hulls, "
                             "48 DOF; seeded synthetic depth cloud per GPU (SURVEY.md §8d generator G)",
                 "points_per_gpu": n, "global_points": n * world, "hulls": ctx.K, "dof": m64.mechanism.num_positions,
-                "order": args.order, "cull": not args.no_cull, "per_point_outputs": not args.no_per_point,
+                "input_order": args.order, "sort_points": not args.no_sort,
+                "set_points_ms_per_frame": set_points_ms,
+                "cull": not args.no_cull, "per_point_outputs": not args.no_per_point,
                 "parallelism": f"points sharded x{world}, RCCL all-reduce of {1 + 6 * ctx.K} f64 per pass",
             },
             "roofline": {

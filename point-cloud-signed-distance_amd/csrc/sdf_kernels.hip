@@ -207,22 +207,63 @@ __device__ __forceinline__ T plane_value(const T* __restrict__ pl, T px, T py, T
   return mfma_(pl[0], px, mfma_(pl[1], py, mfma_(pl[2], pz, -pl[3])));
 }
 
+// Per-wave LDS staging of the evaluated hull's rows (planes, then vertices):
+// one coalesced bulk copy per chunk (dwordx4 loads, every row in flight at
+// once), then wave-uniform broadcast ds_read_b128 in the loops, instead of a
+// dependent scalar-load chain per row.
+constexpr int kStagePlanes = 128;  // plane rows per chunk
+constexpr int kStageVerts = 64;    // vertex rows per chunk
+constexpr int kStageRows = kStagePlanes + kStageVerts;
+#ifndef FSDF_PASS_WAVES_PER_SIMD
+#define FSDF_PASS_WAVES_PER_SIMD 4
+#endif
+constexpr int kPassWavesPerSimd = FSDF_PASS_WAVES_PER_SIMD;  // occupancy target (VGPR budget 512/w)
+
+template <typename T> struct Row4 { typedef T __attribute__((ext_vector_type(4))) type; };
+
+// Must be called with every lane of the wave active (wave-uniform control flow).
+template <typename T>
+__device__ __forceinline__ void stage_rows(T* __restrict__ lds, const T* __restrict__ src, int rows) {
+  typedef typename Row4<T>::type R;
+  const int lane = threadIdx.x & 63;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // prior reads of this stage precede the overwrite
+  for (int r = lane; r < rows; r += 64) *(R*)(lds + 4 * r) = *(const R*)(src + 4 * r);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <typename T>
+__device__ __forceinline__ T row_plane_value(const T* __restrict__ lrow, T px, T py, T pz) {
+  typedef typename Row4<T>::type R;
+  const R pl = *(const R*)lrow;
+  return mfma_(pl[0], px, mfma_(pl[1], py, mfma_(pl[2], pz, -pl[3])));
+}
+
+template <typename T> __device__ __forceinline__ T cert_eps();
+template <> __device__ __forceinline__ double cert_eps() { return 1e-13; }
+template <> __device__ __forceinline__ float cert_eps() { return 4e-6f; }
+
 // Optimality certificate of a candidate closest point q of hull k (the GJK
 // termination test): q is the closest point of conv(V) to p iff
 // max_v (p-q)·v <= (p-q)·q; accepted within a rounding tolerance.
 template <typename T>
 __device__ __forceinline__ bool certified(T px, T py, T pz, T qx, T qy, T qz, int v0, int v1,
-                                          const T* __restrict__ verts, T scale) {
+                                          const T* __restrict__ verts, T scale, T* __restrict__ lw) {
+  typedef typename Row4<T>::type R;
   const T wx = px - qx, wy = py - qy, wz = pz - qz;
   const T wq = mfma_(wx, qx, mfma_(wy, qy, wz * qz));
   T smax = -tinf<T>();
+  T* lv = lw + 4 * kStagePlanes;
+  for (int c0 = v0; c0 < v1; c0 += kStageVerts) {
+    const int cn = min(kStageVerts, v1 - c0);
+    stage_rows(lv, verts + 4 * c0, cn);
 #pragma unroll 4
-  for (int v = v0; v < v1; ++v) {
-    const T* vv = verts + 4 * v;
-    const T sv = mfma_(vv[0], wx, mfma_(vv[1], wy, vv[2] * wz));
-    smax = sv > smax ? sv : smax;
+    for (int v = 0; v < cn; ++v) {
+      const R vv = *(const R*)(lv + 4 * v);
+      const T sv = mfma_(vv[0], wx, mfma_(vv[1], wy, vv[2] * wz));
+      smax = sv > smax ? sv : smax;
+    }
   }
-  const T tol = (T)1e-13 * ((fabs(wx) + fabs(wy)) + fabs(wz)) * scale;
+  const T tol = cert_eps<T>() * ((fabs(wx) + fabs(wy)) + fabs(wz)) * scale;
   return smax <= wq + tol;
 }
 
@@ -235,27 +276,33 @@ __device__ __forceinline__ bool certified(T px, T py, T pz, T qx, T qy, T qz, in
 //     test over the hull's vertices, and only uncertified lanes fall back to the
 //     exhaustive scan of the visible faces.
 // `active`: this lane's result is used (gates the wave-uniform slow branches).
+// `lw`: this wave's LDS stage (kStageRows rows of 4 T).
 // ---------------------------------------------------------------------------
 template <typename T>
 __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassModel<T>& m, bool active, T& d,
-                                         T& gx, T& gy, T& gz, unsigned long long* __restrict__ stats) {
+                                         T& gx, T& gy, T& gz, T* __restrict__ lw,
+                                         unsigned long long* __restrict__ stats) {
   const int f0 = __builtin_amdgcn_readfirstlane(m.face_off[k]);
   const int f1 = __builtin_amdgcn_readfirstlane(m.face_off[k + 1]);
   // two independent running maxima (even / odd faces) shorten the serial
   // compare chain; merged with the first-index rule, identical to one chain
   T hA = -tinf<T>(), hB = -tinf<T>();
   int iA = f0, iB = f0;
-  int f = f0;
+  for (int c0 = f0; c0 < f1; c0 += kStagePlanes) {
+    const int cn = min(kStagePlanes, f1 - c0);
+    stage_rows(lw, m.planes + 4 * c0, cn);
+    int i = 0;
 #pragma unroll 4
-  for (; f + 1 < f1; f += 2) {
-    const T ha = plane_value(m.planes + 4 * f, px, py, pz);
-    const T hb = plane_value(m.planes + 4 * f + 4, px, py, pz);
-    if (ha > hA) { hA = ha; iA = f; }
-    if (hb > hB) { hB = hb; iB = f + 1; }
-  }
-  if (f < f1) {
-    const T ha = plane_value(m.planes + 4 * f, px, py, pz);
-    if (ha > hA) { hA = ha; iA = f; }
+    for (; i + 1 < cn; i += 2) {
+      const T ha = row_plane_value(lw + 4 * i, px, py, pz);
+      const T hb = row_plane_value(lw + 4 * i + 4, px, py, pz);
+      if (ha > hA) { hA = ha; iA = c0 + i; }
+      if (hb > hB) { hB = hb; iB = c0 + i + 1; }
+    }
+    if (i < cn) {
+      const T ha = row_plane_value(lw + 4 * i, px, py, pz);
+      if (ha > hA) { hA = ha; iA = c0 + i; }
+    }
   }
   if (hB > hA || (hB == hA && iB < iA)) { hA = hB; iA = iB; }
   const T hmax = hA;
@@ -289,7 +336,9 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   closest_on_triangle(px, py, pz, m.facex + kFaceX * fs + 12, qx, qy, qz);
   T ex = px - qx, ey = py - qy, ez = pz - qz;
   T best2 = mfma_(ex, ex, mfma_(ey, ey, ez * ez));
-  bool todo = slow && !certified(px, py, pz, qx, qy, qz, v0, v1, m.verts, scale);
+  // (the certificate stages rows cooperatively: call it with the whole wave)
+  const bool certA = certified(px, py, pz, qx, qy, qz, v0, v1, m.verts, scale, lw);
+  bool todo = slow && !certA;
   if (__any(todo)) {
     // stage B: the neighbours across the violated edges of f*
     if (stats && (threadIdx.x & 63) == 0) atomicAdd(stats + 6, 1ull);
@@ -305,7 +354,8 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
         if (d2 < best2) { best2 = d2; qx = cx; qy = cy; qz = cz; }
       }
     }
-    todo = todo && !certified(px, py, pz, qx, qy, qz, v0, v1, m.verts, scale);
+    const bool certB = certified(px, py, pz, qx, qy, qz, v0, v1, m.verts, scale, lw);
+    todo = todo && !certB;
     const uint64_t scan_mask = __ballot(todo);
     if (scan_mask) {
       // stage C: exhaustive scan of the visible faces (the closest boundary
@@ -349,18 +399,22 @@ __device__ __forceinline__ double wave_sum(double v) {
 // Residual pass.
 // ---------------------------------------------------------------------------
 template <typename T, int SLOTS, bool CULL>
-__global__ __launch_bounds__(kBlock) void pass_kernel(const T* __restrict__ pts, int64_t n, PassModel<T> m,
+__global__ __launch_bounds__(kBlock, kPassWavesPerSimd) void pass_kernel(const T* __restrict__ pts, int64_t n, PassModel<T> m,
                                                       PassOutputs out) {
   const int K = m.K;
   const float* __restrict__ spheres = m.spheres;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  double accF[SLOTS][3], accM[SLOTS][3];
+  // per-hull wrench sums live in LDS from the start: row (s*64 + lane) of
+  // this wave's slab is owned by lane `lane` (hull s*64 + lane)
+  __shared__ double red[kBlock / 64][SLOTS * 64 * 6 + 1];
+  double* acc_row = &red[wave][lane * 6];
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) { accF[s][j] = 0.0; accM[s][j] = 0.0; }
+    for (int j = 0; j < 6; ++j) acc_row[s * 64 * 6 + j] = 0.0;
   double cost_acc = 0.0;
+  __shared__ __attribute__((aligned(32))) T stage[kBlock / 64][4 * kStageRows];
 
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t base = (int64_t)blockIdx.x * kBlock + wave * 64; base < n; base += stride) {
@@ -410,7 +464,7 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(const T* __restrict__ pts,
     // evaluations may run out of index order: ties keep the smaller k
     auto evaluate = [&](int k, bool need) {
       T dk, hx, hy, hz;
-      hull_sdf<T>(px, py, pz, k, m, need, dk, hx, hy, hz, out.stats);
+      hull_sdf<T>(px, py, pz, k, m, need, dk, hx, hy, hz, stage[wave], out.stats);
       if (out.stats) {
         const uint64_t nm = __ballot(need);
         if (lane == 0) {
@@ -476,14 +530,9 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(const T* __restrict__ pts,
 #pragma unroll
       for (int j = 0; j < 6; ++j) v[j] = wave_sum(v[j]);
       if (lane == (kk & 63)) {
-        const int slot = kk >> 6;
+        double* r = acc_row + (kk >> 6) * 64 * 6;
 #pragma unroll
-        for (int s = 0; s < SLOTS; ++s) {
-          if (s == slot) {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) { accF[s][j] += v[j]; accM[s][j] += v[3 + j]; }
-          }
-        }
+        for (int j = 0; j < 6; ++j) r[j] += v[j];
       }
     }
 
@@ -500,14 +549,7 @@ __global__ __launch_bounds__(kBlock) void pass_kernel(const T* __restrict__ pts,
   }
 
   // ---- block combine (fixed order) ----
-  __shared__ double red[kBlock / 64][SLOTS * 64 * 6 + 1];
   cost_acc = wave_sum(cost_acc);
-#pragma unroll
-  for (int s = 0; s < SLOTS; ++s) {
-    double* r = &red[wave][(s * 64 + lane) * 6];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) { r[j] = accF[s][j]; r[3 + j] = accM[s][j]; }
-  }
   if (lane == 0) red[wave][SLOTS * 64 * 6] = cost_acc;
   __syncthreads();
   const int len = 1 + 6 * K;

@@ -13,7 +13,8 @@ from ctypes import POINTER, c_char_p, c_double, c_int32, c_int64, c_void_p
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libflashsdf.so")
+# FLASHSDF_LIB overrides the library path (A/B builds of the same ABI)
+LIB_PATH = os.environ.get("FLASHSDF_LIB") or os.path.join(_HERE, "libflashsdf.so")
 
 FSDF_OK = 0
 STATUS_NAMES = {1: "FSDF_ERR_ARG", 2: "FSDF_ERR_HIP", 3: "FSDF_ERR_STATE", 4: "FSDF_ERR_NOMEM",

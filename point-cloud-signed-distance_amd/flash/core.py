@@ -81,9 +81,12 @@ class Manipulator:
     def convex_surfaces(self) -> list[ConvexGeometry]:
         return [s for s in self.surfaces if isinstance(s, ConvexGeometry)]
 
-    def engine(self, device: int = 0, precision: int = 64, cull: bool = True) -> "_lib.Context":
-        """The native context holding this model on `device` (created once)."""
-        key = (device, precision, cull)
+    def engine(self, device: int = 0, precision: int = 64, cull: bool = True,
+               sort_points: bool = True) -> "_lib.Context":
+        """The native context holding this model on `device` (created once).
+        sort_points: the resident cloud is Morton-ordered on the device once per
+        frame (set_points); outputs still come back in caller order."""
+        key = (device, precision, cull, sort_points)
         ctx = self._engines.get(key)
         if ctx is None:
             if len(self.convex_surfaces()) != len(self.surfaces):
@@ -91,7 +94,7 @@ class Manipulator:
                     "RBF (InterpolatingSkin) surfaces are not in the GPU residual pass yet "
                     "(SURVEY.md §8f rank 2); this model has "
                     f"{len(self.surfaces) - len(self.convex_surfaces())} of them")
-            ctx = _lib.Context(device=device, precision=precision, cull=cull)
+            ctx = _lib.Context(device=device, precision=precision, cull=cull, sort_points=sort_points)
             ctx.set_model([(s.hull.vertices, s.hull.faces, s.hull.planes) for s in self.surfaces])
             self._engines[key] = ctx
         return ctx

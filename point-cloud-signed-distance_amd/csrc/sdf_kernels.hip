@@ -75,7 +75,10 @@ __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const doubl
                                                       T* __restrict__ planes_w, T* __restrict__ facex_w,
                                                       float* __restrict__ spheres_w, T* __restrict__ verts_w,
                                                       T* __restrict__ hscale_w) {
-  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int fv = lm.F + lm.V, fv_pad = (fv + 63) & ~63;
+  if (tid >= fv && tid < fv_pad) return;  // padding: hull waves start wave-aligned
+  if (tid >= fv_pad) tid -= fv_pad - fv;
   if (tid < lm.F) {
     const int f = tid;
     const int k = lm.face_hull[f];
@@ -117,25 +120,34 @@ __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const doubl
     xf_point(P, lm.verts_l + 3 * v, w);
     T* o = verts_w + 4 * v;
     o[0] = (T)w[0]; o[1] = (T)w[1]; o[2] = (T)w[2]; o[3] = (T)0;
-  } else if (tid < lm.F + lm.V + lm.K) {
-    const int k = tid - lm.F - lm.V;
+  } else if (tid < lm.F + lm.V + 64 * lm.K) {
+    // one wave per hull (the wave is entirely inside this range: F + V is
+    // padded to a multiple of 64 by the launcher): sphere + certificate scale
+    const int r = tid - lm.F - lm.V;
+    const int k = r >> 6, lane = r & 63;
     const double* P = poses + 12 * k;
-    double cw[3];
-    xf_point(P, lm.sphere_l + 4 * k, cw);
-    spheres_w[4 * k + 0] = (float)cw[0];
-    spheres_w[4 * k + 1] = (float)cw[1];
-    spheres_w[4 * k + 2] = (float)cw[2];
-    // radius was rounded up to float on the host (exact-safe)
-    spheres_w[4 * k + 3] = (float)lm.sphere_l[4 * k + 3];
-    // scale of the optimality certificate: max_v |v|_1 of the world vertices
     T sc = (T)0;
-    for (int v = lm.vert_off[k]; v < lm.vert_off[k + 1]; ++v) {
+    for (int v = lm.vert_off[k] + lane; v < lm.vert_off[k + 1]; v += 64) {
       double w[3];
       xf_point(P, lm.verts_l + 3 * v, w);
       const T l1 = (T)fabs(w[0]) + (T)fabs(w[1]) + (T)fabs(w[2]);
       sc = l1 > sc ? l1 : sc;
     }
-    hscale_w[k] = sc;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const T o = __shfl_xor(sc, off, 64);
+      sc = o > sc ? o : sc;
+    }
+    if (lane == 0) {
+      double cw[3];
+      xf_point(P, lm.sphere_l + 4 * k, cw);
+      spheres_w[4 * k + 0] = (float)cw[0];
+      spheres_w[4 * k + 1] = (float)cw[1];
+      spheres_w[4 * k + 2] = (float)cw[2];
+      // radius was rounded up to float on the host (exact-safe)
+      spheres_w[4 * k + 3] = (float)lm.sphere_l[4 * k + 3];
+      hscale_w[k] = sc;
+    }
   }
 }
 
@@ -399,7 +411,7 @@ __device__ __forceinline__ double wave_sum(double v) {
 // Residual pass.
 // ---------------------------------------------------------------------------
 template <typename T, int SLOTS, bool CULL>
-__global__ __launch_bounds__(kBlock, kPassWavesPerSimd) void pass_kernel(const T* __restrict__ pts, int64_t n, PassModel<T> m,
+__global__ __launch_bounds__(kBlock, SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) void pass_kernel(const T* __restrict__ pts, int64_t n, PassModel<T> m,
                                                       PassOutputs out) {
   const int K = m.K;
   const float* __restrict__ spheres = m.spheres;
@@ -594,7 +606,7 @@ int pass_blocks(int64_t n) {
 
 hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_poses, const PosedModel& pm,
                        hipStream_t s) {
-  const int total = lm.F + lm.V + lm.K;
+  const int total = ((lm.F + lm.V + 63) & ~63) + 64 * lm.K;
   const int grid = (total + kBlock - 1) / kBlock;
   if (precision == 64) {
     hipLaunchKernelGGL(pose_kernel<double>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses,

@@ -28,11 +28,16 @@
  *   - A pose is 12 float64: R (3x3, row-major) then t (3); x_world = R x_local + t.
  *   - Every function returns 0 (FSDF_OK) or a nonzero status; the message of the
  *     last failure on a context is fsdf_last_error(ctx).
- *   - Accumulator layout (length 1 + 6K, K = number of hulls):
+ *   - Accumulator layout (length 1 + 6K + Σ_rbf (4 n_r + 4), K = surfaces):
  *       accum[0]            = Σ_p d*(p)^2                     (cost, no regularizer)
  *       accum[1+6k+0..2]    = Σ_{p: k*(p)=k} 2 d*(p) ∇d*(p)   (force-like, world)
  *       accum[1+6k+3..5]    = Σ_{p: k*(p)=k} 2 d*(p) p × ∇d*(p) (moment about origin)
- *     so that for a world twist (ω, v) of hull k:  δc = -(ω·M_k + v·F_k).
+ *     so that for a world twist (ω, v) of hull k:  δc = -(ω·M_k + v·F_k)
+ *     (zero for RBF surfaces); then per RBF surface r with n_r centres, over
+ *     the points with k* = r:
+ *       λ_w[n_r], λ_a, λ_b[3]  = Σ 2 s ∂s/∂(w, a, b)
+ *       E[n_r][3]              = Σ 2 s ∂s/∂c_i (coefficients held fixed)
+ *     from which the host forms dc/dc_i = E_i − μᵀ(∂M/∂c_i)u, μ = M⁻ᵀλ.
  *   - Nearest-primitive index k*(p) is the FIRST k attaining the minimum,
  *     matching Julia's left-fold `minimum` (src/Flash.jl:267).
  *   - The library never falls back to a CPU path: without a usable gfx950
@@ -78,6 +83,23 @@ typedef struct fsdf_hull {
   const double* planes;   /* [n_faces][4] = (n, d), |n| = 1, n·x <= d inside      */
 } fsdf_hull;
 
+/* A scene surface, in the reference's surface order (Manipulator.surfaces,
+ * src/Flash.jl:62-65): k* indexes this list.
+ *   FSDF_SURFACE_HULL: a convex primitive (`hull`), posed by poses[k].
+ *   FSDF_SURFACE_RBF:  an interpolating skin (src/Flash.jl:207-213) over
+ *                      `n_centers` centres; its world centres and RBF
+ *                      coefficients are supplied per pass (fsdf_set_rbf_params),
+ *                      its pose is ignored. Value: s = f/|∇f| with
+ *                      f(x) = Σ w_i |x-c_i|^3 + a + b·x (XCubed + affine;
+ *                      pinned by test/runtests.jl:17). */
+#define FSDF_SURFACE_HULL 0
+#define FSDF_SURFACE_RBF 1
+typedef struct fsdf_surface {
+  int32_t kind;      /* FSDF_SURFACE_HULL or FSDF_SURFACE_RBF */
+  int32_t n_centers; /* RBF only */
+  fsdf_hull hull;    /* HULL only */
+} fsdf_surface;
+
 /* ---- geometry ingest (host only, no device needed) --------------------------
  * Convex hull of a point set (the shape GJK's support function sees,
  * EnhancedGJK.NeighborMesh over the mesh vertices, src/models.jl:152).
@@ -94,11 +116,20 @@ const char* fsdf_last_error(const fsdf_ctx* ctx);
 /* Launch on a caller-owned hipStream_t (NULL = the context's own stream). */
 int fsdf_set_stream(fsdf_ctx* ctx, void* hip_stream);
 int fsdf_num_hulls(const fsdf_ctx* ctx, int32_t* k_out);
-int fsdf_accum_len(const fsdf_ctx* ctx, int32_t* len_out); /* 1 + 6K */
+int fsdf_accum_len(const fsdf_ctx* ctx, int32_t* len_out); /* 1 + 6K + Σ(4n+4) */
 
 /* Upload the model once (per model). Replaces the per-evaluation
- * CollisionCache construction of src/Flash.jl:246. */
+ * CollisionCache construction of src/Flash.jl:246. fsdf_set_model is the
+ * hull-only form of fsdf_set_surfaces. */
 int fsdf_set_model(fsdf_ctx* ctx, const fsdf_hull* hulls, int32_t n_hulls);
+int fsdf_set_surfaces(fsdf_ctx* ctx, const fsdf_surface* surfaces, int32_t n_surfaces);
+
+/* Per-pass RBF parameters (before fsdf_eval / fsdf_skin when the scene has RBF
+ * surfaces): for every RBF surface in surface order, n_centers rows
+ * (c_x, c_y, c_z, w) in the world frame, then one row (a, b_x, b_y, b_z).
+ * n_doubles must equal 4·Σ(n_centers + 1). The host solves the (n+4)² system
+ * [A P; Pᵀ 0][w; a; b] = [v; 0] (surface points v = 0, skeleton v = -1). */
+int fsdf_set_rbf_params(fsdf_ctx* ctx, const double* params, int64_t n_doubles);
 
 /* Upload the sensed cloud once per frame (src/gradientdescent.jl:43 holds it
  * by reference across every cost evaluation). */

@@ -17,6 +17,9 @@
  *         estimate, replaced here by the exact value — DESIGN.md §2).
  *   pose of a surface = transform_to_root(state, frame)       src/Flash.jl:248
  *       given as R|t per hull; world planes/vertices          -> oracle_pose_model
+ *   s(x) for InterpolatingGeometry = SpatialFields surface     src/Flash.jl:207-213
+ *       restated as f/|∇f| of the XCubed + affine RBF fit    -> oracle_rbf_skin
+ *       (pinned by test/runtests.jl:17, see oracle/rbf.py)
  *   cost = Σ_p skin(p)^2                                      src/gradientdescent.jl:32
  *       plus the per-hull wrench sums that carry ∂cost/∂pose   -> oracle_cost_accum
  *
@@ -108,9 +111,10 @@ void oracle_pose_model(int32_t F, int32_t V, int32_t K, const double* verts_l, c
   }
 }
 
-/* The posed model as the kernel sees it. */
+/* The posed model as the kernel sees it. Surfaces (the k* index space) are
+ * hulls or RBF skins: surf_index[k] = hull index (>= 0) or -(rbf index) - 1. */
 typedef struct {
-  int32_t K;
+  int32_t K; /* hulls */
   const int32_t* face_off;
   const int32_t* vert_off;
   const int32_t* nbr;
@@ -118,7 +122,88 @@ typedef struct {
   const double* facex_w;
   const double* verts_w;
   const double* hscale;
+  int32_t S; /* surfaces */
+  const int32_t* surf_index;
+  const int32_t* rbf_row_off; /* [R+1] rows (n centres + 1 polynomial row) */
+  const int32_t* rbf_acc_off; /* [R+1] offsets in the RBF accumulator block */
+  const double* rbf_rows;     /* [rows][4]: (c, w) ... then (a, b) */
 } oracle_posed;
+
+/* RBF interpolating skin (src/Flash.jl:207-213, SpatialFields XCubed + affine):
+ * f(x) = Σ w_i |x-c_i|^3 + a + b·x, s = f/|∇f|, ∇s = ∇f/|∇f| − f H∇f/|∇f|^3.
+ * F = {f, gx, gy, gz, hxx, hyy, hzz, hxy, hxz, hyz}; same order as the kernel. */
+static void rbf_field(const double* rows, int nc, const double* p, double* F) {
+  const double* poly = rows + 4 * nc;
+  F[0] = fma(poly[1], p[0], fma(poly[2], p[1], fma(poly[3], p[2], poly[0])));
+  F[1] = poly[1]; F[2] = poly[2]; F[3] = poly[3];
+  for (int j = 4; j < 10; ++j) F[j] = 0.0;
+  for (int i = 0; i < nc; ++i) {
+    const double* c = rows + 4 * i;
+    const double dx = p[0] - c[0], dy = p[1] - c[1], dz = p[2] - c[2];
+    const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
+    const double r = sqrt(r2);
+    const double wr = c[3] * r;
+    F[0] = fma(wr, r2, F[0]);
+    const double t3 = 3.0 * wr;
+    F[1] = fma(t3, dx, F[1]); F[2] = fma(t3, dy, F[2]); F[3] = fma(t3, dz, F[3]);
+    const double hq = r2 > 0 ? (3.0 * c[3]) / r : 0.0;
+    F[4] = fma(hq * dx, dx, F[4] + t3);
+    F[5] = fma(hq * dy, dy, F[5] + t3);
+    F[6] = fma(hq * dz, dz, F[6] + t3);
+    F[7] = fma(hq * dx, dy, F[7]);
+    F[8] = fma(hq * dx, dz, F[8]);
+    F[9] = fma(hq * dy, dz, F[9]);
+  }
+}
+
+static void rbf_skin_from_field(const double* F, double* s, double* g, double* c, double* invG) {
+  const double G2 = fma(F[1], F[1], fma(F[2], F[2], F[3] * F[3]));
+  const double G = sqrt(G2);
+  *s = F[0] / G;
+  *invG = 1.0 / G;
+  *c = F[0] / (G2 * G);
+  const double hgx = fma(F[4], F[1], fma(F[7], F[2], F[8] * F[3]));
+  const double hgy = fma(F[7], F[1], fma(F[5], F[2], F[9] * F[3]));
+  const double hgz = fma(F[8], F[1], fma(F[9], F[2], F[6] * F[3]));
+  g[0] = fma(-*c, hgx, F[1] * *invG);
+  g[1] = fma(-*c, hgy, F[2] * *invG);
+  g[2] = fma(-*c, hgz, F[3] * *invG);
+}
+
+void oracle_rbf_skin(const double* rows, int32_t nc, const double* p, double* s, double* g) {
+  double F[10], c, invG;
+  rbf_field(rows, nc, p, F);
+  rbf_skin_from_field(F, s, g, &c, &invG);
+}
+
+/* adds 2s ∂s/∂(w, a, b) and 2s ∂s/∂c_i (coefficients fixed) into acc:
+ * acc[0..n) λ_w, acc[n] λ_a, acc[n+1..n+4) λ_b, acc[n+4+3i..] E_i */
+static void rbf_adjoint(const double* rows, int nc, const double* p, double* acc) {
+  double F[10], s, g[3], c, invG;
+  rbf_field(rows, nc, p, F);
+  rbf_skin_from_field(F, &s, g, &c, &invG);
+  const double two_s = 2.0 * s, dsdf = invG;
+  const double ux = -c * F[1], uy = -c * F[2], uz = -c * F[3];
+  for (int i = 0; i < nc; ++i) {
+    const double* cw = rows + 4 * i;
+    const double dx = p[0] - cw[0], dy = p[1] - cw[1], dz = p[2] - cw[2];
+    const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
+    const double r = sqrt(r2);
+    const double e = fma(dx, ux, fma(dy, uy, dz * uz));
+    acc[i] += two_s * fma(dsdf * r2, r, 3.0 * r * e);
+    const double k1 = fma(3.0 * r, dsdf, r2 > 0 ? (3.0 * e) / r : 0.0);
+    const double k2 = 3.0 * r;
+    const double sc = -two_s * cw[3];
+    double* E = acc + nc + 4 + 3 * i;
+    E[0] += sc * fma(k1, dx, k2 * ux);
+    E[1] += sc * fma(k1, dy, k2 * uy);
+    E[2] += sc * fma(k1, dz, k2 * uz);
+  }
+  acc[nc] += two_s * dsdf;
+  acc[nc + 1] += two_s * fma(dsdf, p[0], ux);
+  acc[nc + 2] += two_s * fma(dsdf, p[1], uy);
+  acc[nc + 3] += two_s * fma(dsdf, p[2], uz);
+}
 
 /* Closest point on triangle v = (a, b, c) to p, Voronoi-region walk. */
 static void closest_on_triangle(const double* p, const double* v, double* q) {
@@ -259,9 +344,15 @@ void oracle_hull_sdf(const oracle_posed* m, int32_t k, const double* p, double* 
 static void skin_one(const oracle_posed* m, const double* p, double* d, int32_t* k, double* g) {
   double best = INFINITY, gb[3] = {0, 0, 0};
   int32_t bk = 0;
-  for (int32_t kk = 0; kk < m->K; ++kk) {
+  for (int32_t kk = 0; kk < m->S; ++kk) {
     double dk, gk[3];
-    oracle_hull_sdf(m, kk, p, &dk, gk);
+    const int32_t si = m->surf_index[kk];
+    if (si >= 0) {
+      oracle_hull_sdf(m, si, p, &dk, gk);
+    } else {
+      const int r = -si - 1, r0 = m->rbf_row_off[r];
+      oracle_rbf_skin(m->rbf_rows + 4 * r0, m->rbf_row_off[r + 1] - r0 - 1, p, &dk, gk);
+    }
     if (dk < best) { best = dk; bk = kk; gb[0] = gk[0]; gb[1] = gk[1]; gb[2] = gk[2]; }
   }
   *d = best;
@@ -292,13 +383,23 @@ void oracle_skin(const oracle_posed* m, const double* pts, int64_t n, double* d_
  * Serial in point order (the reference's `sum` is pairwise; both agree to
  * rounding, compared at 1e-9 relative). */
 void oracle_cost_accum(const oracle_posed* m, const double* pts, int64_t n, double* accum) {
-  memset(accum, 0, sizeof(double) * (size_t)(1 + 6 * m->K));
+  int32_t R = 0;
+  for (int32_t kk = 0; kk < m->S; ++kk) R += m->surf_index[kk] < 0;
+  const int32_t len = 1 + 6 * m->S + (R ? m->rbf_acc_off[R] : 0);
+  memset(accum, 0, sizeof(double) * (size_t)len);
   for (int64_t i = 0; i < n; ++i) {
     const double* p = pts + 3 * i;
     double d, g[3];
     int32_t k;
     skin_one(m, p, &d, &k, g);
     accum[0] = fma(d, d, accum[0]);
+    const int32_t si = m->surf_index[k];
+    if (si < 0) {
+      const int r = -si - 1, r0 = m->rbf_row_off[r];
+      rbf_adjoint(m->rbf_rows + 4 * r0, m->rbf_row_off[r + 1] - r0 - 1, p,
+                  accum + 1 + 6 * m->S + m->rbf_acc_off[r]);
+      continue;
+    }
     const double w = 2.0 * d;
     double* a = accum + 1 + 6 * k;
     a[0] += w * g[0];

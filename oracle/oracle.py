@@ -34,7 +34,9 @@ def build():
 
 class Posed(ctypes.Structure):
     _fields_ = [("K", c_int32), ("face_off", c_void_p), ("vert_off", c_void_p), ("nbr", c_void_p),
-                ("planes_w", c_void_p), ("facex_w", c_void_p), ("verts_w", c_void_p), ("hscale", c_void_p)]
+                ("planes_w", c_void_p), ("facex_w", c_void_p), ("verts_w", c_void_p), ("hscale", c_void_p),
+                ("S", c_int32), ("surf_index", c_void_p), ("rbf_row_off", c_void_p), ("rbf_acc_off", c_void_p),
+                ("rbf_rows", c_void_p)]
 
 
 def load():
@@ -47,6 +49,7 @@ def load():
         lib.oracle_hull_sdf.argtypes = [ctypes.POINTER(Posed), c_int32, c_void_p, c_void_p, c_void_p]
         lib.oracle_skin.argtypes = [ctypes.POINTER(Posed), c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int32]
         lib.oracle_cost_accum.argtypes = [ctypes.POINTER(Posed), c_void_p, c_int64, c_void_p]
+        lib.oracle_rbf_skin.argtypes = [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]
         lib.oracle_max_threads.restype = c_int32
         _lib = lib
     return _lib
@@ -70,8 +73,11 @@ def face_neighbours(faces, fbase):
 
 
 class OracleModel:
-    def __init__(self, hulls):
-        """hulls: list of (vertices, faces, planes) in local frames."""
+    def __init__(self, hulls, surfaces=None):
+        """hulls: list of (vertices, faces, planes) in local frames; surfaces:
+        optional scene order [("hull", h) | ("rbf", n_centres)] (default: hulls only)."""
+        if surfaces is None:
+            surfaces = [("hull", i) for i in range(len(hulls))]
         V, Fc, P, FH, VH, NB, off, voff = [], [], [], [], [], [], [0], [0]
         vbase = 0
         for k, (v, f, p) in enumerate(hulls):
@@ -85,40 +91,69 @@ class OracleModel:
             voff.append(voff[-1] + len(v))
             vbase += len(v)
         self.K = len(hulls)
-        self.verts_l = np.ascontiguousarray(np.concatenate(V))
-        self.faces = np.ascontiguousarray(np.concatenate(Fc))
-        self.planes_l = np.ascontiguousarray(np.concatenate(P))
-        self.face_hull = np.ascontiguousarray(np.concatenate(FH))
-        self.vert_hull = np.ascontiguousarray(np.concatenate(VH))
-        self.nbr = np.ascontiguousarray(np.concatenate(NB))
+        cat = lambda xs, dt: np.ascontiguousarray(np.concatenate(xs) if xs else np.zeros((0,), dt))  # noqa: E731
+        self.verts_l = cat(V, np.float64).reshape(-1, 3)
+        self.faces = cat(Fc, np.int32).reshape(-1, 3)
+        self.planes_l = cat(P, np.float64).reshape(-1, 4)
+        self.face_hull = cat(FH, np.int32)
+        self.vert_hull = cat(VH, np.int32)
+        self.nbr = cat(NB, np.int32).reshape(-1, 3)
         self.face_off = np.asarray(off, np.int32)
         self.vert_off = np.asarray(voff, np.int32)
         self.F = len(self.face_hull)
         self.V = len(self.vert_hull)
         self.hulls = hulls
+        # surface table
+        self.S = len(surfaces)
+        si, rows, acc, hk, self.hull_surface = [], [0], [0], 0, []
+        for k, (kind, spec) in enumerate(surfaces):
+            if kind == "hull":
+                si.append(hk)
+                self.hull_surface.append(k)
+                hk += 1
+            else:
+                si.append(-(len(rows) - 1) - 1)
+                rows.append(rows[-1] + int(spec) + 1)
+                acc.append(acc[-1] + 4 * int(spec) + 4)
+        self.surf_index = np.asarray(si, np.int32)
+        self.rbf_row_off = np.asarray(rows, np.int32)
+        self.rbf_acc_off = np.asarray(acc, np.int32)
+        self.accum_len = 1 + 6 * self.S + int(self.rbf_acc_off[-1])
 
     @staticmethod
     def from_manipulator(manip):
-        return OracleModel([(s.hull.vertices, s.hull.faces, s.hull.planes) for s in manip.convex_surfaces()])
+        from flash.core import ConvexGeometry
+        hulls, surfaces = [], []
+        for s in manip.surfaces:
+            if isinstance(s, ConvexGeometry):
+                surfaces.append(("hull", len(hulls)))
+                hulls.append((s.hull.vertices, s.hull.faces, s.hull.planes))
+            else:
+                surfaces.append(("rbf", len(s.surface_points) + len(s.skeleton_points)))
+        return OracleModel(hulls, surfaces)
 
-    def pose(self, poses):
-        """World-frame model arrays for `poses` ([K,12])."""
-        poses = np.ascontiguousarray(poses, np.float64).reshape(self.K, 12)
-        pw = np.empty((self.F, 4))
-        fx = np.empty((self.F, FX))
-        vw = np.empty((self.V, 4))
-        hs = np.empty(self.K)
+    def pose(self, poses, rbf_rows=None):
+        """World-frame model arrays for `poses` ([S,12], one per surface)."""
+        poses = np.ascontiguousarray(poses, np.float64).reshape(self.S, 12)
+        hp = np.ascontiguousarray(poses[self.hull_surface]) if self.K else np.zeros((1, 12))
+        pw = np.empty((max(self.F, 1), 4))
+        fx = np.empty((max(self.F, 1), FX))
+        vw = np.empty((max(self.V, 1), 4))
+        hs = np.empty(max(self.K, 1))
         load().oracle_pose_model(self.F, self.V, self.K, _p(self.verts_l), _p(self.faces), _p(self.planes_l),
-                                 _p(self.face_hull), _p(self.vert_hull), _p(self.vert_off), _p(poses), _p(pw),
+                                 _p(self.face_hull), _p(self.vert_hull), _p(self.vert_off), _p(hp), _p(pw),
                                  _p(fx), _p(vw), _p(hs))
-        arrays = (pw, fx, vw, hs)
+        rr = np.ascontiguousarray(rbf_rows if rbf_rows is not None else np.zeros((1, 4)), np.float64)
+        arrays = (pw, fx, vw, hs, rr)
         st = Posed(self.K, self.face_off.ctypes.data, self.vert_off.ctypes.data, self.nbr.ctypes.data,
-                   pw.ctypes.data, fx.ctypes.data, vw.ctypes.data, hs.ctypes.data)
+                   pw.ctypes.data, fx.ctypes.data, vw.ctypes.data, hs.ctypes.data, self.S,
+                   self.surf_index.ctypes.data, self.rbf_row_off.ctypes.data, self.rbf_acc_off.ctypes.data,
+                   rr.ctypes.data)
         return st, arrays
 
-    def skin(self, poses, pts, threads: int = 0):
+    def skin(self, poses, pts, threads: int = 0, rbf_rows=None):
         pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
-        st, _keep = self.pose(poses)
+        st, _keep = self.pose(poses, rbf_rows)
         n = len(pts)
         d = np.empty(n)
         k = np.empty(n, np.int32)
@@ -126,10 +161,10 @@ class OracleModel:
         load().oracle_skin(ctypes.byref(st), _p(pts), n, _p(d), _p(k), _p(g), threads)
         return d, k, g
 
-    def cost_accum(self, poses, pts):
+    def cost_accum(self, poses, pts, rbf_rows=None):
         pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
-        st, _keep = self.pose(poses)
-        acc = np.empty(1 + 6 * self.K)
+        st, _keep = self.pose(poses, rbf_rows)
+        acc = np.empty(self.accum_len)
         load().oracle_cost_accum(ctypes.byref(st), _p(pts), len(pts), _p(acc))
         return acc
 

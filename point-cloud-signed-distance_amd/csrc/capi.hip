@@ -60,6 +60,14 @@ struct fsdf_ctx {
   int32_t* d_vert_hull = nullptr;
   int32_t* d_vert_off = nullptr;
   int32_t* d_face_nbr = nullptr;
+  int32_t* d_hull_surface = nullptr;
+  int32_t* d_surface_kind = nullptr;
+  int32_t* d_rbf_surface = nullptr;
+  int32_t* d_rbf_row_off = nullptr;
+  int32_t* d_rbf_acc_off = nullptr;
+  double* d_rbf64 = nullptr;     // per-pass RBF rows (f64)
+  double* h_rbf[kPoseRing] = {}; // pinned staging ring for RBF rows
+  bool rbf_ready = false;
   // posed model
   fsdf::PosedModel pm;
   // poses: pinned ring + device copy
@@ -121,6 +129,19 @@ static void free_model(fsdf_ctx* c) {
   dfree(c->d_vert_hull);
   dfree(c->d_vert_off);
   dfree(c->d_face_nbr);
+  dfree(c->d_hull_surface);
+  dfree(c->d_surface_kind);
+  dfree(c->d_rbf_surface);
+  dfree(c->d_rbf_row_off);
+  dfree(c->d_rbf_acc_off);
+  if (c->pm.rbf_rows != (void*)c->d_rbf64) dfree(c->pm.rbf_rows);
+  c->pm.rbf_rows = nullptr;
+  dfree(c->d_rbf64);
+  for (int i = 0; i < kPoseRing; ++i) {
+    if (c->h_rbf[i]) (void)hipHostFree(c->h_rbf[i]);
+    c->h_rbf[i] = nullptr;
+  }
+  c->rbf_ready = false;
   dfree(c->pm.verts_w);
   dfree(c->pm.hscale_w);
   dfree(c->pm.planes_w);
@@ -198,13 +219,15 @@ extern "C" int fsdf_set_stream(fsdf_ctx* c, void* s) {
 
 extern "C" int fsdf_num_hulls(const fsdf_ctx* c, int32_t* k) {
   if (!c || !k) return FSDF_ERR_ARG;
-  *k = c->lm.K;
+  *k = c->lm.S;  // surfaces of every kind = poses expected per pass
   return FSDF_OK;
 }
 
+static int accum_len(const fsdf_ctx* c) { return 1 + 6 * c->lm.S + c->lm.rbf_acc; }
+
 extern "C" int fsdf_accum_len(const fsdf_ctx* c, int32_t* len) {
   if (!c || !len) return FSDF_ERR_ARG;
-  *len = 1 + 6 * c->lm.K;
+  *len = accum_len(c);
   return FSDF_OK;
 }
 
@@ -214,16 +237,36 @@ extern "C" int fsdf_num_points(const fsdf_ctx* c, int64_t* n) {
   return FSDF_OK;
 }
 
-extern "C" int fsdf_set_model(fsdf_ctx* c, const fsdf_hull* hulls, int32_t K) {
+extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t S) {
   if (!c) return FSDF_ERR_ARG;
-  if (!hulls || K < 1) return fail(c, FSDF_ERR_ARG, "set_model: need at least one hull");
-  if (K > fsdf::kMaxHulls) return fail(c, FSDF_ERR_ARG, "set_model: %d hulls exceeds the limit %d", K, fsdf::kMaxHulls);
+  if (!surfs || S < 1) return fail(c, FSDF_ERR_ARG, "set_surfaces: need at least one surface");
+  if (S > fsdf::kMaxHulls) return fail(c, FSDF_ERR_ARG, "set_surfaces: %d surfaces exceeds the limit %d", S, fsdf::kMaxHulls);
+  std::vector<fsdf_hull> hulls;
+  std::vector<int32_t> hull_surface, surface_kind, rbf_surface, rbf_row_off{0}, rbf_acc_off{0};
+  for (int k = 0; k < S; ++k) {
+    surface_kind.push_back(surfs[k].kind);
+    if (surfs[k].kind == FSDF_SURFACE_HULL) {
+      hulls.push_back(surfs[k].hull);
+      hull_surface.push_back(k);
+    } else if (surfs[k].kind == FSDF_SURFACE_RBF) {
+      if (surfs[k].n_centers < 1) return fail(c, FSDF_ERR_ARG, "set_surfaces: RBF surface %d has no centres", k);
+      rbf_surface.push_back(k);
+      rbf_row_off.push_back(rbf_row_off.back() + surfs[k].n_centers + 1);
+      rbf_acc_off.push_back(rbf_acc_off.back() + 4 * surfs[k].n_centers + 4);
+    } else {
+      return fail(c, FSDF_ERR_ARG, "set_surfaces: surface %d has unknown kind %d", k, surfs[k].kind);
+    }
+  }
+  if (rbf_acc_off.back() > fsdf::kMaxRbfAccum)
+    return fail(c, FSDF_ERR_ARG, "set_surfaces: RBF skins need %d accumulators, limit %d", rbf_acc_off.back(),
+                fsdf::kMaxRbfAccum);
+  const int K = (int)hulls.size();
   std::vector<double> verts, planes, sph;
   std::vector<int32_t> faces, face_hull, face_off, vert_hull, vert_off, face_nbr;
   face_off.push_back(0);
   vert_off.push_back(0);
   for (int k = 0; k < K; ++k) {
-    const fsdf_hull& h = hulls[k];
+    const fsdf_hull& h = hulls[(size_t)k];
     if (h.n_vertices < 4 || h.n_faces < 4 || !h.vertices || !h.faces)
       return fail(c, FSDF_ERR_ARG, "set_model: hull %d has %d vertices / %d faces", k, h.n_vertices, h.n_faces);
     const int vbase = (int)(verts.size() / 3);
@@ -311,11 +354,37 @@ extern "C" int fsdf_set_model(fsdf_ctx* c, const fsdf_hull* hulls, int32_t K) {
   HIPCHECK(c, dalloc(&c->d_face_nbr, face_nbr.size() * sizeof(int32_t)));
   HIPCHECK(c, dalloc((char**)&c->pm.verts_w, (size_t)V * 4 * tsz));
   HIPCHECK(c, dalloc((char**)&c->pm.hscale_w, (size_t)K * tsz));
-  HIPCHECK(c, dalloc((char**)&c->pm.planes_w, (size_t)F * 4 * tsz));
+  HIPCHECK(c, dalloc((char**)&c->pm.planes_w, (size_t)std::max(F, 1) * 4 * tsz));
   HIPCHECK(c, dalloc((char**)&c->pm.facex_w, (size_t)F * fsdf::kFaceX * tsz));
   HIPCHECK(c, dalloc(&c->pm.spheres_w, (size_t)K * 4 * sizeof(float)));
-  HIPCHECK(c, dalloc(&c->d_poses, (size_t)K * 12 * sizeof(double)));
-  HIPCHECK(c, dalloc(&c->d_accum, (size_t)(1 + 6 * K) * sizeof(double)));
+  HIPCHECK(c, dalloc(&c->d_poses, (size_t)S * 12 * sizeof(double)));
+  const int R = (int)rbf_surface.size();
+  HIPCHECK(c, dalloc(&c->d_accum, (size_t)(1 + 6 * S + rbf_acc_off.back()) * sizeof(double)));
+  HIPCHECK(c, dalloc(&c->d_hull_surface, std::max<size_t>(1, hull_surface.size()) * sizeof(int32_t)));
+  HIPCHECK(c, dalloc(&c->d_surface_kind, surface_kind.size() * sizeof(int32_t)));
+  HIPCHECK(c, dalloc(&c->d_rbf_surface, std::max<size_t>(1, rbf_surface.size()) * sizeof(int32_t)));
+  HIPCHECK(c, dalloc(&c->d_rbf_row_off, rbf_row_off.size() * sizeof(int32_t)));
+  HIPCHECK(c, dalloc(&c->d_rbf_acc_off, rbf_acc_off.size() * sizeof(int32_t)));
+  if (!hull_surface.empty())
+    HIPCHECK(c, hipMemcpy(c->d_hull_surface, hull_surface.data(), hull_surface.size() * sizeof(int32_t),
+                          hipMemcpyHostToDevice));
+  HIPCHECK(c, hipMemcpy(c->d_surface_kind, surface_kind.data(), surface_kind.size() * sizeof(int32_t),
+                        hipMemcpyHostToDevice));
+  if (R > 0)
+    HIPCHECK(c, hipMemcpy(c->d_rbf_surface, rbf_surface.data(), rbf_surface.size() * sizeof(int32_t),
+                          hipMemcpyHostToDevice));
+  HIPCHECK(c, hipMemcpy(c->d_rbf_row_off, rbf_row_off.data(), rbf_row_off.size() * sizeof(int32_t),
+                        hipMemcpyHostToDevice));
+  HIPCHECK(c, hipMemcpy(c->d_rbf_acc_off, rbf_acc_off.data(), rbf_acc_off.size() * sizeof(int32_t),
+                        hipMemcpyHostToDevice));
+  const int nrows = rbf_row_off.back();
+  if (R > 0) {
+    HIPCHECK(c, dalloc(&c->d_rbf64, (size_t)nrows * 4 * sizeof(double)));
+    if (c->precision == 64) c->pm.rbf_rows = c->d_rbf64;
+    else HIPCHECK(c, dalloc((char**)&c->pm.rbf_rows, (size_t)nrows * 4 * sizeof(float)));
+    for (int i = 0; i < kPoseRing; ++i)
+      HIPCHECK(c, hipHostMalloc((void**)&c->h_rbf[i], (size_t)nrows * 4 * sizeof(double), hipHostMallocDefault));
+  }
   HIPCHECK(c, hipMemcpy(c->d_verts_l, verts.data(), verts.size() * sizeof(double), hipMemcpyHostToDevice));
   HIPCHECK(c, hipMemcpy(c->d_faces, faces.data(), faces.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   HIPCHECK(c, hipMemcpy(c->d_planes_l, planes.data(), planes.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -328,7 +397,7 @@ extern "C" int fsdf_set_model(fsdf_ctx* c, const fsdf_hull* hulls, int32_t K) {
   for (int i = 0; i < kPoseRing; ++i) {
     if (c->h_poses[i]) (void)hipHostFree(c->h_poses[i]);
     c->h_poses[i] = nullptr;
-    HIPCHECK(c, hipHostMalloc((void**)&c->h_poses[i], (size_t)K * 12 * sizeof(double), hipHostMallocDefault));
+    HIPCHECK(c, hipHostMalloc((void**)&c->h_poses[i], (size_t)S * 12 * sizeof(double), hipHostMallocDefault));
     if (!c->pose_ev[i]) HIPCHECK(c, hipEventCreateWithFlags(&c->pose_ev[i], hipEventDisableTiming));
   }
   c->lm.K = K;
@@ -343,6 +412,44 @@ extern "C" int fsdf_set_model(fsdf_ctx* c, const fsdf_hull* hulls, int32_t K) {
   c->lm.vert_hull = c->d_vert_hull;
   c->lm.vert_off = c->d_vert_off;
   c->lm.face_nbr = c->d_face_nbr;
+  c->lm.S = S;
+  c->lm.R = R;
+  c->lm.rbf_rows = nrows;
+  c->lm.rbf_acc = rbf_acc_off.back();
+  c->lm.hull_surface = c->d_hull_surface;
+  c->lm.surface_kind = c->d_surface_kind;
+  c->lm.rbf_surface = c->d_rbf_surface;
+  c->lm.rbf_row_off = c->d_rbf_row_off;
+  c->lm.rbf_acc_off = c->d_rbf_acc_off;
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_set_model(fsdf_ctx* c, const fsdf_hull* hulls, int32_t K) {
+  if (!c) return FSDF_ERR_ARG;
+  if (!hulls || K < 1) return fail(c, FSDF_ERR_ARG, "set_model: need at least one hull");
+  std::vector<fsdf_surface> s((size_t)K);
+  for (int k = 0; k < K; ++k) {
+    s[(size_t)k].kind = FSDF_SURFACE_HULL;
+    s[(size_t)k].n_centers = 0;
+    s[(size_t)k].hull = hulls[k];
+  }
+  return fsdf_set_surfaces(c, s.data(), K);
+}
+
+extern "C" int fsdf_set_rbf_params(fsdf_ctx* c, const double* params, int64_t n) {
+  if (!c) return FSDF_ERR_ARG;
+  if (c->lm.R == 0) return fail(c, FSDF_ERR_STATE, "set_rbf_params: the scene has no RBF surface");
+  if (!params || n != 4LL * c->lm.rbf_rows)
+    return fail(c, FSDF_ERR_ARG, "set_rbf_params: expected %d doubles, got %lld", 4 * c->lm.rbf_rows, (long long)n);
+  for (int64_t i = 0; i < n; ++i)
+    if (!std::isfinite(params[i])) return fail(c, FSDF_ERR_ARG, "set_rbf_params: entry %lld not finite", (long long)i);
+  HIPCHECK(c, hipSetDevice(c->device));
+  const int sl = c->pose_slot;  // shares the pose ring's slot/event (one upload pair per pass)
+  HIPCHECK(c, hipEventSynchronize(c->pose_ev[sl]));
+  memcpy(c->h_rbf[sl], params, (size_t)n * sizeof(double));
+  HIPCHECK(c, hipMemcpyAsync(c->d_rbf64, c->h_rbf[sl], (size_t)n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  if (c->precision != 64) HIPCHECK(c, fsdf::launch_to_f32(c->d_rbf64, (float*)c->pm.rbf_rows, n, c->stream));
+  c->rbf_ready = true;
   return FSDF_OK;
 }
 
@@ -418,7 +525,7 @@ extern "C" int fsdf_set_points_device(fsdf_ctx* c, const double* d_xyz, int64_t 
 }
 
 static int ensure_partials(fsdf_ctx* c, int nblocks) {
-  const size_t need = (size_t)(1 + 6 * c->lm.K) * nblocks;
+  const size_t need = (size_t)accum_len(c) * nblocks;
   if (c->partials_cap < need) {
     dfree(c->d_partials);
     c->partials_cap = 0;
@@ -429,13 +536,13 @@ static int ensure_partials(fsdf_ctx* c, int nblocks) {
 }
 
 static int upload_poses(fsdf_ctx* c, const double* poses) {
-  for (int i = 0; i < 12 * c->lm.K; ++i)
+  for (int i = 0; i < 12 * c->lm.S; ++i)
     if (!std::isfinite(poses[i])) return fail(c, FSDF_ERR_ARG, "poses: entry %d is not finite", i);
   const int s = c->pose_slot;
   c->pose_slot = (s + 1) % kPoseRing;
   HIPCHECK(c, hipEventSynchronize(c->pose_ev[s]));  // slot free once its last copy ran
-  memcpy(c->h_poses[s], poses, (size_t)c->lm.K * 12 * sizeof(double));
-  HIPCHECK(c, hipMemcpyAsync(c->d_poses, c->h_poses[s], (size_t)c->lm.K * 12 * sizeof(double),
+  memcpy(c->h_poses[s], poses, (size_t)c->lm.S * 12 * sizeof(double));
+  HIPCHECK(c, hipMemcpyAsync(c->d_poses, c->h_poses[s], (size_t)c->lm.S * 12 * sizeof(double),
                              hipMemcpyHostToDevice, c->stream));
   HIPCHECK(c, hipEventRecord(c->pose_ev[s], c->stream));
   return FSDF_OK;
@@ -443,6 +550,8 @@ static int upload_poses(fsdf_ctx* c, const double* poses) {
 
 static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t n, double* d_accum,
                     int32_t* d_kstar, double* d_d, double* d_grad, const int64_t* d_perm) {
+  if (c->lm.R > 0 && !c->rbf_ready)
+    return fail(c, FSDF_ERR_STATE, "eval: the scene has RBF surfaces: call fsdf_set_rbf_params first");
   int rc = upload_poses(c, poses);
   if (rc) return rc;
   HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, c->d_poses, c->pm, c->stream));
@@ -464,9 +573,9 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
       HIPCHECK(c, hipEventRecord(c->prof_ev[c->prof_used + 1], c->stream));
       c->prof_used += 2;
     }
-    HIPCHECK(c, fsdf::launch_reduce(c->d_partials, nblocks, 1 + 6 * c->lm.K, d_accum, c->stream));
+    HIPCHECK(c, fsdf::launch_reduce(c->d_partials, nblocks, accum_len(c), d_accum, c->stream));
   } else {
-    HIPCHECK(c, hipMemsetAsync(d_accum, 0, (size_t)(1 + 6 * c->lm.K) * sizeof(double), c->stream));
+    HIPCHECK(c, hipMemsetAsync(d_accum, 0, (size_t)accum_len(c) * sizeof(double), c->stream));
   }
   return FSDF_OK;
 }
@@ -495,7 +604,7 @@ static int ensure_outputs(fsdf_ctx* c, int64_t n) {
 
 static int fetch(fsdf_ctx* c, int64_t n, double* cost_out, double* accum_out, int32_t* kstar_out, double* d_out,
                  double* grad_out, bool want_pp) {
-  const int len = 1 + 6 * c->lm.K;
+  const int len = accum_len(c);
   std::vector<double> acc(len);
   HIPCHECK(c, hipMemcpyAsync(acc.data(), c->d_accum, len * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   if (want_pp && n > 0) {

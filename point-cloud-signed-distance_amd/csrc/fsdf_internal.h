@@ -31,9 +31,18 @@ constexpr int kBlock = 256;        // 4 waves of 64
 constexpr int kFaceX = 24;         // stride of facex_w rows
 constexpr int kMaxHulls = 256;     // 4 accumulator slots per lane
 constexpr int kMaxBlocks = 2048;
+constexpr int kMaxRbfAccum = 512;  // Σ (4n+4) over RBF skins (= kMaxRbfAcc in the kernel)
 
 struct LocalModel {
-  int K = 0, F = 0, V = 0;
+  int K = 0, F = 0, V = 0;   // K = convex hulls
+  int S = 0, R = 0;          // surfaces (k* index space), RBF skins
+  int rbf_rows = 0;          // Σ (n_centres + 1)
+  int rbf_acc = 0;           // Σ (4 n_centres + 4)
+  const int32_t* hull_surface = nullptr;  // [K]
+  const int32_t* surface_kind = nullptr;  // [S]
+  const int32_t* rbf_surface = nullptr;   // [R]
+  const int32_t* rbf_row_off = nullptr;   // [R+1]
+  const int32_t* rbf_acc_off = nullptr;   // [R+1]
   const double* verts_l = nullptr;
   const int32_t* faces = nullptr;
   const double* planes_l = nullptr;
@@ -51,6 +60,7 @@ struct PosedModel {
   float* spheres_w = nullptr;
   void* verts_w = nullptr;    // T
   void* hscale_w = nullptr;   // T
+  void* rbf_rows = nullptr;   // T [rbf_rows][4], per pass (fsdf_set_rbf_params)
 };
 
 struct PassOutputs {

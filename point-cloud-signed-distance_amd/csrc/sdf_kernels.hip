@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const doubl
   if (tid >= fv_pad) tid -= fv_pad - fv;
   if (tid < lm.F) {
     const int f = tid;
-    const int k = lm.face_hull[f];
+    const int k = lm.hull_surface[lm.face_hull[f]];
     double P[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) P[i] = poses[12 * k + i];
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const doubl
     fx[21] = (T)0; fx[22] = (T)0; fx[23] = (T)0;
   } else if (tid < lm.F + lm.V) {
     const int v = tid - lm.F;
-    const double* P = poses + 12 * lm.vert_hull[v];
+    const double* P = poses + 12 * lm.hull_surface[lm.vert_hull[v]];
     double w[3];
     xf_point(P, lm.verts_l + 3 * v, w);
     T* o = verts_w + 4 * v;
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const doubl
     // padded to a multiple of 64 by the launcher): sphere + certificate scale
     const int r = tid - lm.F - lm.V;
     const int k = r >> 6, lane = r & 63;
-    const double* P = poses + 12 * k;
+    const double* P = poses + 12 * lm.hull_surface[k];
     T sc = (T)0;
     for (int v = lm.vert_off[k] + lane; v < lm.vert_off[k + 1]; v += 64) {
       double w[3];
@@ -203,7 +203,15 @@ __device__ __forceinline__ void closest_on_triangle(T px, T py, T pz, const T* _
 // Posed model as the pass kernel sees it (device pointers, world frame).
 template <typename T>
 struct PassModel {
-  int K;
+  int K;  // hulls
+  int S;  // surfaces (hulls + RBF skins), the k* index space
+  int R;  // RBF skins
+  const int32_t* __restrict__ hull_surface;  // [K] surface index of hull h
+  const int32_t* __restrict__ surface_kind;  // [S] FSDF_SURFACE_*
+  const int32_t* __restrict__ rbf_surface;   // [R] surface index of RBF skin r
+  const int32_t* __restrict__ rbf_row_off;   // [R+1] rows (n centres + 1 poly row)
+  const int32_t* __restrict__ rbf_acc_off;   // [R+1] offsets in the RBF accumulator block
+  const T* __restrict__ rbf_rows;            // [rows][4] (c, w) ... (a, b)
   const int32_t* __restrict__ face_off;
   const int32_t* __restrict__ vert_off;
   const int32_t* __restrict__ nbr;
@@ -226,6 +234,7 @@ __device__ __forceinline__ T plane_value(const T* __restrict__ pl, T px, T py, T
 constexpr int kStagePlanes = 128;  // plane rows per chunk
 constexpr int kStageVerts = 64;    // vertex rows per chunk
 constexpr int kStageRows = kStagePlanes + kStageVerts;
+constexpr int kMaxRbfAcc = kMaxRbfAccum;  // RBF adjoint doubles per wave (Σ 4n+4)
 #ifndef FSDF_PASS_WAVES_PER_SIMD
 #define FSDF_PASS_WAVES_PER_SIMD 4
 #endif
@@ -401,18 +410,127 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   }
 }
 
+// ---------------------------------------------------------------------------
+// RBF interpolating skin (src/Flash.jl:207-213; SpatialFields XCubed + affine):
+//   f(x) = Σ w_i |x-c_i|^3 + a + b·x,   s = f/|∇f|,
+//   ∇s = ∇f/|∇f| − f (H ∇f)/|∇f|^3      (H = Hessian of f).
+// Centre rows are LDS-staged per wave (call with the whole wave active).
+// ---------------------------------------------------------------------------
+template <typename T>
+struct RbfField {
+  T f, gx, gy, gz, hxx, hyy, hzz, hxy, hxz, hyz;
+};
+
+template <typename T>
+__device__ __forceinline__ void rbf_field(T px, T py, T pz, const T* __restrict__ rows, int nc,
+                                          T* __restrict__ lw, RbfField<T>& F) {
+  typedef typename Row4<T>::type R4;
+  const R4 poly = *(const R4*)(rows + 4 * nc);
+  F.f = mfma_(poly[1], px, mfma_(poly[2], py, mfma_(poly[3], pz, poly[0])));
+  F.gx = poly[1]; F.gy = poly[2]; F.gz = poly[3];
+  F.hxx = F.hyy = F.hzz = F.hxy = F.hxz = F.hyz = (T)0;
+  for (int c0 = 0; c0 < nc; c0 += kStageRows) {
+    const int cn = min(kStageRows, nc - c0);
+    stage_rows(lw, rows + 4 * c0, cn);
+    for (int i = 0; i < cn; ++i) {
+      const R4 c = *(const R4*)(lw + 4 * i);
+      const T dx = px - c[0], dy = py - c[1], dz = pz - c[2];
+      const T r2 = mfma_(dx, dx, mfma_(dy, dy, dz * dz));
+      const T r = tsqrt(r2);
+      const T wr = c[3] * r;
+      F.f = mfma_(wr, r2, F.f);
+      const T t3 = (T)3 * wr;
+      F.gx = mfma_(t3, dx, F.gx); F.gy = mfma_(t3, dy, F.gy); F.gz = mfma_(t3, dz, F.gz);
+      const T hq = r2 > (T)0 ? ((T)3 * c[3]) / r : (T)0;
+      F.hxx = mfma_(hq * dx, dx, F.hxx + t3);
+      F.hyy = mfma_(hq * dy, dy, F.hyy + t3);
+      F.hzz = mfma_(hq * dz, dz, F.hzz + t3);
+      F.hxy = mfma_(hq * dx, dy, F.hxy);
+      F.hxz = mfma_(hq * dx, dz, F.hxz);
+      F.hyz = mfma_(hq * dy, dz, F.hyz);
+    }
+  }
+}
+
+// s and ∇s from the field; also returns c = f/|∇f|^3 and 1/|∇f| for the adjoint.
+template <typename T>
+__device__ __forceinline__ void rbf_skin_from_field(const RbfField<T>& F, T& s, T& gx, T& gy, T& gz, T& c,
+                                                    T& invG) {
+  const T G2 = mfma_(F.gx, F.gx, mfma_(F.gy, F.gy, F.gz * F.gz));
+  const T G = tsqrt(G2);
+  s = F.f / G;
+  invG = (T)1 / G;
+  c = F.f / (G2 * G);
+  const T hgx = mfma_(F.hxx, F.gx, mfma_(F.hxy, F.gy, F.hxz * F.gz));
+  const T hgy = mfma_(F.hxy, F.gx, mfma_(F.hyy, F.gy, F.hyz * F.gz));
+  const T hgz = mfma_(F.hxz, F.gx, mfma_(F.hyz, F.gy, F.hzz * F.gz));
+  gx = mfma_(-c, hgx, F.gx * invG);
+  gy = mfma_(-c, hgy, F.gy * invG);
+  gz = mfma_(-c, hgz, F.gz * invG);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
 }
 
+// Adjoint contributions of the lanes whose nearest surface is RBF skin r
+// (sel): per centre λ_w_i = Σ 2s ∂s/∂w_i and E_i = Σ 2s ∂s/∂c_i (coefficients
+// fixed), then λ_a, λ_b — wave-summed, added by lane 0 into acc (LDS):
+//   acc[0..n) = λ_w, acc[n] = λ_a, acc[n+1..n+4) = λ_b, acc[n+4+3i..] = E_i.
+template <typename T>
+__device__ __forceinline__ void rbf_adjoint(T px, T py, T pz, const T* __restrict__ rows, int nc,
+                                            T* __restrict__ lw, bool sel, double* __restrict__ acc) {
+  typedef typename Row4<T>::type R4;
+  RbfField<T> F;
+  rbf_field(px, py, pz, rows, nc, lw, F);
+  T s, sgx, sgy, sgz, c, invG;
+  rbf_skin_from_field(F, s, sgx, sgy, sgz, c, invG);
+  const T two_s = (T)2 * s;
+  const T dsdf = invG;
+  const T ux = -c * F.gx, uy = -c * F.gy, uz = -c * F.gz;  // ∂s/∂∇f
+  const int lane = threadIdx.x & 63;
+  for (int c0 = 0; c0 < nc; c0 += kStageRows) {
+    const int cn = min(kStageRows, nc - c0);
+    stage_rows(lw, rows + 4 * c0, cn);
+    for (int i = 0; i < cn; ++i) {
+      const R4 cw = *(const R4*)(lw + 4 * i);
+      const T dx = px - cw[0], dy = py - cw[1], dz = pz - cw[2];
+      const T r2 = mfma_(dx, dx, mfma_(dy, dy, dz * dz));
+      const T r = tsqrt(r2);
+      const T e = mfma_(dx, ux, mfma_(dy, uy, dz * uz));
+      const T lam = two_s * mfma_(dsdf * r2, r, (T)3 * r * e);
+      const T k1 = mfma_((T)3 * r, dsdf, r2 > (T)0 ? ((T)3 * e) / r : (T)0);
+      const T k2 = (T)3 * r;
+      const T sc = -two_s * cw[3];
+      double v[4] = {(double)lam, (double)(sc * mfma_(k1, dx, k2 * ux)), (double)(sc * mfma_(k1, dy, k2 * uy)),
+                     (double)(sc * mfma_(k1, dz, k2 * uz))};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = wave_sum(sel ? v[j] : 0.0);
+      if (lane == 0) {
+        acc[c0 + i] += v[0];
+        double* E = acc + nc + 4 + 3 * (c0 + i);
+        E[0] += v[1]; E[1] += v[2]; E[2] += v[3];
+      }
+    }
+  }
+  double w[4] = {(double)(two_s * dsdf), (double)(two_s * mfma_(dsdf, px, ux)),
+                 (double)(two_s * mfma_(dsdf, py, uy)), (double)(two_s * mfma_(dsdf, pz, uz))};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = wave_sum(sel ? w[j] : 0.0);
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[nc + j] += w[j];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Residual pass.
 // ---------------------------------------------------------------------------
-template <typename T, int SLOTS, bool CULL>
-__global__ __launch_bounds__(kBlock, SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) void pass_kernel(const T* __restrict__ pts, int64_t n, PassModel<T> m,
-                                                      PassOutputs out) {
+template <typename T, int SLOTS, bool CULL, bool RBF>
+__global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)) void pass_kernel(
+    const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out) {
   const int K = m.K;
   const float* __restrict__ spheres = m.spheres;
   const int lane = threadIdx.x & 63;
@@ -427,6 +545,10 @@ __global__ __launch_bounds__(kBlock, SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 
     for (int j = 0; j < 6; ++j) acc_row[s * 64 * 6 + j] = 0.0;
   double cost_acc = 0.0;
   __shared__ __attribute__((aligned(32))) T stage[kBlock / 64][4 * kStageRows];
+  // RBF adjoint sums of this wave (lane 0 adds)
+  __shared__ double rbf_acc[kBlock / 64][RBF ? kMaxRbfAcc : 1];
+  if (RBF)
+    for (int e = lane; e < m.rbf_acc_off[m.R]; e += 64) rbf_acc[wave][e] = 0.0;
 
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t base = (int64_t)blockIdx.x * kBlock + wave * 64; base < n; base += stride) {
@@ -461,6 +583,19 @@ __global__ __launch_bounds__(kBlock, SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 
     T best = tinf<T>();
     int bk = 0x7fffffff;
     T gx = (T)0, gy = (T)0, gz = (T)0;
+    if (RBF) {
+      // RBF skins first: always needed (no cheap bound), and they tighten `best`
+      for (int r = 0; r < m.R; ++r) {
+        const int ks = m.rbf_surface[r];
+        const int r0 = m.rbf_row_off[r];
+        const int nc = m.rbf_row_off[r + 1] - r0 - 1;
+        RbfField<T> F;
+        rbf_field(px, py, pz, m.rbf_rows + 4 * r0, nc, stage[wave], F);
+        T sv, hx, hy, hz, c_, iG;
+        rbf_skin_from_field(F, sv, hx, hy, hz, c_, iG);
+        if (valid && (sv < best || (sv == best && ks < bk))) { best = sv; bk = ks; gx = hx; gy = hy; gz = hz; }
+      }
+    }
     // hull k is needed by a lane unless its lower bound exceeds min(ub, best)
     // by more than the fp32 rounding margin
     // hull k is needed by a lane unless |p-c_k| - r_k > min(ub, best) + mrg,
@@ -484,12 +619,13 @@ __global__ __launch_bounds__(kBlock, SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 
           atomicAdd(out.stats + 3, (unsigned long long)__builtin_popcountll(nm));
         }
       }
-      if (need && (dk < best || (dk == best && k < bk))) { best = dk; bk = k; gx = hx; gy = hy; gz = hz; }
+      const int ks = RBF ? m.hull_surface[k] : k;
+      if (need && (dk < best || (dk == best && ks < bk))) { best = dk; bk = ks; gx = hx; gy = hy; gz = hz; }
     };
     uint64_t done[SLOTS];
 #pragma unroll
     for (int s = 0; s < SLOTS; ++s) done[s] = 0;
-    if (CULL) {
+    if (CULL && K > 0) {
       // Phase B: each lane's seed hull first (one evaluation per distinct seed
       // in the wave) so that `best` is tight before the sweep.
       uint64_t pend = __ballot(valid);
@@ -533,9 +669,18 @@ __global__ __launch_bounds__(kBlock, SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 
     uint64_t pending = __ballot(valid);
     while (pending) {
       const int leader = __builtin_ctzll(pending);
-      const int kk = __shfl(bk, leader, 64);
+      const int kk = __builtin_amdgcn_readfirstlane(__shfl(bk, leader, 64));
       const bool sel = valid && (bk == kk);
       pending &= ~__ballot(sel);
+      if (RBF && m.surface_kind[kk] != 0) {
+        // RBF skin: adjoint sums instead of a rigid wrench
+        int r = 0;
+        while (m.rbf_surface[r] != kk) ++r;
+        const int r0 = m.rbf_row_off[r];
+        rbf_adjoint(px, py, pz, m.rbf_rows + 4 * r0, m.rbf_row_off[r + 1] - r0 - 1, stage[wave], sel,
+                    &rbf_acc[wave][m.rbf_acc_off[r]]);
+        continue;
+      }
       double v[6];
 #pragma unroll
       for (int j = 0; j < 3; ++j) { v[j] = sel ? cF[j] : 0.0; v[3 + j] = sel ? cM[j] : 0.0; }
@@ -564,12 +709,21 @@ __global__ __launch_bounds__(kBlock, SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 
   cost_acc = wave_sum(cost_acc);
   if (lane == 0) red[wave][SLOTS * 64 * 6] = cost_acc;
   __syncthreads();
-  const int len = 1 + 6 * K;
+  const int len6 = 1 + 6 * m.S;
+  const int len = len6 + (RBF ? m.rbf_acc_off[m.R] : 0);
   for (int t = threadIdx.x; t < len; t += kBlock) {
-    const int src = (t == 0) ? SLOTS * 64 * 6 : t - 1;
-    double s = red[0][src];
+    double s;
+    if (t < len6) {
+      const int src = (t == 0) ? SLOTS * 64 * 6 : t - 1;
+      s = red[0][src];
 #pragma unroll
-    for (int w = 1; w < kBlock / 64; ++w) s += red[w][src];
+      for (int w = 1; w < kBlock / 64; ++w) s += red[w][src];
+    } else {
+      const int src = RBF ? t - len6 : 0;
+      s = rbf_acc[0][src];
+#pragma unroll
+      for (int w = 1; w < kBlock / 64; ++w) s += rbf_acc[w][src];
+    }
     out.partials[(int64_t)t * gridDim.x + blockIdx.x] = s;
   }
 }
@@ -607,6 +761,7 @@ int pass_blocks(int64_t n) {
 hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_poses, const PosedModel& pm,
                        hipStream_t s) {
   const int total = ((lm.F + lm.V + 63) & ~63) + 64 * lm.K;
+  if (total == 0) return hipSuccess;  // RBF-only scene: nothing to pose
   const int grid = (total + kBlock - 1) / kBlock;
   if (precision == 64) {
     hipLaunchKernelGGL(pose_kernel<double>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses,
@@ -619,11 +774,19 @@ hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_pose
   return hipGetLastError();
 }
 
-template <typename T, bool CULL>
+template <typename T, bool CULL, bool RBF>
 static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void* d_pts, int64_t n, int nblocks,
                           const PassOutputs& out, hipStream_t s) {
   PassModel<T> m;
   m.K = lm.K;
+  m.S = lm.S;
+  m.R = lm.R;
+  m.hull_surface = lm.hull_surface;
+  m.surface_kind = lm.surface_kind;
+  m.rbf_surface = lm.rbf_surface;
+  m.rbf_row_off = lm.rbf_row_off;
+  m.rbf_acc_off = lm.rbf_acc_off;
+  m.rbf_rows = (const T*)pm.rbf_rows;
   m.face_off = lm.face_off;
   m.vert_off = lm.vert_off;
   m.nbr = lm.face_nbr;
@@ -633,23 +796,30 @@ static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void
   m.hscale = (const T*)pm.hscale_w;
   m.spheres = pm.spheres_w;
   const T* pts = (const T*)d_pts;
-  if (lm.K <= 64)
-    hipLaunchKernelGGL((pass_kernel<T, 1, CULL>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, m, out);
-  else if (lm.K <= 128)
-    hipLaunchKernelGGL((pass_kernel<T, 2, CULL>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, m, out);
+  if (lm.S <= 64)
+    hipLaunchKernelGGL((pass_kernel<T, 1, CULL, RBF>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, m, out);
+  else if (lm.S <= 128)
+    hipLaunchKernelGGL((pass_kernel<T, 2, CULL, RBF>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, m, out);
   else
-    hipLaunchKernelGGL((pass_kernel<T, 4, CULL>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, m, out);
+    hipLaunchKernelGGL((pass_kernel<T, 4, CULL, RBF>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, m, out);
+}
+
+template <typename T>
+static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm, const void* d_pts, int64_t n,
+                          int nblocks, const PassOutputs& out, hipStream_t s) {
+  if (lm.R > 0) {
+    if (cull) launch_pass_t<T, true, true>(lm, pm, d_pts, n, nblocks, out, s);
+    else launch_pass_t<T, false, true>(lm, pm, d_pts, n, nblocks, out, s);
+  } else {
+    if (cull) launch_pass_t<T, true, false>(lm, pm, d_pts, n, nblocks, out, s);
+    else launch_pass_t<T, false, false>(lm, pm, d_pts, n, nblocks, out, s);
+  }
 }
 
 hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const void* d_pts,
                        int64_t n, int nblocks, const PassOutputs& out, hipStream_t s) {
-  if (precision == 64) {
-    if (cull) launch_pass_t<double, true>(lm, pm, d_pts, n, nblocks, out, s);
-    else launch_pass_t<double, false>(lm, pm, d_pts, n, nblocks, out, s);
-  } else {
-    if (cull) launch_pass_t<float, true>(lm, pm, d_pts, n, nblocks, out, s);
-    else launch_pass_t<float, false>(lm, pm, d_pts, n, nblocks, out, s);
-  }
+  if (precision == 64) launch_pass_p<double>(cull, lm, pm, d_pts, n, nblocks, out, s);
+  else launch_pass_p<float>(cull, lm, pm, d_pts, n, nblocks, out, s);
   return hipGetLastError();
 }
 

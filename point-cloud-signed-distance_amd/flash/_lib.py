@@ -38,6 +38,13 @@ class FsdfHull(ctypes.Structure):
                 ("planes", c_void_p)]
 
 
+SURFACE_HULL, SURFACE_RBF = 0, 1
+
+
+class FsdfSurface(ctypes.Structure):
+    _fields_ = [("kind", c_int32), ("n_centers", c_int32), ("hull", FsdfHull)]
+
+
 # name -> (restype, argtypes); exactly the functions declared in include/flashsdf.h
 _PROTOS = {
     "fsdf_convex_hull": (c_int32, [c_void_p, c_int32, POINTER(c_int32), c_void_p, POINTER(c_int32), c_void_p,
@@ -49,6 +56,8 @@ _PROTOS = {
     "fsdf_num_hulls": (c_int32, [c_void_p, POINTER(c_int32)]),
     "fsdf_accum_len": (c_int32, [c_void_p, POINTER(c_int32)]),
     "fsdf_set_model": (c_int32, [c_void_p, POINTER(FsdfHull), c_int32]),
+    "fsdf_set_surfaces": (c_int32, [c_void_p, POINTER(FsdfSurface), c_int32]),
+    "fsdf_set_rbf_params": (c_int32, [c_void_p, c_void_p, c_int64]),
     "fsdf_set_points": (c_int32, [c_void_p, c_void_p, c_int64]),
     "fsdf_set_points_device": (c_int32, [c_void_p, c_void_p, c_int64]),
     "fsdf_num_points": (c_int32, [c_void_p, POINTER(c_int64)]),
@@ -144,17 +153,37 @@ class Context:
 
     def set_model(self, hulls):
         """hulls: sequence of (vertices [m,3] f64, faces [f,3] i32, planes [f,4] f64 or None)."""
-        arr = (FsdfHull * len(hulls))()
+        self.set_surfaces([("hull", h) for h in hulls])
+
+    def set_surfaces(self, surfaces):
+        """surfaces: sequence of ("hull", (vertices, faces, planes)) or ("rbf", n_centres),
+        in the scene's surface order (k* indexes it)."""
+        arr = (FsdfSurface * len(surfaces))()
         keep = []
-        for i, (v, f, p) in enumerate(hulls):
-            v = np.ascontiguousarray(v, np.float64)
-            f = np.ascontiguousarray(f, np.int32)
-            p = None if p is None else np.ascontiguousarray(p, np.float64)
-            keep += [v, f, p]
-            arr[i] = FsdfHull(v.shape[0], f.shape[0], v.ctypes.data, f.ctypes.data,
-                              None if p is None else p.ctypes.data)
-        check(self._lib.fsdf_set_model(self._ctx, arr, len(hulls)), self._ctx, "set_model")
-        self.K = len(hulls)
+        n_rbf = []
+        for i, (kind, spec) in enumerate(surfaces):
+            if kind == "hull":
+                v, f, p = spec
+                v = np.ascontiguousarray(v, np.float64)
+                f = np.ascontiguousarray(f, np.int32)
+                p = None if p is None else np.ascontiguousarray(p, np.float64)
+                keep += [v, f, p]
+                arr[i] = FsdfSurface(SURFACE_HULL, 0, FsdfHull(v.shape[0], f.shape[0], v.ctypes.data, f.ctypes.data,
+                                                               None if p is None else p.ctypes.data))
+            elif kind == "rbf":
+                arr[i] = FsdfSurface(SURFACE_RBF, int(spec), FsdfHull(0, 0, None, None, None))
+                n_rbf.append(int(spec))
+            else:
+                raise ValueError(kind)
+        check(self._lib.fsdf_set_surfaces(self._ctx, arr, len(surfaces)), self._ctx, "set_surfaces")
+        self.K = len(surfaces)
+        self.rbf_centres = n_rbf
+        self.accum_len = 1 + 6 * self.K + sum(4 * n + 4 for n in n_rbf)
+
+    def set_rbf_params(self, rows: np.ndarray):
+        """Per-pass RBF rows [Σ(n+1), 4] (centres + w, then (a, b)) in surface order."""
+        r = np.ascontiguousarray(rows, np.float64)
+        check(self._lib.fsdf_set_rbf_params(self._ctx, ptr(r), r.size), self._ctx, "set_rbf_params")
 
     def set_points(self, xyz: np.ndarray):
         pts = np.ascontiguousarray(xyz, np.float64).reshape(-1, 3)
@@ -174,7 +203,7 @@ class Context:
     def eval(self, poses, per_point: bool = False):
         """One residual pass over the resident cloud -> (cost, accum[1+6K], extras)."""
         p = self._poses(poses)
-        accum = np.empty(1 + 6 * self.K, np.float64)
+        accum = np.empty(self.accum_len, np.float64)
         cost = c_double(0.0)
         kstar = d = grad = None
         if per_point:

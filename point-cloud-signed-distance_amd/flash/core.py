@@ -89,15 +89,19 @@ class Manipulator:
         key = (device, precision, cull, sort_points)
         ctx = self._engines.get(key)
         if ctx is None:
-            if len(self.convex_surfaces()) != len(self.surfaces):
-                raise NotImplementedError(
-                    "RBF (InterpolatingSkin) surfaces are not in the GPU residual pass yet "
-                    "(SURVEY.md §8f rank 2); this model has "
-                    f"{len(self.surfaces) - len(self.convex_surfaces())} of them")
             ctx = _lib.Context(device=device, precision=precision, cull=cull, sort_points=sort_points)
-            ctx.set_model([(s.hull.vertices, s.hull.faces, s.hull.planes) for s in self.surfaces])
+            spec = []
+            for s in self.surfaces:
+                if isinstance(s, ConvexGeometry):
+                    spec.append(("hull", (s.hull.vertices, s.hull.faces, s.hull.planes)))
+                else:
+                    spec.append(("rbf", len(s.surface_points) + len(s.skeleton_points)))
+            ctx.set_surfaces(spec)
             self._engines[key] = ctx
         return ctx
+
+    def has_rbf(self) -> bool:
+        return any(isinstance(s, InterpolatingGeometry) for s in self.surfaces)
 
     def invalidate(self):
         """Drop device contexts (after editing surfaces / merging)."""
@@ -149,6 +153,28 @@ def hull_poses(manip: Manipulator, q: np.ndarray) -> np.ndarray:
     return np.stack([(T[s.body] @ s.frame).as_pose12() for s in manip.convex_surfaces()])
 
 
+_IDENTITY12 = np.concatenate([np.eye(3).ravel(), np.zeros(3)])
+
+
+def surface_poses(manip: Manipulator, q: np.ndarray) -> np.ndarray:
+    """[S,12] one pose per surface in surface order (identity for RBF skins,
+    whose centres travel separately)."""
+    T = manip.mechanism.body_transforms(q)
+    return np.stack([(T[s.body] @ s.frame).as_pose12() if isinstance(s, ConvexGeometry) else _IDENTITY12
+                     for s in manip.surfaces])
+
+
+def prepare_pass(ctx, manip: Manipulator, q_normalized: np.ndarray, deformation_data: np.ndarray):
+    """Poses for every surface; uploads the RBF rows when the scene has skins.
+    Returns (poses, rbf solves or [])."""
+    solves = []
+    if manip.has_rbf():
+        from . import rbf
+        solves = rbf.solve(manip, q_normalized, deformation_data)
+        ctx.set_rbf_params(rbf.rows(solves))
+    return surface_poses(manip, q_normalized), solves
+
+
 class SceneSkin:
     """The closure returned by skin(state): x -> minimum(s(x) for s in surfaces)
     (src/Flash.jl:265-268). Accepts one point (returns a float) or an (n,3)
@@ -157,11 +183,13 @@ class SceneSkin:
     def __init__(self, state: ManipulatorState, device: int = 0, precision: int = 64):
         self.state = state
         self.ctx = state.manipulator.engine(device, precision)
-        self.poses = hull_poses(state.manipulator, state.manipulator.mechanism.normalize(state.q))
+        self.q = state.manipulator.mechanism.normalize(state.q)
+        self.deformation_data = state.deformation_data.copy()
 
     def evaluate(self, x):
         pts = np.asarray(x, np.float64).reshape(-1, 3)
-        return self.ctx.skin(self.poses, pts)
+        poses, _ = prepare_pass(self.ctx, self.state.manipulator, self.q, self.deformation_data)
+        return self.ctx.skin(poses, pts)
 
     def __call__(self, x):
         x = np.asarray(x, np.float64)

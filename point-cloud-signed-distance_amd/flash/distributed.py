@@ -15,8 +15,9 @@ from __future__ import annotations
 
 import numpy as np
 
-from .core import Manipulator, ManipulatorState, hull_poses
-from .gradientdescent import _regularizer, default_deformation_cost_weight, normalize, unflatten
+from .core import ConvexGeometry, Manipulator, ManipulatorState, prepare_pass
+from .gradientdescent import (_regularizer, default_deformation_cost_weight, gradient_from_accum, normalize,
+                              unflatten)
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
@@ -34,13 +35,9 @@ def allreduce_accum(accum, group=None):
     return accum
 
 
-def chain_gradient(manip: Manipulator, x: np.ndarray, accum: np.ndarray, weight) -> np.ndarray:
-    mech = manip.mechanism
-    body_w = np.zeros((mech.num_bodies, 6))
-    for k, s in enumerate(manip.convex_surfaces()):
-        body_w[s.body] += accum[1 + 6 * k: 7 + 6 * k]
-    nq = mech.num_positions
-    return np.concatenate([mech.config_gradient(x[:nq], body_w), 2.0 * weight * x[nq:]])
+def chain_gradient(manip: Manipulator, x: np.ndarray, accum: np.ndarray, weight, solves=()) -> np.ndarray:
+    """∂c/∂x from an (all-reduced) accumulator (see gradientdescent.gradient_from_accum)."""
+    return gradient_from_accum(manip, np.asarray(x, np.float64), np.asarray(accum), list(solves), weight)
 
 
 class ShardedCostFunctor:
@@ -58,7 +55,7 @@ class ShardedCostFunctor:
         self.dev = torch.device("cuda", device)
         pts = torch.as_tensor(np.ascontiguousarray(local_points, np.float64).reshape(-1, 3), device=self.dev)
         self.ctx.set_points_device(pts.data_ptr(), pts.shape[0])
-        self.accum = torch.zeros(1 + 6 * self.ctx.K, dtype=torch.float64, device=self.dev)
+        self.accum = torch.zeros(self.ctx.accum_len, dtype=torch.float64, device=self.dev)
         self.stream = torch.cuda.current_stream(self.dev)
         self.ctx.set_stream(self.stream.cuda_stream)
 
@@ -66,7 +63,8 @@ class ShardedCostFunctor:
         """Enqueue one residual pass + all-reduce (asynchronous)."""
         unflatten(self.state, x)
         normalize(self.state)
-        self.ctx.eval_device(hull_poses(self.manipulator, self.state.q), self.accum.data_ptr())
+        poses, self._solves = prepare_pass(self.ctx, self.manipulator, self.state.q, self.state.deformation_data)
+        self.ctx.eval_device(poses, self.accum.data_ptr())
         allreduce_accum(self.accum, self.group)
         return self.accum
 
@@ -74,4 +72,4 @@ class ShardedCostFunctor:
         x = np.asarray(x, np.float64)
         acc = self.launch(x).cpu().numpy()
         c = float(acc[0]) + _regularizer(self.state, self.weight)
-        return c, chain_gradient(self.manipulator, x, acc, self.weight)
+        return c, chain_gradient(self.manipulator, x, acc, self.weight, self._solves)

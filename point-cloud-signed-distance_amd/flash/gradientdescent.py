@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .core import Manipulator, ManipulatorState, hull_poses
+from .core import ConvexGeometry, Manipulator, ManipulatorState, prepare_pass
 
 default_deformation_cost_weight = 10
 
@@ -48,8 +48,34 @@ def cost(state: ManipulatorState, sensed_points, deformation_cost_weight=default
     m = state.manipulator
     ctx = m.engine(device, precision)
     pts = np.asarray(sensed_points, np.float64).reshape(-1, 3)
-    d, _, _ = ctx.skin(hull_poses(m, state.q), pts) if len(pts) else (np.zeros(0), None, None)
+    d = np.zeros(0)
+    if len(pts):
+        poses, _ = prepare_pass(ctx, m, state.q, state.deformation_data)
+        d, _, _ = ctx.skin(poses, pts)
     return float(np.dot(d, d)) + _regularizer(state, deformation_cost_weight)
+
+
+def gradient_from_accum(manip: Manipulator, x: np.ndarray, accum: np.ndarray, solves, weight) -> np.ndarray:
+    """∂c/∂x from one pass's accumulator: hull wrenches (slot = surface index)
+    plus the RBF adjoint block, contracted with the joint motion subspaces;
+    ∂c/∂δ from the RBF block plus the regularizer 2wδ."""
+    mech = manip.mechanism
+    nq = mech.num_positions
+    body_w = np.zeros((mech.num_bodies, 6))
+    for k, s in enumerate(manip.surfaces):
+        if isinstance(s, ConvexGeometry):
+            body_w[s.body] += accum[1 + 6 * k: 7 + 6 * k]
+    gd = 2.0 * weight * np.asarray(x[nq:], np.float64)
+    if solves:
+        from . import rbf
+        S = len(manip.surfaces)
+        w_rbf, g_rbf = rbf.chain(manip, mech.normalize(x[:nq]), solves, accum[1 + 6 * S:], manip.num_deformations())
+        body_w += w_rbf
+        gd = gd + g_rbf
+    # the gradient is taken at the caller's (un-normalized) x: the chain rule
+    # includes the normalization projection (src/gradientdescent.jl:30)
+    gq = mech.config_gradient(np.asarray(x[:nq], np.float64), body_w)
+    return np.concatenate([gq, gd])
 
 
 class CostFunctor:
@@ -79,7 +105,8 @@ class CostFunctor:
         unflatten(self.state, x)
         normalize(self.state)
         self._ensure_resident()
-        c, accum, extras = self.ctx.eval(hull_poses(self.manipulator, self.state.q), per_point)
+        poses, self._solves = prepare_pass(self.ctx, self.manipulator, self.state.q, self.state.deformation_data)
+        c, accum, extras = self.ctx.eval(poses, per_point)
         return c + _regularizer(self.state, self.weight), accum, extras
 
     def __call__(self, x) -> float:
@@ -89,17 +116,7 @@ class CostFunctor:
         """(c(x), ∂c/∂x) from one residual pass."""
         x = np.asarray(x, np.float64)
         c, accum, _ = self._pass(x)
-        m = self.manipulator
-        mech = m.mechanism
-        body_w = np.zeros((mech.num_bodies, 6))
-        for k, s in enumerate(m.convex_surfaces()):
-            body_w[s.body] += accum[1 + 6 * k: 7 + 6 * k]
-        nq = mech.num_positions
-        # the gradient is taken at the caller's (un-normalized) x: the chain
-        # rule includes the normalization projection (src/gradientdescent.jl:30)
-        gq = mech.config_gradient(x[:nq], body_w)
-        gd = 2.0 * self.weight * x[nq:]
-        return c, np.concatenate([gq, gd])
+        return c, gradient_from_accum(self.manipulator, x, accum, self._solves, self.weight)
 
     def per_point(self, x):
         """(d*, k*, ∇d*) for every sensed point at configuration x."""

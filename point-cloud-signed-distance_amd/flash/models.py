@@ -228,3 +228,24 @@ def joint_limits(manip: Manipulator):
         if e.joint.kind == "revolute":
             lo[e.q_offset], hi[e.q_offset] = e.joint.lower, e.joint.upper
     return lo, hi
+
+
+def irb_and_squishable():
+    """The multi-body scene of examples/irb_and_squishable.ipynb (cells 3-6):
+    IRB140 with its base joint made QuaternionFloating (cell 4), merged with
+    squishable() and the table box; surfaces = 7 hulls + squishable RBF + table
+    (9), 63 states. Returns (manipulator, x0) with the notebook's placements
+    (cell 6): IRB t = (0, 0, 0.75), squishable t = (0.55, 0.45, 0.8),
+    table t = (0.4, 0, 0.6)."""
+    from .core import num_states
+    m = irb140()
+    m.mechanism.change_joint_type(1, QuaternionFloating("base_link_floating"))
+    merge(m, squishable())
+    merge(m, table())
+    x0 = np.zeros(num_states(m))
+    x0[:m.mechanism.num_positions] = m.mechanism.zero_configuration()
+    for name, t in (("base_link", (0.0, 0.0, 0.75)), ("squishable_body", (0.55, 0.45, 0.8)),
+                    ("table_body", (0.4, 0.0, 0.6))):
+        rng = m.mechanism.q_range(m.mechanism.body_index(name))
+        x0[rng.start + 4: rng.start + 7] = t
+    return m, x0

@@ -1,0 +1,116 @@
+"""GPU: RBF skins (BASELINE configs 3 and 5) against the oracle golden vectors
+and the reference KAT, through the C-ABI."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, rng
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene(name):
+    from flash import Models
+    if name == "c3_beanbag":
+        return Models.beanbag()
+    return Models.irb_and_squishable()[0]
+
+
+def _ctx(m, precision=64, cull=True, sort_points=False):
+    from flash import _lib
+    from flash.core import ConvexGeometry
+    c = _lib.Context(device=0, precision=precision, cull=cull, sort_points=sort_points)
+    c.set_surfaces([("hull", (s.hull.vertices, s.hull.faces, s.hull.planes)) if isinstance(s, ConvexGeometry)
+                    else ("rbf", len(s.surface_points) + len(s.skeleton_points)) for s in m.surfaces])
+    return c
+
+
+def test_beanbag_kat_on_gpu():
+    """test/runtests.jl:17 through Flash.skin(state) on the GPU."""
+    import flash
+    from flash import Models
+    m = Models.beanbag()
+    skin = flash.skin(flash.ManipulatorState(m))
+    v = skin([100.0, 0.0, 0.0])
+    assert v == pytest.approx(99.0, rel=2e-2)
+
+
+@pytest.mark.parametrize("name", ["c3_beanbag", "c5_scene"])
+@pytest.mark.parametrize("cull", [True, False])
+def test_rbf_golden_parity(name, cull):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    m = _scene(name)
+    c = _ctx(m, cull=cull)
+    c.set_points(z["points"])
+    c.set_rbf_params(z["rbf_rows"])
+    cost, acc, (k, d, g) = c.eval(z["poses"], per_point=True)
+    assert np.array_equal(k, z["kstar"])
+    assert np.array_equal(d, z["d"]), np.abs(d - z["d"]).max()
+    assert np.array_equal(g, z["grad"]), np.abs(g - z["grad"]).max()
+    assert np.allclose(acc, z["accum"], rtol=1e-9, atol=1e-9 * np.abs(z["accum"]).max())
+    # the chained gradient of the whole state (63 / 25 states)
+    from flash import rbf as host_rbf
+    from flash.gradientdescent import gradient_from_accum
+    x = z["x"]
+    nq = m.mechanism.num_positions
+    solves = host_rbf.solve(m, m.mechanism.normalize(x[:nq]), x[nq:])
+    gx = gradient_from_accum(m, x, acc, solves, 10)
+    assert np.allclose(gx, z["dcdx"], rtol=1e-7, atol=1e-7 * np.abs(z["dcdx"]).max())
+    c.close()
+
+
+def test_rbf_fp32_beanbag():
+    z = np.load(os.path.join(GOLDEN, "c3_beanbag.npz"))
+    c = _ctx(_scene("c3_beanbag"), precision=32)
+    c.set_points(z["points"])
+    c.set_rbf_params(z["rbf_rows"])
+    cost, acc, (k, d, g) = c.eval(z["poses"], per_point=True)
+    assert np.abs(d - z["d"]).max() < 1e-4 * max(1.0, np.abs(z["d"]).max())
+    assert cost == pytest.approx(z["accum"][0], rel=1e-4)
+    c.close()
+
+
+def test_rbf_requires_params():
+    from flash import _lib
+    c = _ctx(_scene("c3_beanbag"))
+    c.set_points(np.zeros((10, 3)))
+    with pytest.raises(_lib.FlashNativeError) as e:
+        c.eval(np.zeros((1, 12)))
+    assert e.value.status == 3
+    c.close()
+
+
+def test_tracking_deformable_beanbag():
+    """estimate_state on the deformable beanbag (examples/deformable_manipulator
+    .ipynb): the GPU cost/gradient drive the cost down."""
+    import flash
+    from flash import Models, rbf as host_rbf
+    from flash.tracking import NaiveSolver, estimate_state
+    from flash.gradientdescent import CostFunctor
+    m = Models.beanbag()
+    r = rng(11)
+    nq = m.mechanism.num_positions
+    x_true = np.zeros(flash.num_states(m))
+    x_true[:nq] = m.mechanism.zero_configuration()
+    x_true[4:7] = 2 * r.random(3) ** 3
+    x_true[nq:] = 0.5 * (r.random(18) - 0.5)
+    solves = host_rbf.solve(m, m.mechanism.normalize(x_true[:nq]), x_true[nq:])
+    C = solves[0].centres
+    # sensed points on the true skin: project random points along the gradient
+    skin_true = flash.ManipulatorState(m)
+    skin_true.q[:] = x_true[:nq]
+    skin_true.deformation_data[:] = x_true[nq:]
+    f = flash.skin(skin_true)
+    pts = C.mean(0) + r.normal(size=(4000, 3))
+    for _ in range(6):
+        d, _, g = f.evaluate(pts)
+        pts = pts - d[:, None] * g
+    x0 = x_true.copy()
+    x0[4:7] += 0.1
+    cf = CostFunctor(m, pts)
+    c0 = cf(x0)
+    seen = []
+    x = estimate_state(m, pts, x0, callback=lambda x, c: seen.append(c),
+                       solver=NaiveSolver(len(x0), rate=0.05, max_step=0.05, iteration_limit=25))
+    assert seen[-1] < 0.5 * c0

@@ -583,7 +583,7 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
 extern "C" int fsdf_eval_device(fsdf_ctx* c, const double* poses, double* d_accum, int32_t* d_kstar, double* d_d,
                                 double* d_grad) {
   if (!c) return FSDF_ERR_ARG;
-  if (c->lm.K == 0) return fail(c, FSDF_ERR_STATE, "eval: no model (call fsdf_set_model first)");
+  if (c->lm.S == 0) return fail(c, FSDF_ERR_STATE, "eval: no model (call fsdf_set_model first)");
   if (!poses || !d_accum) return fail(c, FSDF_ERR_ARG, "eval_device: poses and d_accum are required");
   HIPCHECK(c, hipSetDevice(c->device));
   return run_pass(c, poses, c->d_pts, c->n, d_accum, d_kstar, d_d, d_grad, c->d_perm);
@@ -623,7 +623,7 @@ static int fetch(fsdf_ctx* c, int64_t n, double* cost_out, double* accum_out, in
 extern "C" int fsdf_eval(fsdf_ctx* c, const double* poses, double* cost_out, double* accum_out, int32_t* kstar_out,
                          double* d_out, double* grad_out) {
   if (!c) return FSDF_ERR_ARG;
-  if (c->lm.K == 0) return fail(c, FSDF_ERR_STATE, "eval: no model (call fsdf_set_model first)");
+  if (c->lm.S == 0) return fail(c, FSDF_ERR_STATE, "eval: no model (call fsdf_set_model first)");
   if (!poses) return fail(c, FSDF_ERR_ARG, "eval: poses required");
   HIPCHECK(c, hipSetDevice(c->device));
   const bool want_pp = kstar_out || d_out || grad_out;
@@ -640,7 +640,7 @@ extern "C" int fsdf_eval(fsdf_ctx* c, const double* poses, double* cost_out, dou
 extern "C" int fsdf_skin(fsdf_ctx* c, const double* poses, const double* xyz, int64_t n, double* d_out,
                          int32_t* kstar_out, double* grad_out) {
   if (!c) return FSDF_ERR_ARG;
-  if (c->lm.K == 0) return fail(c, FSDF_ERR_STATE, "skin: no model (call fsdf_set_model first)");
+  if (c->lm.S == 0) return fail(c, FSDF_ERR_STATE, "skin: no model (call fsdf_set_model first)");
   if (!poses || n < 0 || (n > 0 && !xyz)) return fail(c, FSDF_ERR_ARG, "skin: bad arguments");
   HIPCHECK(c, hipSetDevice(c->device));
   if (n == 0) return FSDF_OK;

@@ -157,6 +157,16 @@ int fsdf_eval_device(fsdf_ctx* ctx, const double* poses, double* d_accum,
 int fsdf_skin(fsdf_ctx* ctx, const double* poses, const double* xyz, int64_t n,
               double* d_out, int32_t* kstar_out, double* grad_out);
 
+/* Depth-sensor raycast on the scene SDF (src/depthsensors.jl:56-97, doRaycast;
+ * the field is Flash.skin(state), src/depthsensors.jl:116): per ray a secant
+ * march from `origin` — step = -SDF/est_grad (est_grad starts at -1, then the
+ * secant slope), |step| <= 0.4, stop at |SDF| <= 1e-5 or after 60 steps;
+ * depth = NaN when the final |SDF| > 1e-2. origin: 3 doubles (world);
+ * rays: [n][3] unit directions (world); depth_out: n doubles. Synchronous.
+ * Uses the current RBF parameters when the scene has skins. */
+int fsdf_raycast(fsdf_ctx* ctx, const double* poses, const double* origin, const double* rays, int64_t n,
+                 double* depth_out);
+
 /* Block until all work queued on the context stream has finished. */
 int fsdf_synchronize(fsdf_ctx* ctx);
 

@@ -411,6 +411,38 @@ void oracle_cost_accum(const oracle_posed* m, const double* pts, int64_t n, doub
   }
 }
 
+/* doRaycast (src/depthsensors.jl:56-81) for every ray on the scene SDF:
+ * secant march, |step| <= 0.4, EPS 1e-5, <= 60 steps, NaN if the final
+ * |SDF| > 1000·EPS. Same operation order as raycast_kernel. */
+void oracle_raycast(const oracle_posed* m, const double* o, const double* rays, int64_t n, double* depth,
+                    int32_t threads) {
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 16)
+#endif
+  for (int64_t i = 0; i < n; ++i) {
+    const double* r = rays + 3 * i;
+    double dist = 0.0, est = -1.0, last, g[3], p[3];
+    int32_t kk, k = 0;
+    p[0] = o[0] + dist * r[0]; p[1] = o[1] + dist * r[1]; p[2] = o[2] + dist * r[2];
+    skin_one(m, p, &last, &kk, g);
+    while (fabs(last) > 1e-5 && k < 60) {
+      double step = -last / est;
+      const double a = fabs(step);
+      step = copysign(a < 0.4 ? a : 0.4, step);
+      dist += step;
+      p[0] = o[0] + dist * r[0]; p[1] = o[1] + dist * r[1]; p[2] = o[2] + dist * r[2];
+      double v;
+      skin_one(m, p, &v, &kk, g);
+      est = (v - last) / step;
+      last = v;
+      ++k;
+    }
+    depth[i] = fabs(last) > 1000.0 * 1e-5 ? NAN : dist;
+  }
+  (void)threads;
+}
+
 /* Threads the oracle would use (for the bench's cpu_baseline "cores"). */
 int32_t oracle_max_threads(void) {
 #ifdef _OPENMP

@@ -50,6 +50,7 @@ def load():
         lib.oracle_skin.argtypes = [ctypes.POINTER(Posed), c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int32]
         lib.oracle_cost_accum.argtypes = [ctypes.POINTER(Posed), c_void_p, c_int64, c_void_p]
         lib.oracle_rbf_skin.argtypes = [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]
+        lib.oracle_raycast.argtypes = [ctypes.POINTER(Posed), c_void_p, c_void_p, c_int64, c_void_p, c_int32]
         lib.oracle_max_threads.restype = c_int32
         _lib = lib
     return _lib
@@ -167,6 +168,15 @@ class OracleModel:
         acc = np.empty(self.accum_len)
         load().oracle_cost_accum(ctypes.byref(st), _p(pts), len(pts), _p(acc))
         return acc
+
+    def raycast(self, poses, origin, rays, threads: int = 0, rbf_rows=None):
+        """doRaycast per ray (src/depthsensors.jl:56-81) -> depth [n] (NaN = miss)."""
+        st, _keep = self.pose(poses, rbf_rows)
+        o = np.ascontiguousarray(origin, np.float64).reshape(3)
+        r = np.ascontiguousarray(rays, np.float64).reshape(-1, 3)
+        depth = np.empty(len(r))
+        load().oracle_raycast(ctypes.byref(st), _p(o), _p(r), len(r), _p(depth), threads)
+        return depth
 
     def world_hull(self, poses, k):
         """(world vertices, faces, world planes) of hull k, plain numpy."""

@@ -715,3 +715,33 @@ extern "C" int fsdf_kernel_stats(fsdf_ctx* c, int32_t enable, uint64_t* counters
   if (counters) HIPCHECK(c, hipMemcpy(counters, c->d_stats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return FSDF_OK;
 }
+
+extern "C" int fsdf_raycast(fsdf_ctx* c, const double* poses, const double* origin, const double* rays, int64_t n,
+                            double* depth_out) {
+  if (!c) return FSDF_ERR_ARG;
+  if (c->lm.S == 0) return fail(c, FSDF_ERR_STATE, "raycast: no model (call fsdf_set_surfaces first)");
+  if (!poses || !origin || n < 0 || (n > 0 && (!rays || !depth_out))) return fail(c, FSDF_ERR_ARG, "raycast: bad arguments");
+  if (c->lm.R > 0 && !c->rbf_ready)
+    return fail(c, FSDF_ERR_STATE, "raycast: the scene has RBF surfaces: call fsdf_set_rbf_params first");
+  for (int j = 0; j < 3; ++j)
+    if (!std::isfinite(origin[j])) return fail(c, FSDF_ERR_ARG, "raycast: origin not finite");
+  HIPCHECK(c, hipSetDevice(c->device));
+  if (n == 0) return FSDF_OK;
+  int rc = ensure_outputs(c, n);
+  if (rc) return rc;
+  if (c->q64_cap < n) {
+    HIPCHECK(c, hipStreamSynchronize(c->stream));
+    dfree(c->d_q64);
+    c->q64_cap = 0;
+    HIPCHECK(c, hipMalloc(&c->d_q64, (size_t)n * 3 * sizeof(double)));
+    c->q64_cap = n;
+  }
+  rc = upload_poses(c, poses);
+  if (rc) return rc;
+  HIPCHECK(c, hipMemcpyAsync(c->d_q64, rays, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, c->d_poses, c->pm, c->stream));
+  HIPCHECK(c, fsdf::launch_raycast(c->precision, c->cull != 0, c->lm, c->pm, origin, c->d_q64, n, c->d_d, c->stream));
+  HIPCHECK(c, hipMemcpyAsync(depth_out, c->d_d, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  return FSDF_OK;
+}

@@ -80,6 +80,10 @@ hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const Pos
                        const void* d_pts, int64_t n, int nblocks, const PassOutputs& out,
                        hipStream_t s);
 
+// origin: 3 host doubles (passed by value); d_rays [n][3] f64 unit directions.
+hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const double* origin,
+                          const double* d_rays, int64_t n, double* d_depth, hipStream_t s);
+
 hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum,
                          hipStream_t s);
 

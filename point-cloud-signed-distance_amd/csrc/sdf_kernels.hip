@@ -526,6 +526,115 @@ __device__ __forceinline__ void rbf_adjoint(T px, T py, T pz, const T* __restric
 }
 
 // ---------------------------------------------------------------------------
+// Scene signed distance of this lane's point: minimum over all surfaces with
+// the first-index tie rule (src/Flash.jl:265-268), its surface index and
+// gradient. Wave-cooperative (ballots, LDS staging): call with the whole wave
+// active; `valid` marks lanes whose result is used.
+// ---------------------------------------------------------------------------
+template <typename T, int SLOTS, bool CULL, bool RBF>
+__device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const PassModel<T>& m, T* __restrict__ lw,
+                                           unsigned long long* __restrict__ stats, T& best, int& bk, T& gx, T& gy,
+                                           T& gz) {
+  const int K = m.K;
+  const float* __restrict__ spheres = m.spheres;
+  const int lane = threadIdx.x & 63;
+  // Phase A (fp32, exact-safe): with c_k inside hull k and r_k its bounding
+  // radius, d_k(p) >= |p-c_k| - r_k (lower bound) and d_k(p) <= |p-c_k|
+  // (upper bound). ub = min_k |p-c_k|; the best-first seed is the hull of
+  // least power distance |p-c_k|^2 - r_k^2 (a heuristic: any seed is exact).
+  float ub2 = __builtin_huge_valf(), pw_min = __builtin_huge_valf(), smax = 0.f;
+  int kseed = 0;
+  float pxf = 0.f, pyf = 0.f, pzf = 0.f;
+  if (CULL) {
+    pxf = (float)px; pyf = (float)py; pzf = (float)pz;
+    for (int k = 0; k < K; ++k) {
+      const float* sp = spheres + 4 * k;
+      const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
+      const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
+      ub2 = fminf(ub2, dist2);
+      const float pwr = __builtin_fmaf(-sp[3], sp[3], dist2);
+      if (pwr < pw_min) { pw_min = pwr; kseed = k; }
+      smax = fmaxf(smax, fabsf(sp[0]) + fabsf(sp[1]) + fabsf(sp[2]) + 2.0f * sp[3]);
+    }
+  }
+  const float ub = __builtin_sqrtf(ub2);
+  // one rounding margin per lane, >= 1e-5 x every magnitude in the test below
+  const float mrg = 1e-5f * (1.0f + fabsf(pxf) + fabsf(pyf) + fabsf(pzf) + smax + 2.0f * ub);
+
+  best = tinf<T>();
+  bk = 0x7fffffff;
+  gx = (T)0; gy = (T)0; gz = (T)0;
+  if (RBF) {
+    // RBF skins first: always needed (no cheap bound), and they tighten `best`
+    for (int r = 0; r < m.R; ++r) {
+      const int ks = m.rbf_surface[r];
+      const int r0 = m.rbf_row_off[r];
+      const int nc = m.rbf_row_off[r + 1] - r0 - 1;
+      RbfField<T> F;
+      rbf_field(px, py, pz, m.rbf_rows + 4 * r0, nc, lw, F);
+      T sv, hx, hy, hz, c_, iG;
+      rbf_skin_from_field(F, sv, hx, hy, hz, c_, iG);
+      if (valid && (sv < best || (sv == best && ks < bk))) { best = sv; bk = ks; gx = hx; gy = hy; gz = hz; }
+    }
+  }
+  // hull k is needed by a lane unless its lower bound exceeds min(ub, best)
+  // by more than the fp32 rounding margin
+  // hull k is needed by a lane unless |p-c_k| - r_k > min(ub, best) + mrg,
+  // tested without a sqrt: |p-c_k|^2 <= (min(ub, best) + mrg + r_k)^2
+  auto needs = [&](int k) -> bool {
+    if (!CULL) return valid;
+    const float* sp = spheres + 4 * k;
+    const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
+    const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
+    const float t = fminf(ub, (float)best) + mrg + sp[3];
+    return valid && t >= 0.0f && dist2 <= t * t;
+  };
+  // evaluations may run out of index order: ties keep the smaller k
+  auto evaluate = [&](int k, bool need) {
+    T dk, hx, hy, hz;
+    hull_sdf<T>(px, py, pz, k, m, need, dk, hx, hy, hz, lw, stats);
+    if (stats) {
+      const uint64_t nm = __ballot(need);
+      if (lane == 0) {
+        atomicAdd(stats + 1, 1ull);
+        atomicAdd(stats + 3, (unsigned long long)__builtin_popcountll(nm));
+      }
+    }
+    const int ks = RBF ? m.hull_surface[k] : k;
+    if (need && (dk < best || (dk == best && ks < bk))) { best = dk; bk = ks; gx = hx; gy = hy; gz = hz; }
+  };
+  uint64_t done[SLOTS];
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) done[s] = 0;
+  if (CULL && K > 0) {
+    // Phase B: each lane's seed hull first (one evaluation per distinct seed
+    // in the wave) so that `best` is tight before the sweep.
+    uint64_t pend = __ballot(valid);
+    while (pend) {
+      const int kk = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(pend), 64));
+      pend &= ~__ballot(valid && kseed == kk);
+      evaluate(kk, needs(kk));
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s)
+        if ((kk >> 6) == s) done[s] |= 1ull << (kk & 63);
+      if (stats && lane == 0) atomicAdd(stats + 5, 1ull);
+    }
+  }
+  // Phase C: sweep the remaining hulls in index order.
+  for (int k = 0; k < K; ++k) {
+    bool skip = false;
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s)
+      if ((k >> 6) == s) skip = (done[s] >> (k & 63)) & 1ull;
+    if (skip) continue;
+    const bool need = needs(k);
+    if (!__any(need)) continue;
+    evaluate(k, need);
+  }
+  if (stats && lane == 0) atomicAdd(stats + 0, 1ull);
+}
+
+// ---------------------------------------------------------------------------
 // Residual pass.
 // ---------------------------------------------------------------------------
 template <typename T, int SLOTS, bool CULL, bool RBF>
@@ -557,100 +666,9 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
     const int64_t ii = valid ? i : n - 1;
     const T px = pts[3 * ii + 0], py = pts[3 * ii + 1], pz = pts[3 * ii + 2];
 
-    // Phase A (fp32, exact-safe): with c_k inside hull k and r_k its bounding
-    // radius, d_k(p) >= |p-c_k| - r_k (lower bound) and d_k(p) <= |p-c_k|
-    // (upper bound). ub = min_k |p-c_k|; the best-first seed is the hull of
-    // least power distance |p-c_k|^2 - r_k^2 (a heuristic: any seed is exact).
-    float ub2 = __builtin_huge_valf(), pw_min = __builtin_huge_valf(), smax = 0.f;
-    int kseed = 0;
-    float pxf = 0.f, pyf = 0.f, pzf = 0.f;
-    if (CULL) {
-      pxf = (float)px; pyf = (float)py; pzf = (float)pz;
-      for (int k = 0; k < K; ++k) {
-        const float* sp = spheres + 4 * k;
-        const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
-        const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
-        ub2 = fminf(ub2, dist2);
-        const float pwr = __builtin_fmaf(-sp[3], sp[3], dist2);
-        if (pwr < pw_min) { pw_min = pwr; kseed = k; }
-        smax = fmaxf(smax, fabsf(sp[0]) + fabsf(sp[1]) + fabsf(sp[2]) + 2.0f * sp[3]);
-      }
-    }
-    const float ub = __builtin_sqrtf(ub2);
-    // one rounding margin per lane, >= 1e-5 x every magnitude in the test below
-    const float mrg = 1e-5f * (1.0f + fabsf(pxf) + fabsf(pyf) + fabsf(pzf) + smax + 2.0f * ub);
-
-    T best = tinf<T>();
-    int bk = 0x7fffffff;
-    T gx = (T)0, gy = (T)0, gz = (T)0;
-    if (RBF) {
-      // RBF skins first: always needed (no cheap bound), and they tighten `best`
-      for (int r = 0; r < m.R; ++r) {
-        const int ks = m.rbf_surface[r];
-        const int r0 = m.rbf_row_off[r];
-        const int nc = m.rbf_row_off[r + 1] - r0 - 1;
-        RbfField<T> F;
-        rbf_field(px, py, pz, m.rbf_rows + 4 * r0, nc, stage[wave], F);
-        T sv, hx, hy, hz, c_, iG;
-        rbf_skin_from_field(F, sv, hx, hy, hz, c_, iG);
-        if (valid && (sv < best || (sv == best && ks < bk))) { best = sv; bk = ks; gx = hx; gy = hy; gz = hz; }
-      }
-    }
-    // hull k is needed by a lane unless its lower bound exceeds min(ub, best)
-    // by more than the fp32 rounding margin
-    // hull k is needed by a lane unless |p-c_k| - r_k > min(ub, best) + mrg,
-    // tested without a sqrt: |p-c_k|^2 <= (min(ub, best) + mrg + r_k)^2
-    auto needs = [&](int k) -> bool {
-      if (!CULL) return valid;
-      const float* sp = spheres + 4 * k;
-      const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
-      const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
-      const float t = fminf(ub, (float)best) + mrg + sp[3];
-      return valid && t >= 0.0f && dist2 <= t * t;
-    };
-    // evaluations may run out of index order: ties keep the smaller k
-    auto evaluate = [&](int k, bool need) {
-      T dk, hx, hy, hz;
-      hull_sdf<T>(px, py, pz, k, m, need, dk, hx, hy, hz, stage[wave], out.stats);
-      if (out.stats) {
-        const uint64_t nm = __ballot(need);
-        if (lane == 0) {
-          atomicAdd(out.stats + 1, 1ull);
-          atomicAdd(out.stats + 3, (unsigned long long)__builtin_popcountll(nm));
-        }
-      }
-      const int ks = RBF ? m.hull_surface[k] : k;
-      if (need && (dk < best || (dk == best && ks < bk))) { best = dk; bk = ks; gx = hx; gy = hy; gz = hz; }
-    };
-    uint64_t done[SLOTS];
-#pragma unroll
-    for (int s = 0; s < SLOTS; ++s) done[s] = 0;
-    if (CULL && K > 0) {
-      // Phase B: each lane's seed hull first (one evaluation per distinct seed
-      // in the wave) so that `best` is tight before the sweep.
-      uint64_t pend = __ballot(valid);
-      while (pend) {
-        const int kk = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(pend), 64));
-        pend &= ~__ballot(valid && kseed == kk);
-        evaluate(kk, needs(kk));
-#pragma unroll
-        for (int s = 0; s < SLOTS; ++s)
-          if ((kk >> 6) == s) done[s] |= 1ull << (kk & 63);
-        if (out.stats && lane == 0) atomicAdd(out.stats + 5, 1ull);
-      }
-    }
-    // Phase C: sweep the remaining hulls in index order.
-    for (int k = 0; k < K; ++k) {
-      bool skip = false;
-#pragma unroll
-      for (int s = 0; s < SLOTS; ++s)
-        if ((k >> 6) == s) skip = (done[s] >> (k & 63)) & 1ull;
-      if (skip) continue;
-      const bool need = needs(k);
-      if (!__any(need)) continue;
-      evaluate(k, need);
-    }
-    if (out.stats && lane == 0) atomicAdd(out.stats + 0, 1ull);
+    T best, gx, gy, gz;
+    int bk;
+    scene_eval<T, SLOTS, CULL, RBF>(px, py, pz, valid, m, stage[wave], out.stats, best, bk, gx, gy, gz);
     if (!valid) bk = 0;
 
     // contributions: c += d^2; F_k += 2 d g; M_k += 2 d (p x g)
@@ -725,6 +743,60 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
       for (int w = 1; w < kBlock / 64; ++w) s += rbf_acc[w][src];
     }
     out.partials[(int64_t)t * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Depth-sensor raycast (src/depthsensors.jl:56-97, doRaycast): secant march
+// along each ray on the scene SDF from the sensor origin:
+//   step = -last/est_grad, clamped to |step| <= 0.4; est_grad starts at -1;
+//   stop when |SDF| <= 1e-5 or after 60 steps; depth = NaN when the final
+//   |SDF| > 1e-2. One lane per ray; each step is one wave-cooperative
+//   scene_eval (lanes that have converged ride along as invalid).
+// ---------------------------------------------------------------------------
+struct RayOrigin {
+  double x, y, z;
+};
+
+template <typename T, int SLOTS, bool CULL, bool RBF>
+__global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)) void
+raycast_kernel(RayOrigin o, const double* __restrict__ rays, int64_t n, PassModel<T> m, double* __restrict__ depth) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  __shared__ __attribute__((aligned(32))) T stage[kBlock / 64][4 * kStageRows];
+  const T EPS = (T)1e-5, SAFE_RATE = (T)0.4;
+  const int SAFE_ITER_LIMIT = 60;
+  const T ox = (T)o.x, oy = (T)o.y, oz = (T)o.z;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t base = (int64_t)blockIdx.x * kBlock + wave * 64; base < n; base += stride) {
+    const int64_t i = base + lane;
+    const bool valid = i < n;
+    const int64_t ii = valid ? i : n - 1;
+    const T rx = (T)rays[3 * ii + 0], ry = (T)rays[3 * ii + 1], rz = (T)rays[3 * ii + 2];
+    T dist = (T)0, est = (T)-1, last, gx, gy, gz;
+    int bk, k = 0;
+    scene_eval<T, SLOTS, CULL, RBF>(ox + dist * rx, oy + dist * ry, oz + dist * rz, valid, m, stage[wave], nullptr,
+                                    last, bk, gx, gy, gz);
+    bool active = valid && fabs(last) > EPS;
+    while (__any(active)) {
+      T step = (T)0;
+      if (active) {
+        step = -last / est;
+        const T a = fabs(step);
+        step = copysign(a < SAFE_RATE ? a : SAFE_RATE, step);
+        dist += step;
+      }
+      T v;
+      scene_eval<T, SLOTS, CULL, RBF>(ox + dist * rx, oy + dist * ry, oz + dist * rz, active, m, stage[wave],
+                                      nullptr, v, bk, gx, gy, gz);
+      if (active) {
+        est = (v - last) / step;
+        last = v;
+        ++k;
+        active = fabs(last) > EPS && k < SAFE_ITER_LIMIT;
+      }
+    }
+    if (valid) depth[i] = fabs(last) > (T)1000 * EPS ? __builtin_nan("") : (double)dist;
   }
 }
 
@@ -820,6 +892,57 @@ hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const Pos
                        int64_t n, int nblocks, const PassOutputs& out, hipStream_t s) {
   if (precision == 64) launch_pass_p<double>(cull, lm, pm, d_pts, n, nblocks, out, s);
   else launch_pass_p<float>(cull, lm, pm, d_pts, n, nblocks, out, s);
+  return hipGetLastError();
+}
+
+template <typename T, bool CULL, bool RBF>
+static void launch_raycast_t(const LocalModel& lm, const PosedModel& pm, const double* origin, const double* rays,
+                             int64_t n, double* depth, hipStream_t s) {
+  PassModel<T> m;
+  m.K = lm.K;
+  m.S = lm.S;
+  m.R = lm.R;
+  m.hull_surface = lm.hull_surface;
+  m.surface_kind = lm.surface_kind;
+  m.rbf_surface = lm.rbf_surface;
+  m.rbf_row_off = lm.rbf_row_off;
+  m.rbf_acc_off = lm.rbf_acc_off;
+  m.rbf_rows = (const T*)pm.rbf_rows;
+  m.face_off = lm.face_off;
+  m.vert_off = lm.vert_off;
+  m.nbr = lm.face_nbr;
+  m.planes = (const T*)pm.planes_w;
+  m.facex = (const T*)pm.facex_w;
+  m.verts = (const T*)pm.verts_w;
+  m.hscale = (const T*)pm.hscale_w;
+  m.spheres = pm.spheres_w;
+  const RayOrigin o{origin[0], origin[1], origin[2]};
+  const int nb = pass_blocks(n);
+  if (lm.S <= 64)
+    hipLaunchKernelGGL((raycast_kernel<T, 1, CULL, RBF>), dim3(nb), dim3(kBlock), 0, s, o, rays, n, m, depth);
+  else if (lm.S <= 128)
+    hipLaunchKernelGGL((raycast_kernel<T, 2, CULL, RBF>), dim3(nb), dim3(kBlock), 0, s, o, rays, n, m, depth);
+  else
+    hipLaunchKernelGGL((raycast_kernel<T, 4, CULL, RBF>), dim3(nb), dim3(kBlock), 0, s, o, rays, n, m, depth);
+}
+
+template <typename T>
+static void launch_raycast_p(bool cull, const LocalModel& lm, const PosedModel& pm, const double* origin,
+                             const double* rays, int64_t n, double* depth, hipStream_t s) {
+  if (lm.R > 0) {
+    if (cull) launch_raycast_t<T, true, true>(lm, pm, origin, rays, n, depth, s);
+    else launch_raycast_t<T, false, true>(lm, pm, origin, rays, n, depth, s);
+  } else {
+    if (cull) launch_raycast_t<T, true, false>(lm, pm, origin, rays, n, depth, s);
+    else launch_raycast_t<T, false, false>(lm, pm, origin, rays, n, depth, s);
+  }
+}
+
+hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const double* origin,
+                          const double* d_rays, int64_t n, double* d_depth, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (precision == 64) launch_raycast_p<double>(cull, lm, pm, origin, d_rays, n, d_depth, s);
+  else launch_raycast_p<float>(cull, lm, pm, origin, d_rays, n, d_depth, s);
   return hipGetLastError();
 }
 

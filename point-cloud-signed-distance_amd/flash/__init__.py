@@ -24,4 +24,10 @@ def __getattr__(name):
     if name == "Tracking":
         from . import tracking
         return tracking
+    if name == "DepthSensors":
+        from . import depthsensors
+        return depthsensors
+    if name == "DepthData":
+        from . import depthdata
+        return depthdata
     raise AttributeError(name)

@@ -65,6 +65,7 @@ _PROTOS = {
     "fsdf_eval_device": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "fsdf_skin": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "fsdf_synchronize": (c_int32, [c_void_p]),
+    "fsdf_raycast": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "fsdf_profile_pass": (c_int32, [c_void_p, c_int32]),
     "fsdf_pass_time": (c_int32, [c_void_p, POINTER(c_double), POINTER(c_int64)]),
     "fsdf_kernel_stats": (c_int32, [c_void_p, c_int32, c_void_p]),
@@ -230,6 +231,15 @@ class Context:
         g = np.empty((n, 3), np.float64)
         check(self._lib.fsdf_skin(self._ctx, ptr(p), ptr(q), n, ptr(d), ptr(k), ptr(g)), self._ctx, "skin")
         return d, k, g
+
+    def raycast(self, poses, origin, rays):
+        """Secant raycast of unit world rays [n,3] from origin -> depth [n] (NaN = miss)."""
+        p = self._poses(poses)
+        o = np.ascontiguousarray(origin, np.float64).reshape(3)
+        r = np.ascontiguousarray(rays, np.float64).reshape(-1, 3)
+        depth = np.empty(len(r), np.float64)
+        check(self._lib.fsdf_raycast(self._ctx, ptr(p), ptr(o), ptr(r), len(r), ptr(depth)), self._ctx, "raycast")
+        return depth
 
     def synchronize(self):
         check(self._lib.fsdf_synchronize(self._ctx), self._ctx, "synchronize")

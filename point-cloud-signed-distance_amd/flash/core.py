@@ -196,6 +196,11 @@ class SceneSkin:
         d, _, _ = self.evaluate(x)
         return float(d[0]) if x.ndim == 1 else d
 
+    def raycast(self, origin, rays):
+        """Depth along each unit world ray (src/depthsensors.jl:56-97) on the GPU."""
+        poses, _ = prepare_pass(self.ctx, self.state.manipulator, self.q, self.deformation_data)
+        return self.ctx.raycast(poses, origin, rays)
+
 
 def surfaces(state: ManipulatorState) -> list:
     """surfaces(state) (src/Flash.jl:261-263): one posed evaluator per surface."""

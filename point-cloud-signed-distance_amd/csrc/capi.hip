@@ -59,7 +59,7 @@ struct fsdf_ctx {
   int32_t* d_face_off = nullptr;
   int32_t* d_vert_hull = nullptr;
   int32_t* d_vert_off = nullptr;
-  int32_t* d_face_nbr = nullptr;
+  int32_t* d_face_rows = nullptr;
   int32_t* d_hull_surface = nullptr;
   int32_t* d_surface_kind = nullptr;
   int32_t* d_rbf_surface = nullptr;
@@ -128,7 +128,7 @@ static void free_model(fsdf_ctx* c) {
   dfree(c->d_face_off);
   dfree(c->d_vert_hull);
   dfree(c->d_vert_off);
-  dfree(c->d_face_nbr);
+  dfree(c->d_face_rows);
   dfree(c->d_hull_surface);
   dfree(c->d_surface_kind);
   dfree(c->d_rbf_surface);
@@ -145,7 +145,6 @@ static void free_model(fsdf_ctx* c) {
   dfree(c->pm.verts_w);
   dfree(c->pm.hscale_w);
   dfree(c->pm.planes_w);
-  dfree(c->pm.facex_w);
   dfree(c->pm.spheres_w);
   dfree(c->d_poses);
   dfree(c->d_accum);
@@ -262,7 +261,9 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
                 fsdf::kMaxRbfAccum);
   const int K = (int)hulls.size();
   std::vector<double> verts, planes, sph;
-  std::vector<int32_t> faces, face_hull, face_off, vert_hull, vert_off, face_nbr;
+  std::vector<int32_t> faces, face_hull, face_off, vert_hull, vert_off, face_rows;
+  int stage_bytes = 0;
+  const int tsz_ = c->precision == 64 ? (int)sizeof(double) : (int)sizeof(float);
   face_off.push_back(0);
   vert_off.push_back(0);
   for (int k = 0; k < K; ++k) {
@@ -324,19 +325,46 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
     }
     // face adjacency across each edge v_i -> v_{i+1} (the twin edge's face);
     // an open mesh edge points back at its own face (the certificate then
-    // simply fails over to the exhaustive scan)
+    // simply fails over to the exhaustive scan). Packed with the face's
+    // hull-local vertex indices into one 16-byte row (fsdf_internal.h).
     {
-      const int fbase = face_off.back();
+      if (h.n_vertices > 0xffff || h.n_faces > 0xffff)
+        return fail(c, FSDF_ERR_ARG, "set_model: hull %d has %d vertices / %d faces (limit 65535)", k,
+                    h.n_vertices, h.n_faces);
       std::map<std::pair<int, int>, int> owner;
       for (int f = 0; f < h.n_faces; ++f)
         for (int e = 0; e < 3; ++e) owner[{h.faces[3 * f + e], h.faces[3 * f + (e + 1) % 3]}] = f;
-      for (int f = 0; f < h.n_faces; ++f)
+      for (int f = 0; f < h.n_faces; ++f) {
+        int nb[3];
         for (int e = 0; e < 3; ++e) {
           auto it = owner.find({h.faces[3 * f + (e + 1) % 3], h.faces[3 * f + e]});
-          face_nbr.push_back(fbase + (it == owner.end() ? f : it->second));
+          nb[e] = it == owner.end() ? f : it->second;
         }
+        const int* fv = h.faces + 3 * f;
+        face_rows.push_back((int32_t)((uint32_t)fv[0] | ((uint32_t)fv[1] << 16)));
+        face_rows.push_back((int32_t)((uint32_t)fv[2] | ((uint32_t)nb[0] << 16)));
+        face_rows.push_back((int32_t)((uint32_t)nb[1] | ((uint32_t)nb[2] << 16)));
+        face_rows.push_back(0);
+      }
+      // per-wave LDS stage: plane + vertex rows of 4 T, one 16-byte face row per face
+      stage_bytes = std::max(stage_bytes, (h.n_faces + h.n_vertices) * 4 * tsz_ + 16 * h.n_faces);
     }
     face_off.push_back((int32_t)(face_hull.size()));
+  }
+  // the RBF centre rows are staged through the same buffer, 64 rows at a time at least
+  stage_bytes = (std::max(stage_bytes, 64 * 4 * tsz_) + 15) & ~15;
+  {
+    fsdf::LocalModel probe;
+    probe.K = K;
+    probe.S = S;
+    probe.R = (int)rbf_surface.size();
+    probe.stage_bytes = stage_bytes;
+    const size_t lds = fsdf::pass_lds_bytes(probe, false);
+    if (lds > (size_t)fsdf::kMaxLds)
+      return fail(c, FSDF_ERR_ARG,
+                  "set_model: the largest hull needs %d bytes of LDS stage per wave (%zu per workgroup, limit %d); "
+                  "decimate it",
+                  stage_bytes, lds, fsdf::kMaxLds);
   }
   HIPCHECK(c, hipSetDevice(c->device));
   HIPCHECK(c, hipStreamSynchronize(c->stream));
@@ -351,11 +379,10 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   HIPCHECK(c, dalloc(&c->d_face_off, face_off.size() * sizeof(int32_t)));
   HIPCHECK(c, dalloc(&c->d_vert_hull, vert_hull.size() * sizeof(int32_t)));
   HIPCHECK(c, dalloc(&c->d_vert_off, vert_off.size() * sizeof(int32_t)));
-  HIPCHECK(c, dalloc(&c->d_face_nbr, face_nbr.size() * sizeof(int32_t)));
+  HIPCHECK(c, dalloc(&c->d_face_rows, std::max<size_t>(4, face_rows.size()) * sizeof(int32_t)));
   HIPCHECK(c, dalloc((char**)&c->pm.verts_w, (size_t)V * 4 * tsz));
   HIPCHECK(c, dalloc((char**)&c->pm.hscale_w, (size_t)K * tsz));
   HIPCHECK(c, dalloc((char**)&c->pm.planes_w, (size_t)std::max(F, 1) * 4 * tsz));
-  HIPCHECK(c, dalloc((char**)&c->pm.facex_w, (size_t)F * fsdf::kFaceX * tsz));
   HIPCHECK(c, dalloc(&c->pm.spheres_w, (size_t)K * 4 * sizeof(float)));
   HIPCHECK(c, dalloc(&c->d_poses, (size_t)S * 12 * sizeof(double)));
   const int R = (int)rbf_surface.size();
@@ -393,7 +420,9 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   HIPCHECK(c, hipMemcpy(c->d_face_off, face_off.data(), face_off.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   HIPCHECK(c, hipMemcpy(c->d_vert_hull, vert_hull.data(), vert_hull.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   HIPCHECK(c, hipMemcpy(c->d_vert_off, vert_off.data(), vert_off.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-  HIPCHECK(c, hipMemcpy(c->d_face_nbr, face_nbr.data(), face_nbr.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  if (!face_rows.empty())
+    HIPCHECK(c, hipMemcpy(c->d_face_rows, face_rows.data(), face_rows.size() * sizeof(int32_t),
+                          hipMemcpyHostToDevice));
   for (int i = 0; i < kPoseRing; ++i) {
     if (c->h_poses[i]) (void)hipHostFree(c->h_poses[i]);
     c->h_poses[i] = nullptr;
@@ -411,7 +440,8 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   c->lm.face_off = c->d_face_off;
   c->lm.vert_hull = c->d_vert_hull;
   c->lm.vert_off = c->d_vert_off;
-  c->lm.face_nbr = c->d_face_nbr;
+  c->lm.face_rows = c->d_face_rows;
+  c->lm.stage_bytes = stage_bytes;
   c->lm.S = S;
   c->lm.R = R;
   c->lm.rbf_rows = nrows;

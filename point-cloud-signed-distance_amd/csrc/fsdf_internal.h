@@ -11,11 +11,11 @@
 //     face_off  [K+1]   i32     faces of hull k are [face_off[k], face_off[k+1])
 //     vert_hull [V]     i32     owning hull of each vertex
 //     vert_off  [K+1]   i32     vertices of hull k are [vert_off[k], vert_off[k+1])
-//     face_nbr  [F][3]  i32     face across edge i (v_i -> v_{i+1}) of each face
+//     face_rows [F][4]  i32     packed hull-local (v0|v1<<16, v2|n0<<16, n1|n2<<16, 0):
+//                               vertex indices and the face across edge i (v_i -> v_{i+1})
 //
 //   posed model (rewritten by every evaluation; T = double or float)
 //     planes_w  [F][4]  T       world plane
-//     facex_w   [F][24] T       3 inward edge planes (m_i, o_i) then a, b, c
 //     spheres_w [K][4]  f32     world centroid + radius (culling only)
 //     verts_w   [V][4]  T       world vertices (support/optimality certificate)
 //     hscale_w  [K]     T       max_v |v|_1 over the hull's world vertices
@@ -28,7 +28,7 @@
 namespace fsdf {
 
 constexpr int kBlock = 256;        // 4 waves of 64
-constexpr int kFaceX = 24;         // stride of facex_w rows
+constexpr int kMaxLds = 163840;    // LDS a workgroup may declare (gfx950)
 constexpr int kMaxHulls = 256;     // 4 accumulator slots per lane
 constexpr int kMaxBlocks = 2048;
 constexpr int kMaxRbfAccum = 512;  // Σ (4n+4) over RBF skins (= kMaxRbfAcc in the kernel)
@@ -51,12 +51,12 @@ struct LocalModel {
   const int32_t* face_off = nullptr;
   const int32_t* vert_hull = nullptr;
   const int32_t* vert_off = nullptr;
-  const int32_t* face_nbr = nullptr;
+  const int32_t* face_rows = nullptr;  // [F][4]
+  int stage_bytes = 0;                 // per-wave LDS stage, context precision (multiple of 16)
 };
 
 struct PosedModel {
   void* planes_w = nullptr;   // T
-  void* facex_w = nullptr;    // T
   float* spheres_w = nullptr;
   void* verts_w = nullptr;    // T
   void* hscale_w = nullptr;   // T
@@ -90,6 +90,9 @@ hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d
 hipError_t launch_to_f32(const double* src, float* dst, int64_t count, hipStream_t s);
 
 int pass_blocks(int64_t n);
+
+// dynamic LDS of one pass (raycast=false) / raycast workgroup for this model
+size_t pass_lds_bytes(const LocalModel& lm, bool raycast);
 
 // Morton-order the f64 AoS cloud d_src into d_dst (context precision) and write
 // the permutation d_perm[resident i] = caller index. Synchronizes `s`.

@@ -47,8 +47,8 @@ template <> __device__ __forceinline__ double tinf() { return __builtin_huge_val
 template <> __device__ __forceinline__ float tinf() { return __builtin_huge_valf(); }
 
 // ---------------------------------------------------------------------------
-// Pose kernel: local model + poses -> world-frame planes, edge planes, vertices.
-// One thread per face, then one per hull (spheres).
+// Pose kernel: local model + poses -> world-frame planes and vertices.
+// One thread per face, one per vertex, then one wave per hull (sphere + scale).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void xf_point(const double* P, const double* v, double* o) {
   // o = R v + t, R row-major P[0..8], t = P[9..11]
@@ -61,20 +61,10 @@ __device__ __forceinline__ void rot_vec(const double* P, const double* v, double
   o[1] = __builtin_fma(P[3], v[0], __builtin_fma(P[4], v[1], P[5] * v[2]));
   o[2] = __builtin_fma(P[6], v[0], __builtin_fma(P[7], v[1], P[8] * v[2]));
 }
-__device__ __forceinline__ void cross3(const double* a, const double* b, double* o) {
-  o[0] = __builtin_fma(a[1], b[2], -(a[2] * b[1]));
-  o[1] = __builtin_fma(a[2], b[0], -(a[0] * b[2]));
-  o[2] = __builtin_fma(a[0], b[1], -(a[1] * b[0]));
-}
-__device__ __forceinline__ double dot3(const double* a, const double* b) {
-  return __builtin_fma(a[0], b[0], __builtin_fma(a[1], b[1], a[2] * b[2]));
-}
-
 template <typename T>
 __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const double* __restrict__ poses,
-                                                      T* __restrict__ planes_w, T* __restrict__ facex_w,
-                                                      float* __restrict__ spheres_w, T* __restrict__ verts_w,
-                                                      T* __restrict__ hscale_w) {
+                                                      T* __restrict__ planes_w, float* __restrict__ spheres_w,
+                                                      T* __restrict__ verts_w, T* __restrict__ hscale_w) {
   int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int fv = lm.F + lm.V, fv_pad = (fv + 63) & ~63;
   if (tid >= fv && tid < fv_pad) return;  // padding: hull waves start wave-aligned
@@ -91,28 +81,8 @@ __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const doubl
     rot_vec(P, n, nw);
     // d_w = d + n_w · t
     const double dw = __builtin_fma(nw[0], P[9], __builtin_fma(nw[1], P[10], __builtin_fma(nw[2], P[11], pl[3])));
-    double a[3], b[3], c[3];
-    xf_point(P, lm.verts_l + 3 * lm.faces[3 * f + 0], a);
-    xf_point(P, lm.verts_l + 3 * lm.faces[3 * f + 1], b);
-    xf_point(P, lm.verts_l + 3 * lm.faces[3 * f + 2], c);
-    const double e0[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
-    const double e1[3] = {c[0] - b[0], c[1] - b[1], c[2] - b[2]};
-    const double e2[3] = {a[0] - c[0], a[1] - c[1], a[2] - c[2]};
-    double m0[3], m1[3], m2[3];
-    cross3(nw, e0, m0);
-    cross3(nw, e1, m1);
-    cross3(nw, e2, m2);
-    const double o0 = dot3(m0, a), o1 = dot3(m1, b), o2 = dot3(m2, c);
     T* pw = planes_w + 4 * f;
     pw[0] = (T)nw[0]; pw[1] = (T)nw[1]; pw[2] = (T)nw[2]; pw[3] = (T)dw;
-    T* fx = facex_w + kFaceX * f;
-    fx[0] = (T)m0[0]; fx[1] = (T)m0[1]; fx[2] = (T)m0[2]; fx[3] = (T)o0;
-    fx[4] = (T)m1[0]; fx[5] = (T)m1[1]; fx[6] = (T)m1[2]; fx[7] = (T)o1;
-    fx[8] = (T)m2[0]; fx[9] = (T)m2[1]; fx[10] = (T)m2[2]; fx[11] = (T)o2;
-    fx[12] = (T)a[0]; fx[13] = (T)a[1]; fx[14] = (T)a[2];
-    fx[15] = (T)b[0]; fx[16] = (T)b[1]; fx[17] = (T)b[2];
-    fx[18] = (T)c[0]; fx[19] = (T)c[1]; fx[20] = (T)c[2];
-    fx[21] = (T)0; fx[22] = (T)0; fx[23] = (T)0;
   } else if (tid < lm.F + lm.V) {
     const int v = tid - lm.F;
     const double* P = poses + 12 * lm.hull_surface[lm.vert_hull[v]];
@@ -154,12 +124,16 @@ __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const doubl
 // ---------------------------------------------------------------------------
 // Closest point on triangle (a, b, c) to p — Voronoi-region walk.
 // ---------------------------------------------------------------------------
+template <typename T> struct Row4 { typedef T __attribute__((ext_vector_type(4))) type; };
+typedef int I4 __attribute__((ext_vector_type(4)));
+
 template <typename T>
-__device__ __forceinline__ void closest_on_triangle(T px, T py, T pz, const T* __restrict__ v, T& qx,
-                                                    T& qy, T& qz) {
-  const T ax = v[0], ay = v[1], az = v[2];
-  const T bx = v[3], by = v[4], bz = v[5];
-  const T cx = v[6], cy = v[7], cz = v[8];
+__device__ __forceinline__ void closest_on_triangle(T px, T py, T pz, const typename Row4<T>::type& A,
+                                                    const typename Row4<T>::type& B,
+                                                    const typename Row4<T>::type& C, T& qx, T& qy, T& qz) {
+  const T ax = A[0], ay = A[1], az = A[2];
+  const T bx = B[0], by = B[1], bz = B[2];
+  const T cx = C[0], cy = C[1], cz = C[2];
   const T abx = bx - ax, aby = by - ay, abz = bz - az;
   const T acx = cx - ax, acy = cy - ay, acz = cz - az;
   const T apx = px - ax, apy = py - ay, apz = pz - az;
@@ -200,12 +174,27 @@ __device__ __forceinline__ void closest_on_triangle(T px, T py, T pz, const T* _
   qz = mfma_(w_, acz, mfma_(v_, abz, az));
 }
 
+// Inward edge-plane value of edge u -> w of a face with unit normal n:
+//   m = n x (w - u),  s = m·p − m·u   (s >= 0 on the triangle's side).
+// Same operation order as oracle/flash_oracle.c (its pose step precomputes m, m·u).
+template <typename T>
+__device__ __forceinline__ T edge_value(const typename Row4<T>::type& n, const typename Row4<T>::type& u,
+                                        const typename Row4<T>::type& w, T px, T py, T pz) {
+  const T e0 = w[0] - u[0], e1 = w[1] - u[1], e2 = w[2] - u[2];
+  const T m0 = mfma_(n[1], e2, -(n[2] * e1));
+  const T m1 = mfma_(n[2], e0, -(n[0] * e2));
+  const T m2 = mfma_(n[0], e1, -(n[1] * e0));
+  const T o = mfma_(m0, u[0], mfma_(m1, u[1], m2 * u[2]));
+  return mfma_(m0, px, mfma_(m1, py, mfma_(m2, pz, -o)));
+}
+
 // Posed model as the pass kernel sees it (device pointers, world frame).
 template <typename T>
 struct PassModel {
   int K;  // hulls
   int S;  // surfaces (hulls + RBF skins), the k* index space
   int R;  // RBF skins
+  int stage_bytes;  // LDS stage per wave (bytes, multiple of 16)
   const int32_t* __restrict__ hull_surface;  // [K] surface index of hull h
   const int32_t* __restrict__ surface_kind;  // [S] FSDF_SURFACE_*
   const int32_t* __restrict__ rbf_surface;   // [R] surface index of RBF skin r
@@ -214,35 +203,61 @@ struct PassModel {
   const T* __restrict__ rbf_rows;            // [rows][4] (c, w) ... (a, b)
   const int32_t* __restrict__ face_off;
   const int32_t* __restrict__ vert_off;
-  const int32_t* __restrict__ nbr;
+  const I4* __restrict__ face_rows;          // [F] packed local vertex / neighbour indices
   const T* __restrict__ planes;
-  const T* __restrict__ facex;
   const T* __restrict__ verts;
   const T* __restrict__ hscale;
   const float* __restrict__ spheres;
 };
 
+// Per-workgroup LDS hull table, filled once in the kernel prologue (row K is
+// a sentinel holding face_off[K] / vert_off[K]): the per-lane culling loops and
+// every hull evaluation read it at LDS latency instead of a global round trip.
+typedef float F4 __attribute__((ext_vector_type(4)));
+struct HullRow {
+  F4 sphere;      // world centroid + radius (f32, exact-safe culling)
+  int f0, v0;     // first face / vertex of the hull
+  double hscale;  // certificate scale max_v |v|_1
+};
+static_assert(sizeof(HullRow) == 32, "HullRow is 32 bytes");
+
+// fill the table (whole workgroup; ends with a barrier) and return the
+// culling-margin scale smax = max_k |c_k|_1 + 2 r_k (wave-uniform)
 template <typename T>
-__device__ __forceinline__ T plane_value(const T* __restrict__ pl, T px, T py, T pz) {
-  return mfma_(pl[0], px, mfma_(pl[1], py, mfma_(pl[2], pz, -pl[3])));
+__device__ __forceinline__ float load_hull_table(const PassModel<T>& m, HullRow* __restrict__ ht) {
+  for (int k = threadIdx.x; k <= m.K; k += kBlock) {
+    HullRow r;
+    r.sphere = k < m.K ? ((const F4*)m.spheres)[k] : F4{0.f, 0.f, 0.f, 0.f};
+    r.f0 = m.face_off[k];
+    r.v0 = m.vert_off[k];
+    r.hscale = k < m.K ? (double)m.hscale[k] : 0.0;
+    ht[k] = r;
+  }
+  __syncthreads();
+  float smax = 0.f;
+  for (int k = threadIdx.x & 63; k < m.K; k += 64) {
+    const F4 sp = ht[k].sphere;
+    smax = fmaxf(smax, fabsf(sp[0]) + fabsf(sp[1]) + fabsf(sp[2]) + 2.0f * sp[3]);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) smax = fmaxf(smax, __shfl_xor(smax, off, 64));
+  return smax;
 }
 
-// Per-wave LDS staging of the evaluated hull's rows (planes, then vertices):
-// one coalesced bulk copy per chunk (dwordx4 loads, every row in flight at
-// once), then wave-uniform broadcast ds_read_b128 in the loops, instead of a
-// dependent scalar-load chain per row.
-constexpr int kStagePlanes = 128;  // plane rows per chunk
-constexpr int kStageVerts = 64;    // vertex rows per chunk
-constexpr int kStageRows = kStagePlanes + kStageVerts;
 constexpr int kMaxRbfAcc = kMaxRbfAccum;  // RBF adjoint doubles per wave (Σ 4n+4)
+// Diagnostic ablations (timing-only builds via -DFSDF_ABLATE=mask; results are
+// wrong): 4 no slow path, 16 no segmented reduction, 32 no per-point stores,
+// 64 no hull staging loads (LDS stage left as is).
+#ifndef FSDF_ABLATE
+#define FSDF_ABLATE 0
+#endif
 #ifndef FSDF_PASS_WAVES_PER_SIMD
 #define FSDF_PASS_WAVES_PER_SIMD 4
 #endif
 constexpr int kPassWavesPerSimd = FSDF_PASS_WAVES_PER_SIMD;  // occupancy target (VGPR budget 512/w)
 
-template <typename T> struct Row4 { typedef T __attribute__((ext_vector_type(4))) type; };
-
-// Must be called with every lane of the wave active (wave-uniform control flow).
+// Row-chunked per-wave LDS staging (RBF centre rows). Must be called with
+// every lane of the wave active (wave-uniform control flow).
 template <typename T>
 __device__ __forceinline__ void stage_rows(T* __restrict__ lds, const T* __restrict__ src, int rows) {
   typedef typename Row4<T>::type R;
@@ -252,10 +267,42 @@ __device__ __forceinline__ void stage_rows(T* __restrict__ lds, const T* __restr
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// One bulk copy of everything hull k's evaluation reads — plane rows, vertex
+// rows, packed face rows — into this wave's LDS stage: every 16-byte chunk of
+// the hull is loaded before any is stored, so the wave pays ONE global-memory
+// latency per hull evaluation; all later reads (broadcast plane reads, per-lane
+// triangle / neighbour / certificate reads) are LDS. Whole wave active.
 template <typename T>
-__device__ __forceinline__ T row_plane_value(const T* __restrict__ lrow, T px, T py, T pz) {
-  typedef typename Row4<T>::type R;
-  const R pl = *(const R*)lrow;
+__device__ __forceinline__ void stage_hull(T* __restrict__ lw, const T* __restrict__ planes,
+                                           const T* __restrict__ verts, const I4* __restrict__ frows, int nf,
+                                           int nv) {
+  constexpr int cpr = (int)sizeof(T) / 4;  // 16-byte chunks per row of 4 T
+  const int P = nf * cpr, Q = P + nv * cpr, N = Q + nf;
+  const int lane = threadIdx.x & 63;
+  const I4* sp = (const I4*)planes;
+  const I4* sv = (const I4*)verts;
+  I4* dst = (I4*)lw;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  for (int c0 = 0; c0 < N; c0 += 8 * 64) {
+    I4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = min(c0 + 64 * j + lane, N - 1);
+      const I4* src = c < P ? sp + c : (c < Q ? sv + (c - P) : frows + (c - Q));
+      if (!(FSDF_ABLATE & 64)) v[j] = *src;
+      else v[j] = I4{c, c, c, 0};
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + 64 * j + lane;
+      if (c < N) dst[c] = v[j];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <typename T>
+__device__ __forceinline__ T plane_h(const typename Row4<T>::type& pl, T px, T py, T pz) {
   return mfma_(pl[0], px, mfma_(pl[1], py, mfma_(pl[2], pz, -pl[3])));
 }
 
@@ -263,29 +310,42 @@ template <typename T> __device__ __forceinline__ T cert_eps();
 template <> __device__ __forceinline__ double cert_eps() { return 1e-13; }
 template <> __device__ __forceinline__ float cert_eps() { return 4e-6f; }
 
-// Optimality certificate of a candidate closest point q of hull k (the GJK
-// termination test): q is the closest point of conv(V) to p iff
+// Optimality certificate of a candidate closest point q of the staged hull
+// (the GJK termination test): q is the closest point of conv(V) to p iff
 // max_v (p-q)·v <= (p-q)·q; accepted within a rounding tolerance.
 template <typename T>
-__device__ __forceinline__ bool certified(T px, T py, T pz, T qx, T qy, T qz, int v0, int v1,
-                                          const T* __restrict__ verts, T scale, T* __restrict__ lw) {
+__device__ __forceinline__ bool certified(T px, T py, T pz, T qx, T qy, T qz, const typename Row4<T>::type* lv,
+                                          int nv, T scale) {
   typedef typename Row4<T>::type R;
   const T wx = px - qx, wy = py - qy, wz = pz - qz;
   const T wq = mfma_(wx, qx, mfma_(wy, qy, wz * qz));
-  T smax = -tinf<T>();
-  T* lv = lw + 4 * kStagePlanes;
-  for (int c0 = v0; c0 < v1; c0 += kStageVerts) {
-    const int cn = min(kStageVerts, v1 - c0);
-    stage_rows(lv, verts + 4 * c0, cn);
+  T sA = -tinf<T>(), sB = -tinf<T>();
+  int v = 0;
 #pragma unroll 4
-    for (int v = 0; v < cn; ++v) {
-      const R vv = *(const R*)(lv + 4 * v);
-      const T sv = mfma_(vv[0], wx, mfma_(vv[1], wy, vv[2] * wz));
-      smax = sv > smax ? sv : smax;
-    }
+  for (; v + 1 < nv; v += 2) {
+    const R a = lv[v], b = lv[v + 1];
+    const T sa = mfma_(a[0], wx, mfma_(a[1], wy, a[2] * wz));
+    const T sb = mfma_(b[0], wx, mfma_(b[1], wy, b[2] * wz));
+    sA = sa > sA ? sa : sA;
+    sB = sb > sB ? sb : sB;
   }
+  if (v < nv) {
+    const R a = lv[v];
+    const T sa = mfma_(a[0], wx, mfma_(a[1], wy, a[2] * wz));
+    sA = sa > sA ? sa : sA;
+  }
+  const T smax = sB > sA ? sB : sA;
   const T tol = cert_eps<T>() * ((fabs(wx) + fabs(wy)) + fabs(wz)) * scale;
   return smax <= wq + tol;
+}
+
+// packed face row: (i0 | i1<<16, i2 | n0<<16, n1 | n2<<16, 0) with i_j the
+// hull-local vertex indices and n_e the hull-local face across edge e (i_e -> i_e+1)
+__device__ __forceinline__ int fr_vert(const I4& r, int j) {
+  return j == 0 ? (r[0] & 0xffff) : (j == 1 ? ((r[0] >> 16) & 0xffff) : (r[1] & 0xffff));
+}
+__device__ __forceinline__ int fr_nbr(const I4& r, int e) {
+  return e == 0 ? ((r[1] >> 16) & 0xffff) : (e == 1 ? (r[2] & 0xffff) : ((r[2] >> 16) & 0xffff));
 }
 
 // ---------------------------------------------------------------------------
@@ -297,69 +357,75 @@ __device__ __forceinline__ bool certified(T px, T py, T pz, T qx, T qy, T qz, in
 //     test over the hull's vertices, and only uncertified lanes fall back to the
 //     exhaustive scan of the visible faces.
 // `active`: this lane's result is used (gates the wave-uniform slow branches).
-// `lw`: this wave's LDS stage (kStageRows rows of 4 T).
+// `bound`: the lane's best distance so far (only a result below it matters).
+// `lw`: this wave's LDS stage (m.stage_bytes). Whole wave active.
 // ---------------------------------------------------------------------------
 template <typename T>
-__device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassModel<T>& m, bool active, T& d,
-                                         T& gx, T& gy, T& gz, T* __restrict__ lw,
-                                         unsigned long long* __restrict__ stats) {
-  const int f0 = __builtin_amdgcn_readfirstlane(m.face_off[k]);
-  const int f1 = __builtin_amdgcn_readfirstlane(m.face_off[k + 1]);
+__device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassModel<T>& m,
+                                         const HullRow* __restrict__ ht, bool active, T bound, T& d, T& gx, T& gy,
+                                         T& gz, T* __restrict__ lw, unsigned long long* __restrict__ stats) {
+  typedef typename Row4<T>::type R;
+  const int f0 = __builtin_amdgcn_readfirstlane(ht[k].f0);
+  const int nf = __builtin_amdgcn_readfirstlane(ht[k + 1].f0) - f0;
+  const int v0 = __builtin_amdgcn_readfirstlane(ht[k].v0);
+  const int nv = __builtin_amdgcn_readfirstlane(ht[k + 1].v0) - v0;
+  stage_hull(lw, m.planes + 4 * f0, m.verts + 4 * v0, m.face_rows + f0, nf, nv);
+  const R* lp = (const R*)lw;
+  const R* lv = lp + nf;
+  const I4* lf = (const I4*)(lv + nv);
   // two independent running maxima (even / odd faces) shorten the serial
   // compare chain; merged with the first-index rule, identical to one chain
   T hA = -tinf<T>(), hB = -tinf<T>();
-  int iA = f0, iB = f0;
-  for (int c0 = f0; c0 < f1; c0 += kStagePlanes) {
-    const int cn = min(kStagePlanes, f1 - c0);
-    stage_rows(lw, m.planes + 4 * c0, cn);
-    int i = 0;
+  int iA = 0, iB = 0;
+  int i = 0;
 #pragma unroll 4
-    for (; i + 1 < cn; i += 2) {
-      const T ha = row_plane_value(lw + 4 * i, px, py, pz);
-      const T hb = row_plane_value(lw + 4 * i + 4, px, py, pz);
-      if (ha > hA) { hA = ha; iA = c0 + i; }
-      if (hb > hB) { hB = hb; iB = c0 + i + 1; }
-    }
-    if (i < cn) {
-      const T ha = row_plane_value(lw + 4 * i, px, py, pz);
-      if (ha > hA) { hA = ha; iA = c0 + i; }
-    }
+  for (; i + 1 < nf; i += 2) {
+    const T ha = plane_h<T>(lp[i], px, py, pz);
+    const T hb = plane_h<T>(lp[i + 1], px, py, pz);
+    if (ha > hA) { hA = ha; iA = i; }
+    if (hb > hB) { hB = hb; iB = i + 1; }
+  }
+  if (i < nf) {
+    const T ha = plane_h<T>(lp[i], px, py, pz);
+    if (ha > hA) { hA = ha; iA = i; }
   }
   if (hB > hA || (hB == hA && iB < iA)) { hA = hB; iA = iB; }
   const T hmax = hA;
-  const int fs = iA;
-  const T* pls = m.planes + 4 * fs;
+  const int fs = iA;  // hull-local
+  const R ns = lp[fs];
   d = hmax;
-  gx = pls[0]; gy = pls[1]; gz = pls[2];
+  gx = ns[0]; gy = ns[1]; gz = ns[2];
   bool slow = false;
   T s0 = (T)0, s1 = (T)0, s2 = (T)0;
   if (hmax > (T)0) {
     // Fast path: the projection of p on the max-violated face lies inside that
     // triangle => it is the closest point and the distance equals hmax.
-    const T* fx = m.facex + kFaceX * fs;
-    s0 = mfma_(fx[0], px, mfma_(fx[1], py, mfma_(fx[2], pz, -fx[3])));
-    s1 = mfma_(fx[4], px, mfma_(fx[5], py, mfma_(fx[6], pz, -fx[7])));
-    s2 = mfma_(fx[8], px, mfma_(fx[9], py, mfma_(fx[10], pz, -fx[11])));
+    const I4 fr = lf[fs];
+    const R a = lv[fr_vert(fr, 0)], b = lv[fr_vert(fr, 1)], c = lv[fr_vert(fr, 2)];
+    s0 = edge_value<T>(ns, a, b, px, py, pz);
+    s1 = edge_value<T>(ns, b, c, px, py, pz);
+    s2 = edge_value<T>(ns, c, a, px, py, pz);
     slow = !(s0 >= (T)0 && s1 >= (T)0 && s2 >= (T)0);
   }
-  slow = slow && active;
+  // hmax is a lower bound of the distance: when it exceeds the lane's best so
+  // far by more than the rounding of either value, hull k cannot win (nor tie)
+  // and its exact distance is not needed — d stays hmax (> bound).
+  const T scale = (T)ht[k].hscale;
+  const T lb_margin = (T)16 * cert_eps<T>() * (scale + ((fabs(px) + fabs(py)) + fabs(pz)));
+  slow = slow && active && !(hmax - lb_margin > bound) && !(FSDF_ABLATE & 4);
   const uint64_t slow_mask = __ballot(slow);
   if (!slow_mask) return;
   if (stats && (threadIdx.x & 63) == 0) {
     atomicAdd(stats + 2, 1ull);
     atomicAdd(stats + 4, (unsigned long long)__builtin_popcountll(slow_mask));
   }
-  const int v0 = __builtin_amdgcn_readfirstlane(m.vert_off[k]);
-  const int v1 = __builtin_amdgcn_readfirstlane(m.vert_off[k + 1]);
-  const T scale = m.hscale[k];
   // stage A: closest point on triangle f*
+  const I4 frs = lf[fs];
   T qx, qy, qz;
-  closest_on_triangle(px, py, pz, m.facex + kFaceX * fs + 12, qx, qy, qz);
+  closest_on_triangle<T>(px, py, pz, lv[fr_vert(frs, 0)], lv[fr_vert(frs, 1)], lv[fr_vert(frs, 2)], qx, qy, qz);
   T ex = px - qx, ey = py - qy, ez = pz - qz;
   T best2 = mfma_(ex, ex, mfma_(ey, ey, ez * ez));
-  // (the certificate stages rows cooperatively: call it with the whole wave)
-  const bool certA = certified(px, py, pz, qx, qy, qz, v0, v1, m.verts, scale, lw);
-  bool todo = slow && !certA;
+  bool todo = slow && !certified(px, py, pz, qx, qy, qz, lv, nv, scale);
   if (__any(todo)) {
     // stage B: the neighbours across the violated edges of f*
     if (stats && (threadIdx.x & 63) == 0) atomicAdd(stats + 6, 1ull);
@@ -367,16 +433,15 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
       if (todo && sv[e] < (T)0) {
-        const int g = m.nbr[3 * fs + e];
+        const I4 gr = lf[fr_nbr(frs, e)];
         T cx, cy, cz;
-        closest_on_triangle(px, py, pz, m.facex + kFaceX * g + 12, cx, cy, cz);
+        closest_on_triangle<T>(px, py, pz, lv[fr_vert(gr, 0)], lv[fr_vert(gr, 1)], lv[fr_vert(gr, 2)], cx, cy, cz);
         const T dx = px - cx, dy = py - cy, dz = pz - cz;
         const T d2 = mfma_(dx, dx, mfma_(dy, dy, dz * dz));
         if (d2 < best2) { best2 = d2; qx = cx; qy = cy; qz = cz; }
       }
     }
-    const bool certB = certified(px, py, pz, qx, qy, qz, v0, v1, m.verts, scale, lw);
-    todo = todo && !certB;
+    todo = todo && !certified(px, py, pz, qx, qy, qz, lv, nv, scale);
     const uint64_t scan_mask = __ballot(todo);
     if (scan_mask) {
       // stage C: exhaustive scan of the visible faces (the closest boundary
@@ -385,11 +450,13 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
       if (stats && (threadIdx.x & 63) == 0) atomicAdd(stats + 7, (unsigned long long)__builtin_popcountll(scan_mask));
       T b2 = tinf<T>();
       T bx = (T)0, by = (T)0, bz = (T)0;
-      for (int ff = f0; ff < f1; ++ff) {
-        const T h = plane_value(m.planes + 4 * ff, px, py, pz);
+      for (int ff = 0; ff < nf; ++ff) {
+        const T h = plane_h<T>(lp[ff], px, py, pz);
         if (todo && h > (T)0 && h * h < b2) {
+          const I4 gr = lf[ff];
           T cx, cy, cz;
-          closest_on_triangle(px, py, pz, m.facex + kFaceX * ff + 12, cx, cy, cz);
+          closest_on_triangle<T>(px, py, pz, lv[fr_vert(gr, 0)], lv[fr_vert(gr, 1)], lv[fr_vert(gr, 2)], cx, cy,
+                                 cz);
           const T dx = px - cx, dy = py - cy, dz = pz - cz;
           const T d2 = mfma_(dx, dx, mfma_(dy, dy, dz * dz));
           if (d2 < b2) { b2 = d2; bx = cx; by = cy; bz = cz; }
@@ -423,14 +490,14 @@ struct RbfField {
 
 template <typename T>
 __device__ __forceinline__ void rbf_field(T px, T py, T pz, const T* __restrict__ rows, int nc,
-                                          T* __restrict__ lw, RbfField<T>& F) {
+                                          T* __restrict__ lw, int cap, RbfField<T>& F) {
   typedef typename Row4<T>::type R4;
   const R4 poly = *(const R4*)(rows + 4 * nc);
   F.f = mfma_(poly[1], px, mfma_(poly[2], py, mfma_(poly[3], pz, poly[0])));
   F.gx = poly[1]; F.gy = poly[2]; F.gz = poly[3];
   F.hxx = F.hyy = F.hzz = F.hxy = F.hxz = F.hyz = (T)0;
-  for (int c0 = 0; c0 < nc; c0 += kStageRows) {
-    const int cn = min(kStageRows, nc - c0);
+  for (int c0 = 0; c0 < nc; c0 += cap) {
+    const int cn = min(cap, nc - c0);
     stage_rows(lw, rows + 4 * c0, cn);
     for (int i = 0; i < cn; ++i) {
       const R4 c = *(const R4*)(lw + 4 * i);
@@ -481,18 +548,18 @@ __device__ __forceinline__ double wave_sum(double v) {
 //   acc[0..n) = λ_w, acc[n] = λ_a, acc[n+1..n+4) = λ_b, acc[n+4+3i..] = E_i.
 template <typename T>
 __device__ __forceinline__ void rbf_adjoint(T px, T py, T pz, const T* __restrict__ rows, int nc,
-                                            T* __restrict__ lw, bool sel, double* __restrict__ acc) {
+                                            T* __restrict__ lw, int cap, bool sel, double* __restrict__ acc) {
   typedef typename Row4<T>::type R4;
   RbfField<T> F;
-  rbf_field(px, py, pz, rows, nc, lw, F);
+  rbf_field(px, py, pz, rows, nc, lw, cap, F);
   T s, sgx, sgy, sgz, c, invG;
   rbf_skin_from_field(F, s, sgx, sgy, sgz, c, invG);
   const T two_s = (T)2 * s;
   const T dsdf = invG;
   const T ux = -c * F.gx, uy = -c * F.gy, uz = -c * F.gz;  // ∂s/∂∇f
   const int lane = threadIdx.x & 63;
-  for (int c0 = 0; c0 < nc; c0 += kStageRows) {
-    const int cn = min(kStageRows, nc - c0);
+  for (int c0 = 0; c0 < nc; c0 += cap) {
+    const int cn = min(cap, nc - c0);
     stage_rows(lw, rows + 4 * c0, cn);
     for (int i = 0; i < cn; ++i) {
       const R4 cw = *(const R4*)(lw + 4 * i);
@@ -532,29 +599,29 @@ __device__ __forceinline__ void rbf_adjoint(T px, T py, T pz, const T* __restric
 // active; `valid` marks lanes whose result is used.
 // ---------------------------------------------------------------------------
 template <typename T, int SLOTS, bool CULL, bool RBF>
-__device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const PassModel<T>& m, T* __restrict__ lw,
+__device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const PassModel<T>& m,
+                                           const HullRow* __restrict__ ht, float smax, T* __restrict__ lw,
                                            unsigned long long* __restrict__ stats, T& best, int& bk, T& gx, T& gy,
                                            T& gz) {
   const int K = m.K;
-  const float* __restrict__ spheres = m.spheres;
   const int lane = threadIdx.x & 63;
   // Phase A (fp32, exact-safe): with c_k inside hull k and r_k its bounding
   // radius, d_k(p) >= |p-c_k| - r_k (lower bound) and d_k(p) <= |p-c_k|
   // (upper bound). ub = min_k |p-c_k|; the best-first seed is the hull of
   // least power distance |p-c_k|^2 - r_k^2 (a heuristic: any seed is exact).
-  float ub2 = __builtin_huge_valf(), pw_min = __builtin_huge_valf(), smax = 0.f;
+  float ub2 = __builtin_huge_valf(), pw_min = __builtin_huge_valf();
   int kseed = 0;
   float pxf = 0.f, pyf = 0.f, pzf = 0.f;
   if (CULL) {
     pxf = (float)px; pyf = (float)py; pzf = (float)pz;
+#pragma unroll 4
     for (int k = 0; k < K; ++k) {
-      const float* sp = spheres + 4 * k;
+      const F4 sp = ht[k].sphere;
       const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
       const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
       ub2 = fminf(ub2, dist2);
       const float pwr = __builtin_fmaf(-sp[3], sp[3], dist2);
       if (pwr < pw_min) { pw_min = pwr; kseed = k; }
-      smax = fmaxf(smax, fabsf(sp[0]) + fabsf(sp[1]) + fabsf(sp[2]) + 2.0f * sp[3]);
     }
   }
   const float ub = __builtin_sqrtf(ub2);
@@ -571,7 +638,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
       const int r0 = m.rbf_row_off[r];
       const int nc = m.rbf_row_off[r + 1] - r0 - 1;
       RbfField<T> F;
-      rbf_field(px, py, pz, m.rbf_rows + 4 * r0, nc, lw, F);
+      rbf_field(px, py, pz, m.rbf_rows + 4 * r0, nc, lw, m.stage_bytes / (4 * (int)sizeof(T)), F);
       T sv, hx, hy, hz, c_, iG;
       rbf_skin_from_field(F, sv, hx, hy, hz, c_, iG);
       if (valid && (sv < best || (sv == best && ks < bk))) { best = sv; bk = ks; gx = hx; gy = hy; gz = hz; }
@@ -583,7 +650,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   // tested without a sqrt: |p-c_k|^2 <= (min(ub, best) + mrg + r_k)^2
   auto needs = [&](int k) -> bool {
     if (!CULL) return valid;
-    const float* sp = spheres + 4 * k;
+    const F4 sp = ht[k].sphere;
     const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
     const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
     const float t = fminf(ub, (float)best) + mrg + sp[3];
@@ -592,7 +659,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   // evaluations may run out of index order: ties keep the smaller k
   auto evaluate = [&](int k, bool need) {
     T dk, hx, hy, hz;
-    hull_sdf<T>(px, py, pz, k, m, need, dk, hx, hy, hz, lw, stats);
+    hull_sdf<T>(px, py, pz, k, m, ht, need, best, dk, hx, hy, hz, lw, stats);
     if (stats) {
       const uint64_t nm = __ballot(need);
       if (lane == 0) {
@@ -637,27 +704,36 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
 // ---------------------------------------------------------------------------
 // Residual pass.
 // ---------------------------------------------------------------------------
+extern __shared__ __attribute__((aligned(16))) char fsdf_lds[];
+
 template <typename T, int SLOTS, bool CULL, bool RBF>
 __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)) void pass_kernel(
     const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out) {
-  const int K = m.K;
-  const float* __restrict__ spheres = m.spheres;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
+  // All LDS is one dynamic region (16-byte aligned carve, see pass_lds_bytes):
+  //   red     [4 waves][kRedStride] f64  per-hull wrench sums + cost
+  //   rbf_acc [4 waves][kMaxRbfAcc] f64  (RBF variants only)
+  //   stage   [4 waves][m.stage_bytes]   hull / RBF row stage
   // per-hull wrench sums live in LDS from the start: row (s*64 + lane) of
   // this wave's slab is owned by lane `lane` (hull s*64 + lane)
-  __shared__ double red[kBlock / 64][SLOTS * 64 * 6 + 1];
-  double* acc_row = &red[wave][lane * 6];
+  constexpr int kRedStride = SLOTS * 64 * 6 + 2;
+  double* red = (double*)fsdf_lds;
+  double* acc_row = red + wave * kRedStride + lane * 6;
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s)
 #pragma unroll
     for (int j = 0; j < 6; ++j) acc_row[s * 64 * 6 + j] = 0.0;
   double cost_acc = 0.0;
-  __shared__ __attribute__((aligned(32))) T stage[kBlock / 64][4 * kStageRows];
   // RBF adjoint sums of this wave (lane 0 adds)
-  __shared__ double rbf_acc[kBlock / 64][RBF ? kMaxRbfAcc : 1];
+  double* rbf_acc = red + (kBlock / 64) * kRedStride;
+  double* rbf_wave = rbf_acc + wave * kMaxRbfAcc;
+  HullRow* ht = (HullRow*)(fsdf_lds + ((kBlock / 64) * kRedStride + (RBF ? (kBlock / 64) * kMaxRbfAcc : 0)) * 8);
+  T* stage = (T*)((char*)(ht + m.K + 1) + wave * m.stage_bytes);
+  const int stage_cap = m.stage_bytes / (4 * (int)sizeof(T));
   if (RBF)
-    for (int e = lane; e < m.rbf_acc_off[m.R]; e += 64) rbf_acc[wave][e] = 0.0;
+    for (int e = lane; e < m.rbf_acc_off[m.R]; e += 64) rbf_wave[e] = 0.0;
+  const float smax = load_hull_table(m, ht);
 
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t base = (int64_t)blockIdx.x * kBlock + wave * 64; base < n; base += stride) {
@@ -668,7 +744,7 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
 
     T best, gx, gy, gz;
     int bk;
-    scene_eval<T, SLOTS, CULL, RBF>(px, py, pz, valid, m, stage[wave], out.stats, best, bk, gx, gy, gz);
+    scene_eval<T, SLOTS, CULL, RBF>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz);
     if (!valid) bk = 0;
 
     // contributions: c += d^2; F_k += 2 d g; M_k += 2 d (p x g)
@@ -684,7 +760,7 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
       cM[1] = w * __builtin_fma(dpz, dgx, -(dpx * dgz));
       cM[2] = w * __builtin_fma(dpx, dgy, -(dpy * dgx));
     }
-    uint64_t pending = __ballot(valid);
+    uint64_t pending = (FSDF_ABLATE & 16) ? 0 : __ballot(valid);
     while (pending) {
       const int leader = __builtin_ctzll(pending);
       const int kk = __builtin_amdgcn_readfirstlane(__shfl(bk, leader, 64));
@@ -695,8 +771,8 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
         int r = 0;
         while (m.rbf_surface[r] != kk) ++r;
         const int r0 = m.rbf_row_off[r];
-        rbf_adjoint(px, py, pz, m.rbf_rows + 4 * r0, m.rbf_row_off[r + 1] - r0 - 1, stage[wave], sel,
-                    &rbf_acc[wave][m.rbf_acc_off[r]]);
+        rbf_adjoint(px, py, pz, m.rbf_rows + 4 * r0, m.rbf_row_off[r + 1] - r0 - 1, stage, stage_cap, sel,
+                    rbf_wave + m.rbf_acc_off[r]);
         continue;
       }
       double v[6];
@@ -711,7 +787,7 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
       }
     }
 
-    if (valid) {
+    if (valid && !(FSDF_ABLATE & 32)) {
       const int64_t o = out.perm ? out.perm[i] : i;
       if (out.kstar) out.kstar[o] = bk;
       if (out.d) out.d[o] = (double)best;
@@ -725,7 +801,7 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
 
   // ---- block combine (fixed order) ----
   cost_acc = wave_sum(cost_acc);
-  if (lane == 0) red[wave][SLOTS * 64 * 6] = cost_acc;
+  if (lane == 0) red[wave * kRedStride + SLOTS * 64 * 6] = cost_acc;
   __syncthreads();
   const int len6 = 1 + 6 * m.S;
   const int len = len6 + (RBF ? m.rbf_acc_off[m.R] : 0);
@@ -733,14 +809,14 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
     double s;
     if (t < len6) {
       const int src = (t == 0) ? SLOTS * 64 * 6 : t - 1;
-      s = red[0][src];
+      s = red[src];
 #pragma unroll
-      for (int w = 1; w < kBlock / 64; ++w) s += red[w][src];
+      for (int w = 1; w < kBlock / 64; ++w) s += red[w * kRedStride + src];
     } else {
       const int src = RBF ? t - len6 : 0;
-      s = rbf_acc[0][src];
+      s = rbf_acc[src];
 #pragma unroll
-      for (int w = 1; w < kBlock / 64; ++w) s += rbf_acc[w][src];
+      for (int w = 1; w < kBlock / 64; ++w) s += rbf_acc[w * kMaxRbfAcc + src];
     }
     out.partials[(int64_t)t * gridDim.x + blockIdx.x] = s;
   }
@@ -763,7 +839,9 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
 raycast_kernel(RayOrigin o, const double* __restrict__ rays, int64_t n, PassModel<T> m, double* __restrict__ depth) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  __shared__ __attribute__((aligned(32))) T stage[kBlock / 64][4 * kStageRows];
+  HullRow* ht = (HullRow*)fsdf_lds;  // dynamic LDS: hull table, then 4 wave stages
+  T* stage = (T*)((char*)(ht + m.K + 1) + wave * m.stage_bytes);
+  const float smax = load_hull_table(m, ht);
   const T EPS = (T)1e-5, SAFE_RATE = (T)0.4;
   const int SAFE_ITER_LIMIT = 60;
   const T ox = (T)o.x, oy = (T)o.y, oz = (T)o.z;
@@ -775,7 +853,7 @@ raycast_kernel(RayOrigin o, const double* __restrict__ rays, int64_t n, PassMode
     const T rx = (T)rays[3 * ii + 0], ry = (T)rays[3 * ii + 1], rz = (T)rays[3 * ii + 2];
     T dist = (T)0, est = (T)-1, last, gx, gy, gz;
     int bk, k = 0;
-    scene_eval<T, SLOTS, CULL, RBF>(ox + dist * rx, oy + dist * ry, oz + dist * rz, valid, m, stage[wave], nullptr,
+    scene_eval<T, SLOTS, CULL, RBF>(ox + dist * rx, oy + dist * ry, oz + dist * rz, valid, m, ht, smax, stage, nullptr,
                                     last, bk, gx, gy, gz);
     bool active = valid && fabs(last) > EPS;
     while (__any(active)) {
@@ -787,7 +865,7 @@ raycast_kernel(RayOrigin o, const double* __restrict__ rays, int64_t n, PassMode
         dist += step;
       }
       T v;
-      scene_eval<T, SLOTS, CULL, RBF>(ox + dist * rx, oy + dist * ry, oz + dist * rz, active, m, stage[wave],
+      scene_eval<T, SLOTS, CULL, RBF>(ox + dist * rx, oy + dist * ry, oz + dist * rz, active, m, ht, smax, stage,
                                       nullptr, v, bk, gx, gy, gz);
       if (active) {
         est = (v - last) / step;
@@ -837,22 +915,21 @@ hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_pose
   const int grid = (total + kBlock - 1) / kBlock;
   if (precision == 64) {
     hipLaunchKernelGGL(pose_kernel<double>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses,
-                       (double*)pm.planes_w, (double*)pm.facex_w, pm.spheres_w, (double*)pm.verts_w,
-                       (double*)pm.hscale_w);
+                       (double*)pm.planes_w, pm.spheres_w, (double*)pm.verts_w, (double*)pm.hscale_w);
   } else {
     hipLaunchKernelGGL(pose_kernel<float>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses, (float*)pm.planes_w,
-                       (float*)pm.facex_w, pm.spheres_w, (float*)pm.verts_w, (float*)pm.hscale_w);
+                       pm.spheres_w, (float*)pm.verts_w, (float*)pm.hscale_w);
   }
   return hipGetLastError();
 }
 
-template <typename T, bool CULL, bool RBF>
-static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void* d_pts, int64_t n, int nblocks,
-                          const PassOutputs& out, hipStream_t s) {
+template <typename T>
+static PassModel<T> pass_model(const LocalModel& lm, const PosedModel& pm) {
   PassModel<T> m;
   m.K = lm.K;
   m.S = lm.S;
   m.R = lm.R;
+  m.stage_bytes = lm.stage_bytes;
   m.hull_surface = lm.hull_surface;
   m.surface_kind = lm.surface_kind;
   m.rbf_surface = lm.rbf_surface;
@@ -861,19 +938,39 @@ static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void
   m.rbf_rows = (const T*)pm.rbf_rows;
   m.face_off = lm.face_off;
   m.vert_off = lm.vert_off;
-  m.nbr = lm.face_nbr;
+  m.face_rows = (const I4*)lm.face_rows;
   m.planes = (const T*)pm.planes_w;
-  m.facex = (const T*)pm.facex_w;
   m.verts = (const T*)pm.verts_w;
   m.hscale = (const T*)pm.hscale_w;
   m.spheres = pm.spheres_w;
+  return m;
+}
+
+static int slots_for(int S) { return S <= 64 ? 1 : (S <= 128 ? 2 : 4); }
+
+size_t pass_lds_bytes(const LocalModel& lm, bool raycast) {
+  const size_t stage = (size_t)(kBlock / 64) * (size_t)lm.stage_bytes + (size_t)(lm.K + 1) * sizeof(HullRow);
+  if (raycast) return stage;
+  const size_t red = (size_t)(kBlock / 64) * (size_t)(slots_for(lm.S) * 64 * 6 + 2) * sizeof(double);
+  const size_t rbf = lm.R > 0 ? (size_t)(kBlock / 64) * kMaxRbfAcc * sizeof(double) : 0;
+  return red + rbf + stage;
+}
+
+template <typename K, typename... Args>
+static void launch_lds(K kernel, int grid, size_t lds, hipStream_t s, Args... args) {
+  if (lds > 65536) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), lds, s, args...);
+}
+
+template <typename T, bool CULL, bool RBF>
+static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void* d_pts, int64_t n, int nblocks,
+                          const PassOutputs& out, hipStream_t s) {
+  const PassModel<T> m = pass_model<T>(lm, pm);
   const T* pts = (const T*)d_pts;
-  if (lm.S <= 64)
-    hipLaunchKernelGGL((pass_kernel<T, 1, CULL, RBF>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, m, out);
-  else if (lm.S <= 128)
-    hipLaunchKernelGGL((pass_kernel<T, 2, CULL, RBF>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, m, out);
-  else
-    hipLaunchKernelGGL((pass_kernel<T, 4, CULL, RBF>), dim3(nblocks), dim3(kBlock), 0, s, pts, n, m, out);
+  const size_t lds = pass_lds_bytes(lm, false);
+  if (lm.S <= 64) launch_lds(pass_kernel<T, 1, CULL, RBF>, nblocks, lds, s, pts, n, m, out);
+  else if (lm.S <= 128) launch_lds(pass_kernel<T, 2, CULL, RBF>, nblocks, lds, s, pts, n, m, out);
+  else launch_lds(pass_kernel<T, 4, CULL, RBF>, nblocks, lds, s, pts, n, m, out);
 }
 
 template <typename T>
@@ -898,32 +995,13 @@ hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const Pos
 template <typename T, bool CULL, bool RBF>
 static void launch_raycast_t(const LocalModel& lm, const PosedModel& pm, const double* origin, const double* rays,
                              int64_t n, double* depth, hipStream_t s) {
-  PassModel<T> m;
-  m.K = lm.K;
-  m.S = lm.S;
-  m.R = lm.R;
-  m.hull_surface = lm.hull_surface;
-  m.surface_kind = lm.surface_kind;
-  m.rbf_surface = lm.rbf_surface;
-  m.rbf_row_off = lm.rbf_row_off;
-  m.rbf_acc_off = lm.rbf_acc_off;
-  m.rbf_rows = (const T*)pm.rbf_rows;
-  m.face_off = lm.face_off;
-  m.vert_off = lm.vert_off;
-  m.nbr = lm.face_nbr;
-  m.planes = (const T*)pm.planes_w;
-  m.facex = (const T*)pm.facex_w;
-  m.verts = (const T*)pm.verts_w;
-  m.hscale = (const T*)pm.hscale_w;
-  m.spheres = pm.spheres_w;
+  const PassModel<T> m = pass_model<T>(lm, pm);
   const RayOrigin o{origin[0], origin[1], origin[2]};
   const int nb = pass_blocks(n);
-  if (lm.S <= 64)
-    hipLaunchKernelGGL((raycast_kernel<T, 1, CULL, RBF>), dim3(nb), dim3(kBlock), 0, s, o, rays, n, m, depth);
-  else if (lm.S <= 128)
-    hipLaunchKernelGGL((raycast_kernel<T, 2, CULL, RBF>), dim3(nb), dim3(kBlock), 0, s, o, rays, n, m, depth);
-  else
-    hipLaunchKernelGGL((raycast_kernel<T, 4, CULL, RBF>), dim3(nb), dim3(kBlock), 0, s, o, rays, n, m, depth);
+  const size_t lds = pass_lds_bytes(lm, true);
+  if (lm.S <= 64) launch_lds(raycast_kernel<T, 1, CULL, RBF>, nb, lds, s, o, rays, n, m, depth);
+  else if (lm.S <= 128) launch_lds(raycast_kernel<T, 2, CULL, RBF>, nb, lds, s, o, rays, n, m, depth);
+  else launch_lds(raycast_kernel<T, 4, CULL, RBF>, nb, lds, s, o, rays, n, m, depth);
 }
 
 template <typename T>

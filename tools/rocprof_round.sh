@@ -17,4 +17,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/${TAG}_fetch -o run -- python3 $ARGS > $OUT/${TAG}_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/${TAG}_write -o run -- python3 $ARGS > $OUT/${TAG}_write.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES --output-format csv -d $OUT/${TAG}_sq -o run -- python3 $ARGS > $OUT/${TAG}_sq.log 2>&1 || echo "sq pass failed (counter set?)"
+timeout -k 10 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_FMA_F64 SQ_LDS_BANK_CONFLICT --output-format csv -d $OUT/${TAG}_sq2 -o run -- python3 $ARGS > $OUT/${TAG}_sq2.log 2>&1 || echo "sq2 pass failed"
 echo done

@@ -21,7 +21,7 @@ def main(src, tag, dst):
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, f"{tag}_trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     out = {}
-    for part in ("fetch", "write", "sq"):
+    for part in ("fetch", "write", "sq", "sq2"):
         path = os.path.join(src, f"{tag}_{part}", "run_counter_collection.csv")
         if not os.path.exists(path):
             continue

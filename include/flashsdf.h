@@ -179,11 +179,16 @@ int fsdf_profile_pass(fsdf_ctx* ctx, int32_t enable);
 int fsdf_pass_time(fsdf_ctx* ctx, double* total_ms_out, int64_t* launches_out);
 
 /* Kernel work counters (diagnostics). enable=1 zeroes and starts counting in
- * every following pass; enable=0 stops and writes the 8 counters:
+ * every following pass; enable=0 stops and writes the counters:
  *   [0] wave-iterations (64 points each)  [1] hull evaluations (per wave)
  *   [2] slow-path entries (per wave)      [3] lane-needs summed over evaluations
  *   [4] lanes on the slow path            [5] best-first seed evaluations
- *   [6] waves reaching stage B (neighbours) [7] lanes in the exhaustive scan */
+ *   [6] waves reaching stage B (neighbours) [7] lanes in the exhaustive scan
+ *   [8] faces of the evaluated hulls      [9] faces in the plane-max scan
+ *   [10..18] shader-clock cycles per phase (culling, hull staging, plane max,
+ *   fast path, closest-feature search, whole wave-iteration, segmented
+ *   reduction, per-point stores, scene evaluation) — only in diagnostic
+ *   builds (-DFSDF_PHASE_TIMING=1), zero otherwise. 19 counters. */
 int fsdf_kernel_stats(fsdf_ctx* ctx, int32_t enable, uint64_t* counters_out);
 
 #ifdef __cplusplus

@@ -346,8 +346,9 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
         face_rows.push_back((int32_t)((uint32_t)nb[1] | ((uint32_t)nb[2] << 16)));
         face_rows.push_back(0);
       }
-      // per-wave LDS stage: plane + vertex rows of 4 T, one 16-byte face row per face
-      stage_bytes = std::max(stage_bytes, (h.n_faces + h.n_vertices) * 4 * tsz_ + 16 * h.n_faces);
+      // per-wave LDS stage: plane rows (padded to a multiple of 8 = the kernel's
+      // largest plane batch) + vertex rows of 4 T, one 16-byte face row per face
+      stage_bytes = std::max(stage_bytes, (((h.n_faces + 7) & ~7) + h.n_vertices) * 4 * tsz_ + 16 * h.n_faces);
     }
     face_off.push_back((int32_t)(face_hull.size()));
   }
@@ -731,18 +732,20 @@ extern "C" int fsdf_pass_time(fsdf_ctx* c, double* total_ms, int64_t* launches) 
   return FSDF_OK;
 }
 
+static constexpr int kStatCount = 19;
+
 extern "C" int fsdf_kernel_stats(fsdf_ctx* c, int32_t enable, uint64_t* counters) {
   if (!c) return FSDF_ERR_ARG;
   HIPCHECK(c, hipSetDevice(c->device));
-  if (!c->d_stats) HIPCHECK(c, hipMalloc(&c->d_stats, 8 * sizeof(unsigned long long)));
+  if (!c->d_stats) HIPCHECK(c, hipMalloc(&c->d_stats, kStatCount * sizeof(unsigned long long)));
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   if (enable) {
-    HIPCHECK(c, hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long)));
+    HIPCHECK(c, hipMemset(c->d_stats, 0, kStatCount * sizeof(unsigned long long)));
     c->stats_on = true;
     return FSDF_OK;
   }
   c->stats_on = false;
-  if (counters) HIPCHECK(c, hipMemcpy(counters, c->d_stats, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (counters) HIPCHECK(c, hipMemcpy(counters, c->d_stats, kStatCount * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return FSDF_OK;
 }
 

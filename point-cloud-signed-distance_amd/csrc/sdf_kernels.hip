@@ -125,6 +125,7 @@ __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const doubl
 // Closest point on triangle (a, b, c) to p — Voronoi-region walk.
 // ---------------------------------------------------------------------------
 template <typename T> struct Row4 { typedef T __attribute__((ext_vector_type(4))) type; };
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 typedef int I4 __attribute__((ext_vector_type(4)));
 
 template <typename T>
@@ -221,6 +222,12 @@ struct HullRow {
 };
 static_assert(sizeof(HullRow) == 32, "HullRow is 32 bytes");
 
+// Bounding sphere of the wave's points (f32, wave-uniform): every valid lane's
+// point p satisfies |p - c| <= r up to f32 rounding (covered by the margins).
+struct WaveSphere {
+  float x, y, z, r;
+};
+
 // fill the table (whole workgroup; ends with a barrier) and return the
 // culling-margin scale smax = max_k |c_k|_1 + 2 r_k (wave-uniform)
 template <typename T>
@@ -244,7 +251,39 @@ __device__ __forceinline__ float load_hull_table(const PassModel<T>& m, HullRow*
   return smax;
 }
 
-constexpr int kMaxRbfAcc = kMaxRbfAccum;  // RBF adjoint doubles per wave (Σ 4n+4)
+constexpr int kMaxRbfAcc = kMaxRbfAccum;
+// Diagnostic phase timing (-DFSDF_PHASE_TIMING=1): lane 0 of each wave adds
+// shader-clock deltas to stats[10..18]: culling, hull staging, plane max, fast
+// path, closest-feature search, whole wave-iteration, segmented reduction,
+// per-point stores, scene evaluation.
+#ifndef FSDF_PHASE_TIMING
+#define FSDF_PHASE_TIMING 0
+#endif
+// (the clock read drains every outstanding memory operation and pins the
+// schedule, so a phase is charged for its own loads)
+__device__ __forceinline__ uint64_t phase_clock() {
+  if (!FSDF_PHASE_TIMING) return 0;
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0);
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#if FSDF_PHASE_TIMING
+__shared__ unsigned long long fsdf_phase_acc[kBlock / 64][10];  // per wave, flushed at kernel end
+#endif
+__device__ __forceinline__ void phase_add(unsigned long long* stats, int slot, uint64_t t0) {
+#if FSDF_PHASE_TIMING
+  const uint64_t t1 = phase_clock();
+  if (stats && (threadIdx.x & 63) == 0) fsdf_phase_acc[threadIdx.x >> 6][slot - 10] += t1 - t0;
+#endif
+}
+// the event counters (stats[0..9]) are off in phase-timing builds: their
+// contended atomics would dominate the timed windows
+__device__ __forceinline__ bool count_events(const unsigned long long* stats) {
+  return !FSDF_PHASE_TIMING && stats != nullptr;
+}  // RBF adjoint doubles per wave (Σ 4n+4)
 // Diagnostic ablations (timing-only builds via -DFSDF_ABLATE=mask; results are
 // wrong): 4 no slow path, 16 no segmented reduction, 32 no per-point stores,
 // 64 no hull staging loads (LDS stage left as is).
@@ -272,17 +311,26 @@ __device__ __forceinline__ void stage_rows(T* __restrict__ lds, const T* __restr
 // the hull is loaded before any is stored, so the wave pays ONE global-memory
 // latency per hull evaluation; all later reads (broadcast plane reads, per-lane
 // triangle / neighbour / certificate reads) are LDS. Whole wave active.
+#ifndef FSDF_PLANE_BATCH
+#define FSDF_PLANE_BATCH 8
+#endif
+constexpr int kPlaneBatch = FSDF_PLANE_BATCH;  // plane rows per LDS batch (power of 2, >= 2)
+
 template <typename T>
 __device__ __forceinline__ void stage_hull(T* __restrict__ lw, const T* __restrict__ planes,
                                            const T* __restrict__ verts, const I4* __restrict__ frows, int nf,
                                            int nv) {
+  typedef typename Row4<T>::type R;
   constexpr int cpr = (int)sizeof(T) / 4;  // 16-byte chunks per row of 4 T
   const int P = nf * cpr, Q = P + nv * cpr, N = Q + nf;
+  const int padc = (((nf + kPlaneBatch - 1) & ~(kPlaneBatch - 1)) - nf) * cpr;  // rows padded to the batch
   const int lane = threadIdx.x & 63;
   const I4* sp = (const I4*)planes;
   const I4* sv = (const I4*)verts;
   I4* dst = (I4*)lw;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  // padding planes (0, 0, 0, +inf): h = -inf, never the maximum
+  if (lane < padc / cpr) ((R*)lw)[nf + lane] = R{(T)0, (T)0, (T)0, tinf<T>()};
   for (int c0 = 0; c0 < N; c0 += 8 * 64) {
     I4 v[8];
 #pragma unroll
@@ -295,7 +343,7 @@ __device__ __forceinline__ void stage_hull(T* __restrict__ lw, const T* __restri
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = c0 + 64 * j + lane;
-      if (c < N) dst[c] = v[j];
+      if (c < N) dst[c < P ? c : c + padc] = v[j];
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -362,34 +410,49 @@ __device__ __forceinline__ int fr_nbr(const I4& r, int e) {
 // ---------------------------------------------------------------------------
 template <typename T>
 __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassModel<T>& m,
-                                         const HullRow* __restrict__ ht, bool active, T bound, T& d, T& gx, T& gy,
-                                         T& gz, T* __restrict__ lw, unsigned long long* __restrict__ stats) {
+                                         const HullRow* __restrict__ ht, bool active, T bound,
+                                         T& d, T& gx, T& gy, T& gz, T* __restrict__ lw,
+                                         unsigned long long* __restrict__ stats) {
   typedef typename Row4<T>::type R;
   const int f0 = __builtin_amdgcn_readfirstlane(ht[k].f0);
   const int nf = __builtin_amdgcn_readfirstlane(ht[k + 1].f0) - f0;
   const int v0 = __builtin_amdgcn_readfirstlane(ht[k].v0);
   const int nv = __builtin_amdgcn_readfirstlane(ht[k + 1].v0) - v0;
+  uint64_t tp = phase_clock();
   stage_hull(lw, m.planes + 4 * f0, m.verts + 4 * v0, m.face_rows + f0, nf, nv);
+  phase_add(stats, 11, tp);
+  tp = phase_clock();
+  const int nfp = (nf + kPlaneBatch - 1) & ~(kPlaneBatch - 1);
   const R* lp = (const R*)lw;
-  const R* lv = lp + nf;
+  const R* lv = lp + nfp;
   const I4* lf = (const I4*)(lv + nv);
+  const T scale = (T)ht[k].hscale;
   // two independent running maxima (even / odd faces) shorten the serial
   // compare chain; merged with the first-index rule, identical to one chain
+  // Batches of kPlaneBatch padded rows: all the batch's LDS reads are issued
+  // before the first is consumed (one LDS latency per batch).
   T hA = -tinf<T>(), hB = -tinf<T>();
   int iA = 0, iB = 0;
-  int i = 0;
-#pragma unroll 4
-  for (; i + 1 < nf; i += 2) {
-    const T ha = plane_h<T>(lp[i], px, py, pz);
-    const T hb = plane_h<T>(lp[i + 1], px, py, pz);
-    if (ha > hA) { hA = ha; iA = i; }
-    if (hb > hB) { hB = hb; iB = i + 1; }
-  }
-  if (i < nf) {
-    const T ha = plane_h<T>(lp[i], px, py, pz);
-    if (ha > hA) { hA = ha; iA = i; }
+  for (int i = 0; i < nfp; i += kPlaneBatch) {
+    R c[kPlaneBatch];
+#pragma unroll
+    for (int q = 0; q < kPlaneBatch; ++q) c[q] = lp[i + q];
+#pragma unroll
+    for (int q = 0; q < kPlaneBatch; q += 2) {
+      const T ha = plane_h<T>(c[q], px, py, pz);
+      const T hb = plane_h<T>(c[q + 1], px, py, pz);
+      if (ha > hA) { hA = ha; iA = i + q; }
+      if (hb > hB) { hB = hb; iB = i + q + 1; }
+    }
   }
   if (hB > hA || (hB == hA && iB < iA)) { hA = hB; iA = iB; }
+  const unsigned kept = nf;
+  phase_add(stats, 12, tp);
+  tp = phase_clock();
+  if (count_events(stats) && lane_id() == 0) {
+    atomicAdd(stats + 8, (unsigned long long)nf);
+    atomicAdd(stats + 9, (unsigned long long)kept);
+  }
   const T hmax = hA;
   const int fs = iA;  // hull-local
   const R ns = lp[fs];
@@ -410,12 +473,13 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   // hmax is a lower bound of the distance: when it exceeds the lane's best so
   // far by more than the rounding of either value, hull k cannot win (nor tie)
   // and its exact distance is not needed — d stays hmax (> bound).
-  const T scale = (T)ht[k].hscale;
   const T lb_margin = (T)16 * cert_eps<T>() * (scale + ((fabs(px) + fabs(py)) + fabs(pz)));
   slow = slow && active && !(hmax - lb_margin > bound) && !(FSDF_ABLATE & 4);
   const uint64_t slow_mask = __ballot(slow);
+  phase_add(stats, 13, tp);
   if (!slow_mask) return;
-  if (stats && (threadIdx.x & 63) == 0) {
+  tp = phase_clock();
+  if (count_events(stats) && (threadIdx.x & 63) == 0) {
     atomicAdd(stats + 2, 1ull);
     atomicAdd(stats + 4, (unsigned long long)__builtin_popcountll(slow_mask));
   }
@@ -428,7 +492,7 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   bool todo = slow && !certified(px, py, pz, qx, qy, qz, lv, nv, scale);
   if (__any(todo)) {
     // stage B: the neighbours across the violated edges of f*
-    if (stats && (threadIdx.x & 63) == 0) atomicAdd(stats + 6, 1ull);
+    if (count_events(stats) && (threadIdx.x & 63) == 0) atomicAdd(stats + 6, 1ull);
     const T sv[3] = {s0, s1, s2};
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
@@ -447,7 +511,7 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
       // stage C: exhaustive scan of the visible faces (the closest boundary
       // point of a convex polytope lies on one of them); a face whose plane
       // distance already exceeds the best distance cannot improve it.
-      if (stats && (threadIdx.x & 63) == 0) atomicAdd(stats + 7, (unsigned long long)__builtin_popcountll(scan_mask));
+      if (count_events(stats) && (threadIdx.x & 63) == 0) atomicAdd(stats + 7, (unsigned long long)__builtin_popcountll(scan_mask));
       T b2 = tinf<T>();
       T bx = (T)0, by = (T)0, bz = (T)0;
       for (int ff = 0; ff < nf; ++ff) {
@@ -465,6 +529,7 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
       if (todo) { best2 = b2; qx = bx; qy = by; qz = bz; }
     }
   }
+  phase_add(stats, 14, tp);
   if (slow) {
     if (best2 > (T)0) {
       d = tsqrt(best2);
@@ -612,19 +677,80 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   float ub2 = __builtin_huge_valf(), pw_min = __builtin_huge_valf();
   int kseed = 0;
   float pxf = 0.f, pyf = 0.f, pzf = 0.f;
+  // candidate hulls of the wave (bit k&63 of cand[k>>6]); all hulls without culling
+  uint64_t cand[SLOTS];
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) {
+    const int left = K - 64 * s;
+    cand[s] = left >= 64 ? ~0ull : (left > 0 ? (1ull << left) - 1 : 0ull);
+  }
+  const uint64_t tc = phase_clock();
+  // the wave's bounding sphere (bbox centre, half diagonal) over the valid
+  // lanes (invalid lanes stand in for the first valid one)
+  pxf = (float)px; pyf = (float)py; pzf = (float)pz;
+  WaveSphere ws;
+  {
+    const uint64_t vm = __ballot(valid);
+    const int src = vm ? __builtin_ctzll(vm) : 0;
+    float qx = pxf, qy = pyf, qz = pzf;
+    if (!valid) { qx = __shfl(pxf, src, 64); qy = __shfl(pyf, src, 64); qz = __shfl(pzf, src, 64); }
+    float lx = qx, ly = qy, lz = qz, hx = qx, hy = qy, hz = qz;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      lx = fminf(lx, __shfl_xor(lx, off, 64)); hx = fmaxf(hx, __shfl_xor(hx, off, 64));
+      ly = fminf(ly, __shfl_xor(ly, off, 64)); hy = fmaxf(hy, __shfl_xor(hy, off, 64));
+      lz = fminf(lz, __shfl_xor(lz, off, 64)); hz = fmaxf(hz, __shfl_xor(hz, off, 64));
+    }
+    const float ex = hx - lx, ey = hy - ly, ez = hz - lz;
+    ws.x = 0.5f * (lx + hx); ws.y = 0.5f * (ly + hy); ws.z = 0.5f * (lz + hz);
+    ws.r = 0.5f * __builtin_sqrtf(__builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez)));
+  }
   if (CULL) {
-    pxf = (float)px; pyf = (float)py; pzf = (float)pz;
-#pragma unroll 4
-    for (int k = 0; k < K; ++k) {
-      const F4 sp = ht[k].sphere;
-      const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
-      const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
-      ub2 = fminf(ub2, dist2);
-      const float pwr = __builtin_fmaf(-sp[3], sp[3], dist2);
-      if (pwr < pw_min) { pw_min = pwr; kseed = k; }
+    // Wave-level culling, one hull per lane: with the wave's points inside the
+    // sphere (c_w, r_w) and D_k = |c_w - c_k|, every point of the wave has
+    // d_k >= D_k - r_w - r_k and d_k <= D_k + r_w, so a hull whose lower bound
+    // exceeds UB_w = min_k (D_k + r_w) by the fp32 margin is needed by no lane.
+    const float cwx = ws.x, cwy = ws.y, cwz = ws.z, rw = ws.r;
+    float Dk[SLOTS];
+    float ubw = __builtin_huge_valf();
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+      const int k = 64 * s + lane;
+      Dk[s] = __builtin_huge_valf();
+      if (k < K) {
+        const F4 sp = ht[k].sphere;
+        const float dx = cwx - sp[0], dy = cwy - sp[1], dz = cwz - sp[2];
+        Dk[s] = __builtin_sqrtf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)));
+        ubw = fminf(ubw, Dk[s] + rw);
+      }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) ubw = fminf(ubw, __shfl_xor(ubw, off, 64));
+    const float mrgw = 1e-5f * (1.0f + fabsf(cwx) + fabsf(cwy) + fabsf(cwz) + smax + 4.0f * rw + 2.0f * ubw);
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+      const int k = 64 * s + lane;
+      const bool c = k < K && Dk[s] - rw - ht[k < K ? k : 0].sphere[3] <= ubw + mrgw;
+      cand[s] = __ballot(c);
+    }
+    // per lane over the candidates: ub = min_k |p-c_k| and the best-first seed
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+      uint64_t cm = cand[s];
+      while (cm) {
+        const int k = 64 * s + __builtin_ctzll(cm);
+        cm &= cm - 1;
+        const F4 sp = ht[k].sphere;
+        const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
+        const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
+        ub2 = fminf(ub2, dist2);
+        const float pwr = __builtin_fmaf(-sp[3], sp[3], dist2);
+        if (pwr < pw_min) { pw_min = pwr; kseed = k; }
+      }
     }
   }
   const float ub = __builtin_sqrtf(ub2);
+  phase_add(stats, 10, tc);
   // one rounding margin per lane, >= 1e-5 x every magnitude in the test below
   const float mrg = 1e-5f * (1.0f + fabsf(pxf) + fabsf(pyf) + fabsf(pzf) + smax + 2.0f * ub);
 
@@ -660,7 +786,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   auto evaluate = [&](int k, bool need) {
     T dk, hx, hy, hz;
     hull_sdf<T>(px, py, pz, k, m, ht, need, best, dk, hx, hy, hz, lw, stats);
-    if (stats) {
+    if (count_events(stats)) {
       const uint64_t nm = __ballot(need);
       if (lane == 0) {
         atomicAdd(stats + 1, 1ull);
@@ -684,21 +810,22 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s)
         if ((kk >> 6) == s) done[s] |= 1ull << (kk & 63);
-      if (stats && lane == 0) atomicAdd(stats + 5, 1ull);
+      if (count_events(stats) && lane == 0) atomicAdd(stats + 5, 1ull);
     }
   }
-  // Phase C: sweep the remaining hulls in index order.
-  for (int k = 0; k < K; ++k) {
-    bool skip = false;
+  // Phase C: sweep the remaining candidates in index order.
 #pragma unroll
-    for (int s = 0; s < SLOTS; ++s)
-      if ((k >> 6) == s) skip = (done[s] >> (k & 63)) & 1ull;
-    if (skip) continue;
-    const bool need = needs(k);
-    if (!__any(need)) continue;
-    evaluate(k, need);
+  for (int s = 0; s < SLOTS; ++s) {
+    uint64_t cm = cand[s] & ~done[s];
+    while (cm) {
+      const int k = 64 * s + __builtin_ctzll(cm);
+      cm &= cm - 1;
+      const bool need = needs(k);
+      if (!__any(need)) continue;
+      evaluate(k, need);
+    }
   }
-  if (stats && lane == 0) atomicAdd(stats + 0, 1ull);
+  if (count_events(stats) && lane == 0) atomicAdd(stats + 0, 1ull);
 }
 
 // ---------------------------------------------------------------------------
@@ -734,13 +861,16 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
   if (RBF)
     for (int e = lane; e < m.rbf_acc_off[m.R]; e += 64) rbf_wave[e] = 0.0;
   const float smax = load_hull_table(m, ht);
-
+#if FSDF_PHASE_TIMING
+  if (lane < 10) fsdf_phase_acc[wave][lane] = 0;
+#endif
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t base = (int64_t)blockIdx.x * kBlock + wave * 64; base < n; base += stride) {
     const int64_t i = base + lane;
     const bool valid = i < n;
     const int64_t ii = valid ? i : n - 1;
     const T px = pts[3 * ii + 0], py = pts[3 * ii + 1], pz = pts[3 * ii + 2];
+    const uint64_t t_iter = phase_clock();
 
     T best, gx, gy, gz;
     int bk;
@@ -760,6 +890,8 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
       cM[1] = w * __builtin_fma(dpz, dgx, -(dpx * dgz));
       cM[2] = w * __builtin_fma(dpx, dgy, -(dpy * dgx));
     }
+    phase_add(out.stats, 18, t_iter);
+    const uint64_t t_red = phase_clock();
     uint64_t pending = (FSDF_ABLATE & 16) ? 0 : __ballot(valid);
     while (pending) {
       const int leader = __builtin_ctzll(pending);
@@ -787,6 +919,8 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
       }
     }
 
+    phase_add(out.stats, 16, t_red);
+    const uint64_t t_st = phase_clock();
     if (valid && !(FSDF_ABLATE & 32)) {
       const int64_t o = out.perm ? out.perm[i] : i;
       if (out.kstar) out.kstar[o] = bk;
@@ -797,8 +931,13 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
         out.grad[3 * o + 2] = (double)gz;
       }
     }
+    phase_add(out.stats, 17, t_st);
+    phase_add(out.stats, 15, t_iter);
   }
 
+#if FSDF_PHASE_TIMING
+  if (out.stats && lane < 9) atomicAdd(out.stats + 10 + lane, fsdf_phase_acc[wave][lane]);
+#endif
   // ---- block combine (fixed order) ----
   cost_acc = wave_sum(cost_acc);
   if (lane == 0) red[wave * kRedStride + SLOTS * 64 * 6] = cost_acc;

@@ -254,10 +254,11 @@ class Context:
         return ms.value, n.value
 
     STAT_NAMES = ("wave_iters", "hull_evals", "slow_waves", "lane_needs", "slow_lanes", "seed_evals",
-                  "stageB_waves", "full_scan_lanes")
+                  "stageB_waves", "full_scan_lanes", "faces_total", "faces_kept", "cyc_cull", "cyc_stage",
+                  "cyc_plane", "cyc_fast", "cyc_slow", "cyc_iter", "cyc_reduce", "cyc_store", "cyc_scene")
 
     def kernel_stats(self, enable: bool):
         """enable=True: start counting; enable=False: stop, return the counters."""
-        out = np.zeros(8, np.uint64)
+        out = np.zeros(len(self.STAT_NAMES), np.uint64)
         check(self._lib.fsdf_kernel_stats(self._ctx, int(enable), ptr(out)), self._ctx, "kernel_stats")
-        return None if enable else dict(zip(self.STAT_NAMES, (int(v) for v in out[:8])))
+        return None if enable else dict(zip(self.STAT_NAMES, (int(v) for v in out)))

@@ -62,7 +62,7 @@ def main():
         c.kernel_stats(True)
         c.eval(poses)
         st = c.kernel_stats(False)
-        w = st["wave_iters"]
+        w = st["wave_iters"] or -(-args.points // 64)  # phase-timing builds do not count events
         ms = float(np.median(times[v]))
         row = {"order": v[0], "cull": v[1], "precision": v[2], "sort_points": v[3], "set_points_ms": setup_ms[v],
                "pass_ms_median": ms,
@@ -70,7 +70,11 @@ def main():
                "hull_evals_per_wave": st["hull_evals"] / w, "seed_evals_per_wave": st["seed_evals"] / w,
                "slow_per_wave": st["slow_waves"] / w, "lane_need_frac": st["lane_needs"] / max(st["hull_evals"] * 64, 1),
                "slow_lane_frac": st["slow_lanes"] / max(st["slow_waves"] * 64, 1),
-               "full_scan_lane_frac_of_slow": st["full_scan_lanes"] / max(st["slow_lanes"], 1), **st}
+               "full_scan_lane_frac_of_slow": st["full_scan_lanes"] / max(st["slow_lanes"], 1),
+               "face_keep_frac": st["faces_kept"] / max(st["faces_total"], 1), **st}
+        if st.get("cyc_iter"):
+            row["cycle_frac"] = {k[4:]: round(st[k] / st["cyc_iter"], 4) for k in st if k.startswith("cyc_")}
+            row["cycles_per_wave_iter"] = st["cyc_iter"] / w
         res.append(row)
         print(json.dumps(row), flush=True)
     if args.json:

@@ -47,3 +47,28 @@ def read_point_cloud(file) -> PointCloud:
 def subsample(points: np.ndarray, step: int = 200) -> np.ndarray:
     """msg[:points][1:200:end] (examples/irb_and_squishable.ipynb cell 12)."""
     return np.ascontiguousarray(np.asarray(points)[::step])
+
+
+def kinect_to_pointcloud(x, y, z, num: int | None = None, utime: int = 0) -> dict:
+    """The message conversion of convert_kinect_log_data.py:11-31 on arrays.
+
+    A kinect.pointcloud_t (KINECT_POINTS_REDUCED) interleaves positions and
+    colours in its x/y/z arrays: even indices are xyz, odd indices rgb. The
+    bot_core.pointcloud_t it becomes holds n_points = num // 2 points
+    (x[i], y[i], z[i]) for even i, and n_channels = 3 channels "r", "g", "b"
+    whose values are x[i], y[i], z[i] for odd i. Returns that message as a dict
+    (utime, n_points, points [n,3] f32, n_channels, channel_names, channels
+    [3,n] f32). LCM wire encoding is out of scope: the lcmtypes are not part of
+    the reference."""
+    x, y, z = (np.asarray(v, np.float32) for v in (x, y, z))
+    num = len(x) if num is None else int(num)
+    pts = np.stack([x[0:num:2], y[0:num:2], z[0:num:2]], axis=1)
+    chans = np.stack([v[1:num:2] for v in (x, y, z)])
+    return {"utime": int(utime), "n_points": num // 2, "points": np.ascontiguousarray(pts), "n_channels": 3,
+            "channel_names": ["r", "g", "b"], "channels": np.ascontiguousarray(chans)}
+
+
+def pointcloud_positions(msg: dict, step: int = 200) -> np.ndarray:
+    """[n,3] float64 positions of a bot_core.pointcloud_t dict, subsampled as
+    msg[:points][1:200:end] (examples/irb_and_squishable.ipynb cell 12)."""
+    return subsample(np.asarray(msg["points"], np.float64), step)

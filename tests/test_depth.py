@@ -64,3 +64,20 @@ def test_read_reference_clouds():
     assert len(read_point_cloud(os.path.join(base, "squishable_squished_xyzrgb.txt"))) == 25164
     with pytest.raises(ValueError):  # xyz-only: the reference indexes columns 4-6 and fails too
         read_point_cloud(os.path.join(base, "box_on_table_points.txt"))
+
+
+def test_kinect_to_pointcloud_interleave():
+    """convert_kinect_log_data.py:16-24: even samples are xyz, odd samples rgb,
+    n_points = num // 2; then the notebook's [1:200:end] subsampling."""
+    from flash.depthdata import kinect_to_pointcloud, pointcloud_positions
+    rng = np.random.default_rng(3)
+    num = 1001  # odd: the reference writes ceil(num/2) points but n_points = num // 2 (kept as is)
+    x, y, z = rng.random((3, num)).astype(np.float32)
+    msg = kinect_to_pointcloud(x, y, z, num, utime=42)
+    assert msg["utime"] == 42 and msg["n_channels"] == 3 and msg["channel_names"] == ["r", "g", "b"]
+    assert msg["n_points"] == num // 2 and len(msg["points"]) == (num + 1) // 2
+    assert np.array_equal(msg["points"][3], [x[6], y[6], z[6]])
+    assert np.array_equal(msg["channels"][:, 3], [x[7], y[7], z[7]])
+    assert msg["channels"].shape == (3, num // 2)
+    pos = pointcloud_positions(msg)
+    assert pos.dtype == np.float64 and np.array_equal(pos[1], msg["points"][200].astype(np.float64))

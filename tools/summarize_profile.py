@@ -8,6 +8,8 @@ by 1/2 — reported both raw and doubled; WRITE_SIZE exact for wide stores).
 FETCH_SIZE / WRITE_SIZE are in KiB (rocprofv3 derived counters).
 
     python tools/summarize_profile.py gpurun_out/prof r01b profiles/r01
+
+also writes profiles/latest_pmc.json, which bench.py reads for roofline.traffic.
 """
 import collections
 import csv
@@ -45,7 +47,15 @@ def main(src, tag, dst):
                 "note": "traffic = 2*FETCH_SIZE + WRITE_SIZE (KiB->B); FETCH counts Infinity-Cache hits too"}
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
-    print(json.dumps(out.get("pass_kernel_hbm_bytes_per_launch"), indent=1))
+    hb = out.get("pass_kernel_hbm_bytes_per_launch")
+    if hb:
+        # the record bench.py reads for roofline.traffic (same workload: bench.py defaults)
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        rel = os.path.relpath(os.path.join(dst, "pmc_summary.json"), root)
+        with open(os.path.join(root, "profiles", "latest_pmc.json"), "w") as f:
+            json.dump({"workload": "bench.py default", "kernel": pk[0],
+                       "traffic_bytes_per_launch": hb["traffic_bytes"], "source": rel}, f, indent=1)
+    print(json.dumps(hb, indent=1))
 
 
 if __name__ == "__main__":

@@ -323,14 +323,11 @@ __device__ __forceinline__ void stage_hull(T* __restrict__ lw, const T* __restri
   typedef typename Row4<T>::type R;
   constexpr int cpr = (int)sizeof(T) / 4;  // 16-byte chunks per row of 4 T
   const int P = nf * cpr, Q = P + nv * cpr, N = Q + nf;
-  const int padc = (((nf + kPlaneBatch - 1) & ~(kPlaneBatch - 1)) - nf) * cpr;  // rows padded to the batch
   const int lane = threadIdx.x & 63;
   const I4* sp = (const I4*)planes;
   const I4* sv = (const I4*)verts;
   I4* dst = (I4*)lw;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  // padding planes (0, 0, 0, +inf): h = -inf, never the maximum
-  if (lane < padc / cpr) ((R*)lw)[nf + lane] = R{(T)0, (T)0, (T)0, tinf<T>()};
   for (int c0 = 0; c0 < N; c0 += 8 * 64) {
     I4 v[8];
 #pragma unroll
@@ -343,7 +340,7 @@ __device__ __forceinline__ void stage_hull(T* __restrict__ lw, const T* __restri
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = c0 + 64 * j + lane;
-      if (c < N) dst[c < P ? c : c + padc] = v[j];
+      if (c < N) dst[c] = v[j];
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -361,6 +358,8 @@ template <> __device__ __forceinline__ float cert_eps() { return 4e-6f; }
 // Optimality certificate of a candidate closest point q of the staged hull
 // (the GJK termination test): q is the closest point of conv(V) to p iff
 // max_v (p-q)·v <= (p-q)·q; accepted within a rounding tolerance.
+// Two chains over the staged vertex rows; an odd count repeats the last
+// vertex, which leaves the maximum unchanged.
 template <typename T>
 __device__ __forceinline__ bool certified(T px, T py, T pz, T qx, T qy, T qz, const typename Row4<T>::type* lv,
                                           int nv, T scale) {
@@ -368,19 +367,13 @@ __device__ __forceinline__ bool certified(T px, T py, T pz, T qx, T qy, T qz, co
   const T wx = px - qx, wy = py - qy, wz = pz - qz;
   const T wq = mfma_(wx, qx, mfma_(wy, qy, wz * qz));
   T sA = -tinf<T>(), sB = -tinf<T>();
-  int v = 0;
 #pragma unroll 4
-  for (; v + 1 < nv; v += 2) {
-    const R a = lv[v], b = lv[v + 1];
+  for (int v = 0; v < nv; v += 2) {
+    const R a = lv[v], b = lv[min(v + 1, nv - 1)];
     const T sa = mfma_(a[0], wx, mfma_(a[1], wy, a[2] * wz));
     const T sb = mfma_(b[0], wx, mfma_(b[1], wy, b[2] * wz));
     sA = sa > sA ? sa : sA;
     sB = sb > sB ? sb : sB;
-  }
-  if (v < nv) {
-    const R a = lv[v];
-    const T sa = mfma_(a[0], wx, mfma_(a[1], wy, a[2] * wz));
-    sA = sa > sA ? sa : sA;
   }
   const T smax = sB > sA ? sB : sA;
   const T tol = cert_eps<T>() * ((fabs(wx) + fabs(wy)) + fabs(wz)) * scale;
@@ -422,21 +415,23 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   stage_hull(lw, m.planes + 4 * f0, m.verts + 4 * v0, m.face_rows + f0, nf, nv);
   phase_add(stats, 11, tp);
   tp = phase_clock();
-  const int nfp = (nf + kPlaneBatch - 1) & ~(kPlaneBatch - 1);
   const R* lp = (const R*)lw;
-  const R* lv = lp + nfp;
+  const R* lv = lp + nf;
   const I4* lf = (const I4*)(lv + nv);
   const T scale = (T)ht[k].hscale;
   // two independent running maxima (even / odd faces) shorten the serial
   // compare chain; merged with the first-index rule, identical to one chain
-  // Batches of kPlaneBatch padded rows: all the batch's LDS reads are issued
-  // before the first is consumed (one LDS latency per batch).
+  // Batches of kPlaneBatch rows: all the batch's LDS reads are issued before
+  // the first is consumed (one LDS latency per batch). The last batch reads
+  // the last row again in place of missing ones: a repeat has the last face's
+  // value under a larger index, so it never displaces it (strict >, and the
+  // chain merge keeps the smaller index on ties).
   T hA = -tinf<T>(), hB = -tinf<T>();
   int iA = 0, iB = 0;
-  for (int i = 0; i < nfp; i += kPlaneBatch) {
+  for (int i = 0; i < nf; i += kPlaneBatch) {
     R c[kPlaneBatch];
 #pragma unroll
-    for (int q = 0; q < kPlaneBatch; ++q) c[q] = lp[i + q];
+    for (int q = 0; q < kPlaneBatch; ++q) c[q] = lp[min(i + q, nf - 1)];
 #pragma unroll
     for (int q = 0; q < kPlaneBatch; q += 2) {
       const T ha = plane_h<T>(c[q], px, py, pz);
@@ -601,10 +596,33 @@ __device__ __forceinline__ void rbf_skin_from_field(const RbfField<T>& F, T& s, 
   gz = mfma_(-c, hgz, F.gz * invG);
 }
 
+// Wave-wide f64 sum in the VALU (DPP, no LDS round trips): inclusive scan
+// within each 16-lane row (row_shr 1, 2, 4, 8), then row_bcast 15 / 31 carry
+// the row totals; lane 63 holds the sum, returned to every lane. Fixed order
+// (deterministic). Whole wave active.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_shifted(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROW_MASK, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+#ifndef FSDF_DPP_SUM
+#define FSDF_DPP_SUM 1
+#endif
 __device__ __forceinline__ double wave_sum(double v) {
+  if (!FSDF_DPP_SUM) {
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+  }
+  v += dpp_shifted<0x111, 0xf>(v);  // row_shr:1
+  v += dpp_shifted<0x112, 0xf>(v);  // row_shr:2
+  v += dpp_shifted<0x114, 0xf>(v);  // row_shr:4
+  v += dpp_shifted<0x118, 0xf>(v);  // row_shr:8
+  v += dpp_shifted<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_shifted<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63),
+                          __builtin_amdgcn_readlane(__double2loint(v), 63));
 }
 
 // Adjoint contributions of the lanes whose nearest surface is RBF skin r

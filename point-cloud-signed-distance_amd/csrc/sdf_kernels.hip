@@ -358,8 +358,8 @@ template <> __device__ __forceinline__ float cert_eps() { return 4e-6f; }
 // Optimality certificate of a candidate closest point q of the staged hull
 // (the GJK termination test): q is the closest point of conv(V) to p iff
 // max_v (p-q)·v <= (p-q)·q; accepted within a rounding tolerance.
-// Two chains over the staged vertex rows; an odd count repeats the last
-// vertex, which leaves the maximum unchanged.
+// Two v_max chains over the staged vertex rows (the maximum is exact in any
+// order); an odd count repeats the last vertex, which leaves it unchanged.
 template <typename T>
 __device__ __forceinline__ bool certified(T px, T py, T pz, T qx, T qy, T qz, const typename Row4<T>::type* lv,
                                           int nv, T scale) {
@@ -370,12 +370,10 @@ __device__ __forceinline__ bool certified(T px, T py, T pz, T qx, T qy, T qz, co
 #pragma unroll 4
   for (int v = 0; v < nv; v += 2) {
     const R a = lv[v], b = lv[min(v + 1, nv - 1)];
-    const T sa = mfma_(a[0], wx, mfma_(a[1], wy, a[2] * wz));
-    const T sb = mfma_(b[0], wx, mfma_(b[1], wy, b[2] * wz));
-    sA = sa > sA ? sa : sA;
-    sB = sb > sB ? sb : sB;
+    sA = __builtin_fmax(sA, mfma_(a[0], wx, mfma_(a[1], wy, a[2] * wz)));
+    sB = __builtin_fmax(sB, mfma_(b[0], wx, mfma_(b[1], wy, b[2] * wz)));
   }
-  const T smax = sB > sA ? sB : sA;
+  const T smax = __builtin_fmax(sA, sB);
   const T tol = cert_eps<T>() * ((fabs(wx) + fabs(wy)) + fabs(wz)) * scale;
   return smax <= wq + tol;
 }
@@ -421,26 +419,38 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   const T scale = (T)ht[k].hscale;
   // two independent running maxima (even / odd faces) shorten the serial
   // compare chain; merged with the first-index rule, identical to one chain
-  // Batches of kPlaneBatch rows: all the batch's LDS reads are issued before
-  // the first is consumed (one LDS latency per batch). The last batch reads
-  // the last row again in place of missing ones: a repeat has the last face's
-  // value under a larger index, so it never displaces it (strict >, and the
-  // chain merge keeps the smaller index on ties).
-  T hA = -tinf<T>(), hB = -tinf<T>();
-  int iA = 0, iB = 0;
-  for (int i = 0; i < nf; i += kPlaneBatch) {
+  // Batches of kPlaneBatch rows, all of a batch's LDS reads issued before the
+  // first is consumed. The loop keeps only the exact maximum (a v_max tree per
+  // batch) and the first batch that strictly raised it; the first face of that
+  // batch equal to the maximum is then found by re-evaluating the batch (same
+  // operations, same bits) — the first-index argmax over all faces. Missing
+  // rows of the last batch repeat the last face (same value, never first).
+  T hA = -tinf<T>();
+  int ib = 0;
+  auto batch = [&](int i, bool tail) {
     R c[kPlaneBatch];
 #pragma unroll
-    for (int q = 0; q < kPlaneBatch; ++q) c[q] = lp[min(i + q, nf - 1)];
+    for (int q = 0; q < kPlaneBatch; ++q) c[q] = lp[tail ? min(i + q, nf - 1) : i + q];
+    T h[kPlaneBatch];
 #pragma unroll
-    for (int q = 0; q < kPlaneBatch; q += 2) {
-      const T ha = plane_h<T>(c[q], px, py, pz);
-      const T hb = plane_h<T>(c[q + 1], px, py, pz);
-      if (ha > hA) { hA = ha; iA = i + q; }
-      if (hb > hB) { hB = hb; iB = i + q + 1; }
-    }
+    for (int q = 0; q < kPlaneBatch; ++q) h[q] = plane_h<T>(c[q], px, py, pz);
+#pragma unroll
+    for (int w = 1; w < kPlaneBatch; w *= 2)
+#pragma unroll
+      for (int q = 0; q + w < kPlaneBatch; q += 2 * w) h[q] = __builtin_fmax(h[q], h[q + w]);
+    if (h[0] > hA) { hA = h[0]; ib = i; }
+  };
+  int i0 = 0;
+  for (; i0 + kPlaneBatch <= nf; i0 += kPlaneBatch) batch(i0, false);  // one base address, immediate offsets
+  if (i0 < nf) batch(i0, true);
+  // faces before batch ib are all < hA, so the window may start earlier
+  const int fb = nf >= kPlaneBatch ? min(ib, nf - kPlaneBatch) : ib;
+  int iA = min(fb + kPlaneBatch - 1, nf - 1);
+#pragma unroll
+  for (int q = kPlaneBatch - 1; q >= 0; --q) {
+    const int f = nf >= kPlaneBatch ? fb + q : min(fb + q, nf - 1);
+    if (plane_h<T>(lp[f], px, py, pz) == hA) iA = f;
   }
-  if (hB > hA || (hB == hA && iB < iA)) { hA = hB; iA = iB; }
   const unsigned kept = nf;
   phase_add(stats, 12, tp);
   tp = phase_clock();

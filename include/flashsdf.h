@@ -184,7 +184,7 @@ int fsdf_pass_time(fsdf_ctx* ctx, double* total_ms_out, int64_t* launches_out);
  *   [2] slow-path entries (per wave)      [3] lane-needs summed over evaluations
  *   [4] lanes on the slow path            [5] best-first seed evaluations
  *   [6] waves reaching stage B (neighbours) [7] lanes in the exhaustive scan
- *   [8] faces of the evaluated hulls      [9] faces in the plane-max scan
+ *   [8] candidate hulls after wave culling [9] faces of the evaluated hulls
  *   [10..18] shader-clock cycles per phase (culling, hull staging, plane max,
  *   fast path, closest-feature search, whole wave-iteration, segmented
  *   reduction, per-point stores, scene evaluation) — only in diagnostic

@@ -451,12 +451,10 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
     const int f = nf >= kPlaneBatch ? fb + q : min(fb + q, nf - 1);
     if (plane_h<T>(lp[f], px, py, pz) == hA) iA = f;
   }
-  const unsigned kept = nf;
   phase_add(stats, 12, tp);
   tp = phase_clock();
   if (count_events(stats) && lane_id() == 0) {
-    atomicAdd(stats + 8, (unsigned long long)nf);
-    atomicAdd(stats + 9, (unsigned long long)kept);
+    atomicAdd(stats + 9, (unsigned long long)nf);
   }
   const T hmax = hA;
   const int fs = iA;  // hull-local
@@ -619,6 +617,26 @@ __device__ __forceinline__ double dpp_shifted(double v) {
 #ifndef FSDF_DPP_SUM
 #define FSDF_DPP_SUM 1
 #endif
+// Wave-wide f32 min / max in the VALU (DPP scan, identity fill), result to
+// every lane. Whole wave active.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_shifted_f(float v, float identity) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(identity), __float_as_int(v), CTRL, ROW_MASK,
+                                                    0xf, false));
+}
+template <bool MAX>
+__device__ __forceinline__ float wave_minmax(float v) {
+  const float id = MAX ? -__builtin_huge_valf() : __builtin_huge_valf();
+  auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : fminf(a, b); };
+  v = op(v, dpp_shifted_f<0x111, 0xf>(v, id));
+  v = op(v, dpp_shifted_f<0x112, 0xf>(v, id));
+  v = op(v, dpp_shifted_f<0x114, 0xf>(v, id));
+  v = op(v, dpp_shifted_f<0x118, 0xf>(v, id));
+  v = op(v, dpp_shifted_f<0x142, 0xa>(v, id));
+  v = op(v, dpp_shifted_f<0x143, 0xc>(v, id));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
   if (!FSDF_DPP_SUM) {
 #pragma unroll
@@ -722,13 +740,8 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     const int src = vm ? __builtin_ctzll(vm) : 0;
     float qx = pxf, qy = pyf, qz = pzf;
     if (!valid) { qx = __shfl(pxf, src, 64); qy = __shfl(pyf, src, 64); qz = __shfl(pzf, src, 64); }
-    float lx = qx, ly = qy, lz = qz, hx = qx, hy = qy, hz = qz;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      lx = fminf(lx, __shfl_xor(lx, off, 64)); hx = fmaxf(hx, __shfl_xor(hx, off, 64));
-      ly = fminf(ly, __shfl_xor(ly, off, 64)); hy = fmaxf(hy, __shfl_xor(hy, off, 64));
-      lz = fminf(lz, __shfl_xor(lz, off, 64)); hz = fmaxf(hz, __shfl_xor(hz, off, 64));
-    }
+    const float lx = wave_minmax<false>(qx), ly = wave_minmax<false>(qy), lz = wave_minmax<false>(qz);
+    const float hx = wave_minmax<true>(qx), hy = wave_minmax<true>(qy), hz = wave_minmax<true>(qz);
     const float ex = hx - lx, ey = hy - ly, ez = hz - lz;
     ws.x = 0.5f * (lx + hx); ws.y = 0.5f * (ly + hy); ws.z = 0.5f * (lz + hz);
     ws.r = 0.5f * __builtin_sqrtf(__builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez)));
@@ -752,14 +765,19 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
         ubw = fminf(ubw, Dk[s] + rw);
       }
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) ubw = fminf(ubw, __shfl_xor(ubw, off, 64));
+    ubw = wave_minmax<false>(ubw);
     const float mrgw = 1e-5f * (1.0f + fabsf(cwx) + fabsf(cwy) + fabsf(cwz) + smax + 4.0f * rw + 2.0f * ubw);
 #pragma unroll
     for (int s = 0; s < SLOTS; ++s) {
       const int k = 64 * s + lane;
       const bool c = k < K && Dk[s] - rw - ht[k < K ? k : 0].sphere[3] <= ubw + mrgw;
       cand[s] = __ballot(c);
+    }
+    if (count_events(stats) && lane == 0) {
+      unsigned long long nc = 0;
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) nc += __builtin_popcountll(cand[s]);
+      atomicAdd(stats + 8, nc);
     }
     // per lane over the candidates: ub = min_k |p-c_k| and the best-first seed
 #pragma unroll

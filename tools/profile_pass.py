@@ -71,7 +71,7 @@ def main():
                "slow_per_wave": st["slow_waves"] / w, "lane_need_frac": st["lane_needs"] / max(st["hull_evals"] * 64, 1),
                "slow_lane_frac": st["slow_lanes"] / max(st["slow_waves"] * 64, 1),
                "full_scan_lane_frac_of_slow": st["full_scan_lanes"] / max(st["slow_lanes"], 1),
-               "face_keep_frac": st["faces_kept"] / max(st["faces_total"], 1), **st}
+               "candidates_per_wave": st["wave_candidates"] / w, **st}
         if st.get("cyc_iter"):
             row["cycle_frac"] = {k[4:]: round(st[k] / st["cyc_iter"], 4) for k in st if k.startswith("cyc_")}
             row["cycles_per_wave_iter"] = st["cyc_iter"] / w

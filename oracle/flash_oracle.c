@@ -127,6 +127,7 @@ typedef struct {
   const int32_t* rbf_row_off; /* [R+1] rows (n centres + 1 polynomial row) */
   const int32_t* rbf_acc_off; /* [R+1] offsets in the RBF accumulator block */
   const double* rbf_rows;     /* [rows][4]: (c, w) ... then (a, b) */
+  const int32_t* faces;       /* [F][3] global vertex indices (CCW from outside) */
 } oracle_posed;
 
 /* RBF interpolating skin (src/Flash.jl:207-213, SpatialFields XCubed + affine):
@@ -205,8 +206,9 @@ static void rbf_adjoint(const double* rows, int nc, const double* p, double* acc
   acc[nc + 3] += two_s * fma(dsdf, p[2], uz);
 }
 
-/* Closest point on triangle v = (a, b, c) to p, Voronoi-region walk. */
-static void closest_on_triangle(const double* p, const double* v, double* q) {
+/* Closest point on triangle v = (a, b, c) to p, Voronoi-region walk. *reg:
+ * 0, 1, 2 vertex a, b, c; 3, 4, 5 edge a->b, b->c, c->a; 6 interior. */
+static void closest_on_triangle(const double* p, const double* v, double* q, int* reg) {
   const double ax = v[0], ay = v[1], az = v[2];
   const double bx = v[3], by = v[4], bz = v[5];
   const double cx = v[6], cy = v[7], cz = v[8];
@@ -215,25 +217,27 @@ static void closest_on_triangle(const double* p, const double* v, double* q) {
   const double apx = p[0] - ax, apy = p[1] - ay, apz = p[2] - az;
   const double d1 = fma(abx, apx, fma(aby, apy, abz * apz));
   const double d2 = fma(acx, apx, fma(acy, apy, acz * apz));
-  if (d1 <= 0 && d2 <= 0) { q[0] = ax; q[1] = ay; q[2] = az; return; }
+  if (d1 <= 0 && d2 <= 0) { q[0] = ax; q[1] = ay; q[2] = az; *reg = 0; return; }
   const double bpx = p[0] - bx, bpy = p[1] - by, bpz = p[2] - bz;
   const double d3 = fma(abx, bpx, fma(aby, bpy, abz * bpz));
   const double d4 = fma(acx, bpx, fma(acy, bpy, acz * bpz));
-  if (d3 >= 0 && d4 <= d3) { q[0] = bx; q[1] = by; q[2] = bz; return; }
+  if (d3 >= 0 && d4 <= d3) { q[0] = bx; q[1] = by; q[2] = bz; *reg = 1; return; }
   const double vc = fma(d1, d4, -(d3 * d2));
   if (vc <= 0 && d1 >= 0 && d3 <= 0) {
     const double t = d1 / (d1 - d3);
     q[0] = fma(t, abx, ax); q[1] = fma(t, aby, ay); q[2] = fma(t, abz, az);
+    *reg = 3;
     return;
   }
   const double cpx = p[0] - cx, cpy = p[1] - cy, cpz = p[2] - cz;
   const double d5 = fma(abx, cpx, fma(aby, cpy, abz * cpz));
   const double d6 = fma(acx, cpx, fma(acy, cpy, acz * cpz));
-  if (d6 >= 0 && d5 <= d6) { q[0] = cx; q[1] = cy; q[2] = cz; return; }
+  if (d6 >= 0 && d5 <= d6) { q[0] = cx; q[1] = cy; q[2] = cz; *reg = 2; return; }
   const double vb = fma(d5, d2, -(d1 * d6));
   if (vb <= 0 && d2 >= 0 && d6 <= 0) {
     const double t = d2 / (d2 - d6);
     q[0] = fma(t, acx, ax); q[1] = fma(t, acy, ay); q[2] = fma(t, acz, az);
+    *reg = 5;
     return;
   }
   const double va = fma(d3, d6, -(d5 * d4));
@@ -241,6 +245,7 @@ static void closest_on_triangle(const double* p, const double* v, double* q) {
   if (va <= 0 && e43 >= 0 && e56 >= 0) {
     const double t = e43 / (e43 + e56);
     q[0] = fma(t, cx - bx, bx); q[1] = fma(t, cy - by, by); q[2] = fma(t, cz - bz, bz);
+    *reg = 4;
     return;
   }
   const double inv = 1.0 / (va + vb + vc);
@@ -248,6 +253,7 @@ static void closest_on_triangle(const double* p, const double* v, double* q) {
   q[0] = fma(ww, acx, fma(vv, abx, ax));
   q[1] = fma(ww, acy, fma(vv, aby, ay));
   q[2] = fma(ww, acz, fma(vv, abz, az));
+  *reg = 6;
 }
 
 static inline double plane_value(const double* pl, const double* p) {
@@ -259,28 +265,68 @@ static inline double dist2_to(const double* p, const double* q) {
   return fma(dx, dx, fma(dy, dy, dz * dz));
 }
 
-/* GJK's termination test as an optimality certificate: q is the closest point
- * of conv(V) to p iff max_v (p-q)·v <= (p-q)·q (within rounding tolerance). */
-static int certified(const double* p, const double* q, int v0, int v1, const double* verts, double scale) {
-  const double wx = p[0] - q[0], wy = p[1] - q[1], wz = p[2] - q[2];
-  const double wq = fma(wx, q[0], fma(wy, q[1], wz * q[2]));
-  double smax = -INFINITY;
-  for (int v = v0; v < v1; ++v) {
-    const double* vv = verts + 4 * v;
-    const double sv = fma(vv[0], wx, fma(vv[1], wy, vv[2] * wz));
-    smax = sv > smax ? sv : smax;
+static inline double edge_val(const double* fx, int e, const double* p) {
+  const double* m = fx + 4 * e;
+  return fma(m[0], p[0], fma(m[1], p[1], fma(m[2], p[2], -m[3])));
+}
+
+/* Local optimality certificate of q = closest point of triangle f (Voronoi
+ * region reg) to p, as the kernel's cert_step: w = p - q in the normal cone
+ * of the hull at q. Edge u->v shared with g: both in-plane edge values of p
+ * <= tol; vertex v: w.(u - v) <= tol for every neighbour u, walking the fan of
+ * faces around v through the neighbour table (<= 32 steps). On failure *n1,
+ * *n2 name the faces of the descent step (-1 = none). */
+static int cert_step(const oracle_posed* m, const double* p, int f, int reg, double scale, int* n1, int* n2) {
+  *n1 = -1;
+  *n2 = -1;
+  if (reg == 6) return plane_value(m->planes_w + 4 * f, p) > 0; /* projection: optimal iff p above f */
+  const int32_t* fv = m->faces + 3 * f;
+  if (reg >= 3) {
+    const int e = reg - 3;
+    const int g = m->nbr[3 * f + e];
+    const int32_t w = fv[e == 2 ? 0 : e + 1];
+    const int32_t* gv = m->faces + 3 * g;
+    const int eg = gv[0] == w ? 0 : (gv[1] == w ? 1 : 2); /* g's edge w -> u */
+    const double sf = edge_val(m->facex_w + FX * f, e, p);
+    const double sg = edge_val(m->facex_w + FX * g, eg, p);
+    const double* U = m->verts_w + 4 * fv[e];
+    const double* W = m->verts_w + 4 * w;
+    const double tol = 1e-13 * (((fabs(p[0]) + fabs(p[1])) + fabs(p[2])) + scale) *
+                       ((fabs(W[0] - U[0]) + fabs(W[1] - U[1])) + fabs(W[2] - U[2]));
+    if (sf <= tol && sg <= tol) return 1;
+    if (sg > tol && g != f) *n1 = g;
+    return 0;
   }
+  const int32_t v = fv[reg];
+  const double* V = m->verts_w + 4 * v;
+  const double wx = p[0] - V[0], wy = p[1] - V[1], wz = p[2] - V[2];
   const double tol = 1e-13 * ((fabs(wx) + fabs(wy)) + fabs(wz)) * scale;
-  return smax <= wq + tol;
+  int g = f, j = reg;
+  for (int it = 0; it < 32; ++it) {
+    const double* U = m->verts_w + 4 * m->faces[3 * g + (j == 2 ? 0 : j + 1)];
+    const double dot = fma(wx, U[0] - V[0], fma(wy, U[1] - V[1], wz * (U[2] - V[2])));
+    const int g2 = m->nbr[3 * g + j];
+    if (dot > tol) {
+      *n1 = g != f ? g : g2;
+      *n2 = (g != f && g2 != f) ? g2 : -1;
+      return 0;
+    }
+    if (g2 == f) return 1;
+    const int32_t* gv = m->faces + 3 * g2;
+    j = gv[0] == v ? 0 : (gv[1] == v ? 1 : 2);
+    g = g2;
+  }
+  return 0;
 }
 
 /* Signed distance of p to posed hull k, with its unit gradient. Restates
  * ConvexSurface(x) (src/Flash.jl:238-243) as the exact polytope SDF:
  *   inside / on the surface: max_f h_f (first max face's normal);
  *   outside: h_{f*} when p projects into triangle f*; else the closest point on
- *   triangle f*, then on its neighbours across violated edges, each candidate
- *   certified by the support test; uncertified -> exhaustive scan of the
- *   visible faces whose plane distance is below the best so far. */
+ *   triangle f*, certified by the normal cone at its feature (cert_step); a
+ *   failed certificate names the faces of a strictly descending step (<= 24
+ *   steps); a stalled walk -> exhaustive scan of the visible faces whose plane
+ *   distance is below the best so far (strict < keeps the walk's point). */
 void oracle_hull_sdf(const oracle_posed* m, int32_t k, const double* p, double* d, double* g) {
   const int f0 = m->face_off[k], f1 = m->face_off[k + 1];
   double hmax = -INFINITY;
@@ -298,35 +344,45 @@ void oracle_hull_sdf(const oracle_posed* m, int32_t k, const double* p, double* 
                        fma(fx[4], p[0], fma(fx[5], p[1], fma(fx[6], p[2], -fx[7]))),
                        fma(fx[8], p[0], fma(fx[9], p[1], fma(fx[10], p[2], -fx[11])))};
   if (s[0] >= 0 && s[1] >= 0 && s[2] >= 0) return;
-  const int v0 = m->vert_off[k], v1 = m->vert_off[k + 1];
   const double scale = m->hscale[k];
   double q[3];
-  closest_on_triangle(p, fx + 12, q);
+  int rA;
+  closest_on_triangle(p, fx + 12, q, &rA);
   double best2 = dist2_to(p, q);
-  if (!certified(p, q, v0, v1, m->verts_w, scale)) {
-    for (int e = 0; e < 3; ++e) {
-      if (s[e] < 0) {
-        const int gf = m->nbr[3 * fs + e];
+  /* stage B: descent walk (<= 24 steps), each step to a face the failed
+   * certificate names, accepted only if strictly closer */
+  int cf = fs, cr = rA, todo = 1;
+  for (int step = 0; step < 24; ++step) {
+    int n1, n2;
+    if (cert_step(m, p, cf, cr, scale, &n1, &n2)) { todo = 0; break; }
+    int moved = 0;
+    for (int t = 0; t < 2; ++t) {
+      const int g = t == 0 ? n1 : n2;
+      if (g >= 0) {
         double c[3];
-        closest_on_triangle(p, m->facex_w + FX * gf + 12, c);
+        int rg;
+        closest_on_triangle(p, m->facex_w + FX * g + 12, c, &rg);
         const double d2 = dist2_to(p, c);
-        if (d2 < best2) { best2 = d2; q[0] = c[0]; q[1] = c[1]; q[2] = c[2]; }
+        if (d2 < best2) { best2 = d2; q[0] = c[0]; q[1] = c[1]; q[2] = c[2]; cf = g; cr = rg; moved = 1; }
       }
     }
-    if (!certified(p, q, v0, v1, m->verts_w, scale)) {
-      double b2 = INFINITY, b[3] = {0, 0, 0};
-      for (int f = f0; f < f1; ++f) {
-        const double h = plane_value(m->planes_w + 4 * f, p);
-        if (h > 0 && h * h < b2) {
-          double c[3];
-          closest_on_triangle(p, m->facex_w + FX * f + 12, c);
-          const double d2 = dist2_to(p, c);
-          if (d2 < b2) { b2 = d2; b[0] = c[0]; b[1] = c[1]; b[2] = c[2]; }
-        }
+    if (!moved) break;
+  }
+  if (todo) {
+    /* stage C: continues from the walk's point; only a strictly closer face replaces it */
+    double b2 = best2, b[3] = {q[0], q[1], q[2]};
+    for (int f = f0; f < f1; ++f) {
+      const double h = plane_value(m->planes_w + 4 * f, p);
+      if (h > 0 && h * h < b2) {
+        double c[3];
+        int rg;
+        closest_on_triangle(p, m->facex_w + FX * f + 12, c, &rg);
+        const double d2 = dist2_to(p, c);
+        if (d2 < b2) { b2 = d2; b[0] = c[0]; b[1] = c[1]; b[2] = c[2]; }
       }
-      best2 = b2;
-      q[0] = b[0]; q[1] = b[1]; q[2] = b[2];
     }
+    best2 = b2;
+    q[0] = b[0]; q[1] = b[1]; q[2] = b[2];
   }
   if (best2 > 0) {
     *d = sqrt(best2);

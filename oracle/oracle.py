@@ -36,7 +36,7 @@ class Posed(ctypes.Structure):
     _fields_ = [("K", c_int32), ("face_off", c_void_p), ("vert_off", c_void_p), ("nbr", c_void_p),
                 ("planes_w", c_void_p), ("facex_w", c_void_p), ("verts_w", c_void_p), ("hscale", c_void_p),
                 ("S", c_int32), ("surf_index", c_void_p), ("rbf_row_off", c_void_p), ("rbf_acc_off", c_void_p),
-                ("rbf_rows", c_void_p)]
+                ("rbf_rows", c_void_p), ("faces", c_void_p)]
 
 
 def load():
@@ -149,7 +149,7 @@ class OracleModel:
         st = Posed(self.K, self.face_off.ctypes.data, self.vert_off.ctypes.data, self.nbr.ctypes.data,
                    pw.ctypes.data, fx.ctypes.data, vw.ctypes.data, hs.ctypes.data, self.S,
                    self.surf_index.ctypes.data, self.rbf_row_off.ctypes.data, self.rbf_acc_off.ctypes.data,
-                   rr.ctypes.data)
+                   rr.ctypes.data, self.faces.ctypes.data)
         return st, arrays
 
     def skin(self, poses, pts, threads: int = 0, rbf_rows=None):

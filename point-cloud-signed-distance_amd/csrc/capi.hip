@@ -146,6 +146,7 @@ static void free_model(fsdf_ctx* c) {
   dfree(c->pm.hscale_w);
   dfree(c->pm.planes_w);
   dfree(c->pm.spheres_w);
+  dfree(c->pm.screen_w);
   dfree(c->d_poses);
   dfree(c->d_accum);
   c->lm = fsdf::LocalModel();
@@ -386,6 +387,7 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   HIPCHECK(c, dalloc((char**)&c->pm.hscale_w, (size_t)K * tsz));
   HIPCHECK(c, dalloc((char**)&c->pm.planes_w, (size_t)std::max(F, 1) * 4 * tsz));
   HIPCHECK(c, dalloc(&c->pm.spheres_w, (size_t)K * 4 * sizeof(float)));
+  HIPCHECK(c, dalloc(&c->pm.screen_w, (size_t)std::max(F + K, 1) * 4 * sizeof(float)));
   HIPCHECK(c, dalloc(&c->d_poses, (size_t)S * 12 * sizeof(double)));
   const int R = (int)rbf_surface.size();
   HIPCHECK(c, dalloc(&c->d_accum, (size_t)(1 + 6 * S + rbf_acc_off.back()) * sizeof(double)));

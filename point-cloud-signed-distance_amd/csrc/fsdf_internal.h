@@ -19,6 +19,11 @@
 //     spheres_w [K][4]  f32     world centroid + radius (culling only)
 //     verts_w   [V][4]  T       world vertices (support/optimality certificate)
 //     hscale_w  [K]     T       max_v |v|_1 over the hull's world vertices
+//     screen_w  [F+K][4] f32    fp32 screening planes, hull-centred, in face pairs:
+//                               hull k's pair j at slots face_off[k]+k+2j (32 B):
+//                               (nx_a nx_b ny_a ny_b nz_a nz_b -d'_a -d'_b), a = 2j,
+//                               b = 2j+1 (= a when nf is odd and j is the last pair),
+//                               d' = d - n·c with c the hull's f32 sphere centre
 //
 //   per-block partial sums  partials [1+6K][nblocks] f64 (column = block)
 #pragma once
@@ -60,6 +65,7 @@ struct PosedModel {
   float* spheres_w = nullptr;
   void* verts_w = nullptr;    // T
   void* hscale_w = nullptr;   // T
+  float* screen_w = nullptr;  // [F+K][4] (f64 contexts; see the layout above)
   void* rbf_rows = nullptr;   // T [rbf_rows][4], per pass (fsdf_set_rbf_params)
 };
 

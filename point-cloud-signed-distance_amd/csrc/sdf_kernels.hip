@@ -64,7 +64,8 @@ __device__ __forceinline__ void rot_vec(const double* P, const double* v, double
 template <typename T>
 __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const double* __restrict__ poses,
                                                       T* __restrict__ planes_w, float* __restrict__ spheres_w,
-                                                      T* __restrict__ verts_w, T* __restrict__ hscale_w) {
+                                                      T* __restrict__ verts_w, T* __restrict__ hscale_w,
+                                                      float* __restrict__ screen_w) {
   int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int fv = lm.F + lm.V, fv_pad = (fv + 63) & ~63;
   if (tid >= fv && tid < fv_pad) return;  // padding: hull waves start wave-aligned
@@ -83,6 +84,23 @@ __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const doubl
     const double dw = __builtin_fma(nw[0], P[9], __builtin_fma(nw[1], P[10], __builtin_fma(nw[2], P[11], pl[3])));
     T* pw = planes_w + 4 * f;
     pw[0] = (T)nw[0]; pw[1] = (T)nw[1]; pw[2] = (T)nw[2]; pw[3] = (T)dw;
+    if (screen_w) {
+      // fp32 screening copy, centred on the hull's f32 sphere centre c (the
+      // same bits the sphere thread below stores): d' = d - n·c
+      const int h = lm.face_hull[f];
+      const int j = f - lm.face_off[h], nf = lm.face_off[h + 1] - lm.face_off[h];
+      double cw[3];
+      xf_point(P, lm.sphere_l + 4 * h, cw);
+      const double c0 = (double)(float)cw[0], c1 = (double)(float)cw[1], c2 = (double)(float)cw[2];
+      const double dc = dw - __builtin_fma(nw[0], c0, __builtin_fma(nw[1], c1, nw[2] * c2));
+      float* pair = screen_w + 4 * (lm.face_off[h] + h + (j & ~1));
+      const float v[4] = {(float)nw[0], (float)nw[1], (float)nw[2], (float)(-dc)};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) pair[2 * c + (j & 1)] = v[c];
+      if ((nf & 1) && j == nf - 1)  // odd count: the last pair repeats its face
+#pragma unroll
+        for (int c = 0; c < 4; ++c) pair[2 * c + 1] = v[c];
+    }
   } else if (tid < lm.F + lm.V) {
     const int v = tid - lm.F;
     const double* P = poses + 12 * lm.hull_surface[lm.vert_hull[v]];
@@ -128,10 +146,13 @@ template <typename T> struct Row4 { typedef T __attribute__((ext_vector_type(4))
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 typedef int I4 __attribute__((ext_vector_type(4)));
 
+// reg: the Voronoi region of the result — 0, 1, 2 vertex a, b, c; 3, 4, 5 the
+// edge a→b, b→c, c→a (face edges 0, 1, 2); 6 the interior.
 template <typename T>
 __device__ __forceinline__ void closest_on_triangle(T px, T py, T pz, const typename Row4<T>::type& A,
                                                     const typename Row4<T>::type& B,
-                                                    const typename Row4<T>::type& C, T& qx, T& qy, T& qz) {
+                                                    const typename Row4<T>::type& C, T& qx, T& qy, T& qz,
+                                                    int& reg) {
   const T ax = A[0], ay = A[1], az = A[2];
   const T bx = B[0], by = B[1], bz = B[2];
   const T cx = C[0], cy = C[1], cz = C[2];
@@ -140,25 +161,27 @@ __device__ __forceinline__ void closest_on_triangle(T px, T py, T pz, const type
   const T apx = px - ax, apy = py - ay, apz = pz - az;
   const T d1 = mfma_(abx, apx, mfma_(aby, apy, abz * apz));
   const T d2 = mfma_(acx, apx, mfma_(acy, apy, acz * apz));
-  if (d1 <= (T)0 && d2 <= (T)0) { qx = ax; qy = ay; qz = az; return; }
+  if (d1 <= (T)0 && d2 <= (T)0) { qx = ax; qy = ay; qz = az; reg = 0; return; }
   const T bpx = px - bx, bpy = py - by, bpz = pz - bz;
   const T d3 = mfma_(abx, bpx, mfma_(aby, bpy, abz * bpz));
   const T d4 = mfma_(acx, bpx, mfma_(acy, bpy, acz * bpz));
-  if (d3 >= (T)0 && d4 <= d3) { qx = bx; qy = by; qz = bz; return; }
+  if (d3 >= (T)0 && d4 <= d3) { qx = bx; qy = by; qz = bz; reg = 1; return; }
   const T vc = mfma_(d1, d4, -(d3 * d2));
   if (vc <= (T)0 && d1 >= (T)0 && d3 <= (T)0) {
     const T t = d1 / (d1 - d3);
     qx = mfma_(t, abx, ax); qy = mfma_(t, aby, ay); qz = mfma_(t, abz, az);
+    reg = 3;
     return;
   }
   const T cpx = px - cx, cpy = py - cy, cpz = pz - cz;
   const T d5 = mfma_(abx, cpx, mfma_(aby, cpy, abz * cpz));
   const T d6 = mfma_(acx, cpx, mfma_(acy, cpy, acz * cpz));
-  if (d6 >= (T)0 && d5 <= d6) { qx = cx; qy = cy; qz = cz; return; }
+  if (d6 >= (T)0 && d5 <= d6) { qx = cx; qy = cy; qz = cz; reg = 2; return; }
   const T vb = mfma_(d5, d2, -(d1 * d6));
   if (vb <= (T)0 && d2 >= (T)0 && d6 <= (T)0) {
     const T t = d2 / (d2 - d6);
     qx = mfma_(t, acx, ax); qy = mfma_(t, acy, ay); qz = mfma_(t, acz, az);
+    reg = 5;
     return;
   }
   const T va = mfma_(d3, d6, -(d5 * d4));
@@ -166,6 +189,7 @@ __device__ __forceinline__ void closest_on_triangle(T px, T py, T pz, const type
   if (va <= (T)0 && e43 >= (T)0 && e56 >= (T)0) {
     const T t = e43 / (e43 + e56);
     qx = mfma_(t, cx - bx, bx); qy = mfma_(t, cy - by, by); qz = mfma_(t, cz - bz, bz);
+    reg = 4;
     return;
   }
   const T inv = (T)1 / (va + vb + vc);
@@ -173,6 +197,7 @@ __device__ __forceinline__ void closest_on_triangle(T px, T py, T pz, const type
   qx = mfma_(w_, acx, mfma_(v_, abx, ax));
   qy = mfma_(w_, acy, mfma_(v_, aby, ay));
   qz = mfma_(w_, acz, mfma_(v_, abz, az));
+  reg = 6;
 }
 
 // Inward edge-plane value of edge u -> w of a face with unit normal n:
@@ -209,6 +234,7 @@ struct PassModel {
   const T* __restrict__ verts;
   const T* __restrict__ hscale;
   const float* __restrict__ spheres;
+  const float* __restrict__ screen;          // fp32 screening pairs (f64 contexts)
 };
 
 // Per-workgroup LDS hull table, filled once in the kernel prologue (row K is
@@ -286,7 +312,8 @@ __device__ __forceinline__ bool count_events(const unsigned long long* stats) {
 }  // RBF adjoint doubles per wave (Σ 4n+4)
 // Diagnostic ablations (timing-only builds via -DFSDF_ABLATE=mask; results are
 // wrong): 4 no slow path, 16 no segmented reduction, 32 no per-point stores,
-// 64 no hull staging loads (LDS stage left as is).
+// 64 no hull staging loads (LDS stage left as is), 128 no plane max (face 0),
+// 256 certificates skipped (stage A accepted), 512 no stage B/C.
 #ifndef FSDF_ABLATE
 #define FSDF_ABLATE 0
 #endif
@@ -314,7 +341,8 @@ __device__ __forceinline__ void stage_rows(T* __restrict__ lds, const T* __restr
 #ifndef FSDF_PLANE_BATCH
 #define FSDF_PLANE_BATCH 8
 #endif
-constexpr int kPlaneBatch = FSDF_PLANE_BATCH;  // plane rows per LDS batch (power of 2, >= 2)
+constexpr int kPlaneBatch = FSDF_PLANE_BATCH;
+constexpr int kWalkSteps = 24;  // descent-walk cap before the exhaustive stage C  // plane rows per LDS batch (power of 2, >= 2)
 
 template <typename T>
 __device__ __forceinline__ void stage_hull(T* __restrict__ lw, const T* __restrict__ planes,
@@ -346,6 +374,20 @@ __device__ __forceinline__ void stage_hull(T* __restrict__ lw, const T* __restri
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Wave-uniform rows read through the scalar unit: a pointer in the constant
+// address space makes every uniform-index read an s_load into SGPRs, which the
+// VALU takes as a broadcast operand — no LDS bandwidth (the plane max was
+// LDS-bound: two broadcast ds_read_b128 per face and wave, 4 waves per LDS).
+#ifndef FSDF_SCALAR_PLANES
+#define FSDF_SCALAR_PLANES 1
+#endif
+template <typename T>
+using CRow = const __attribute__((address_space(4))) typename Row4<T>::type*;
+template <typename T>
+__device__ __forceinline__ CRow<T> scalar_rows(const T* p) {
+  return (CRow<T>)(p);
+}
+
 template <typename T>
 __device__ __forceinline__ T plane_h(const typename Row4<T>::type& pl, T px, T py, T pz) {
   return mfma_(pl[0], px, mfma_(pl[1], py, mfma_(pl[2], pz, -pl[3])));
@@ -355,29 +397,6 @@ template <typename T> __device__ __forceinline__ T cert_eps();
 template <> __device__ __forceinline__ double cert_eps() { return 1e-13; }
 template <> __device__ __forceinline__ float cert_eps() { return 4e-6f; }
 
-// Optimality certificate of a candidate closest point q of the staged hull
-// (the GJK termination test): q is the closest point of conv(V) to p iff
-// max_v (p-q)·v <= (p-q)·q; accepted within a rounding tolerance.
-// Two v_max chains over the staged vertex rows (the maximum is exact in any
-// order); an odd count repeats the last vertex, which leaves it unchanged.
-template <typename T>
-__device__ __forceinline__ bool certified(T px, T py, T pz, T qx, T qy, T qz, const typename Row4<T>::type* lv,
-                                          int nv, T scale) {
-  typedef typename Row4<T>::type R;
-  const T wx = px - qx, wy = py - qy, wz = pz - qz;
-  const T wq = mfma_(wx, qx, mfma_(wy, qy, wz * qz));
-  T sA = -tinf<T>(), sB = -tinf<T>();
-#pragma unroll 4
-  for (int v = 0; v < nv; v += 2) {
-    const R a = lv[v], b = lv[min(v + 1, nv - 1)];
-    sA = __builtin_fmax(sA, mfma_(a[0], wx, mfma_(a[1], wy, a[2] * wz)));
-    sB = __builtin_fmax(sB, mfma_(b[0], wx, mfma_(b[1], wy, b[2] * wz)));
-  }
-  const T smax = __builtin_fmax(sA, sB);
-  const T tol = cert_eps<T>() * ((fabs(wx) + fabs(wy)) + fabs(wz)) * scale;
-  return smax <= wq + tol;
-}
-
 // packed face row: (i0 | i1<<16, i2 | n0<<16, n1 | n2<<16, 0) with i_j the
 // hull-local vertex indices and n_e the hull-local face across edge e (i_e -> i_e+1)
 __device__ __forceinline__ int fr_vert(const I4& r, int j) {
@@ -385,6 +404,140 @@ __device__ __forceinline__ int fr_vert(const I4& r, int j) {
 }
 __device__ __forceinline__ int fr_nbr(const I4& r, int e) {
   return e == 0 ? ((r[1] >> 16) & 0xffff) : (e == 1 ? (r[2] & 0xffff) : ((r[2] >> 16) & 0xffff));
+}
+
+// Local optimality certificate of q = the closest point of triangle f (in
+// Voronoi region reg) to p: q is the closest point of the convex hull iff
+// w = p − q lies in the hull's normal cone at q (exact characterisation):
+//   edge u→v of f, shared with face g:  m_f·w <= 0 and m_g·w <= 0 (m the
+//     in-plane inward edge normals; m·w is the edge value of p since q is on
+//     the edge line);
+//   vertex v:  w·(u − v) <= 0 for every neighbour u of v — the fan of faces
+//     around v is walked through the packed neighbour rows (<= 32 steps).
+// When the test fails it names the faces holding strictly closer points (a
+// descent step): across the edge, g; at a vertex whose edge v→u is violated,
+// the face g of that edge in the fan and the face across it (n1, n2; -1 =
+// none; the current face f is never repeated). An interior point is
+// certified iff p is above f's plane; a fan longer than 32 gives no
+// certificate and no step. Tolerances accept rounding-level violations (a
+// false certificate moves the answer by O(tol^2)). oracle/flash_oracle.c:
+// cert_step mirrors every operation.
+template <typename T>
+__device__ __forceinline__ bool cert_step(T px, T py, T pz, int f, int reg,
+                                          const typename Row4<T>::type* __restrict__ lp,
+                                          const typename Row4<T>::type* __restrict__ lv,
+                                          const I4* __restrict__ lf, T scale, int& n1, int& n2) {
+  typedef typename Row4<T>::type R;
+  n1 = -1;
+  n2 = -1;
+  // interior of triangle f: q is p's projection on f's plane, optimal iff p is
+  // on the outer side (the plane supports the hull)
+  if (reg == 6) return plane_h<T>(lp[f], px, py, pz) > (T)0;
+  const I4 fr = lf[f];
+  if (reg >= 3) {
+    const int e = reg - 3;
+    const R U = lv[fr_vert(fr, e)], W = lv[fr_vert(fr, e == 2 ? 0 : e + 1)];
+    const int g = fr_nbr(fr, e);
+    const T sf = edge_value<T>(lp[f], U, W, px, py, pz);
+    const T sg = edge_value<T>(lp[g], W, U, px, py, pz);
+    // |m| = |W − U|: the tolerance is a lateral offset of eps (|p|_1 + scale)
+    const T tol = cert_eps<T>() * (((fabs(px) + fabs(py)) + fabs(pz)) + scale) *
+                  ((fabs(W[0] - U[0]) + fabs(W[1] - U[1])) + fabs(W[2] - U[2]));
+    if (sf <= tol && sg <= tol) return true;
+    if (sg > tol && g != f) n1 = g;
+    return false;
+  }
+  const int v = fr_vert(fr, reg);
+  const R V = lv[v];
+  const T wx = px - V[0], wy = py - V[1], wz = pz - V[2];
+  const T tol = cert_eps<T>() * ((fabs(wx) + fabs(wy)) + fabs(wz)) * scale;
+  int g = f, j = reg;
+  I4 r = fr;
+  for (int it = 0; it < 32; ++it) {
+    const R Un = lv[fr_vert(r, j == 2 ? 0 : j + 1)];
+    const T dot = mfma_(wx, Un[0] - V[0], mfma_(wy, Un[1] - V[1], wz * (Un[2] - V[2])));
+    const int g2 = fr_nbr(r, j);  // across edge v -> u
+    if (dot > tol) {
+      n1 = g != f ? g : g2;
+      n2 = g != f && g2 != f ? g2 : -1;
+      return false;
+    }
+    if (g2 == f) return true;
+    r = lf[g2];
+    j = fr_vert(r, 0) == v ? 0 : (fr_vert(r, 1) == v ? 1 : 2);
+    g = g2;
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------------------
+// fp32-screened plane max (f64 contexts): the exact first-index argmax of the
+// fp64 plane values h_f = n_f·p − d_f, from an fp32 pass over all faces plus
+// an fp64 pass over ONE batch of 8.
+//   Screen: h'_f = n'·q − d'' in packed fp32 (v_pk_fma_f32: two faces per
+//   instruction, plane pairs read through the scalar unit), q = fl32(p − c),
+//   c the hull's sphere centre, with |h'_f − h_f| <= E = 16u (|q|_1 + r)
+//   (u = 2^-24; |n_i| <= 1 and |d − n·c| <= r). Per batch of 8 faces the
+//   maximum b; b1 = best batch maximum, b2 = best over the other batches.
+//   If b2 < b1 − 2E, every face g outside the best batch has
+//   h_g <= b2 + E < b1 − E <= max h over the batch: the exact maximum lies in
+//   the best batch only, and its first-index argmax over the batch's 8 faces
+//   (fp64, the same plane_h arithmetic) IS the first-index argmax over all
+//   faces — bit for bit the full fp64 scan (the oracle's). Lanes without that
+//   margin (near-ties across batches) return false and take the full scan.
+// Returns true iff the result is final for every lane that needs it.
+// ---------------------------------------------------------------------------
+#ifndef FSDF_SCREEN32
+#define FSDF_SCREEN32 1
+#endif
+typedef float F2v __attribute__((ext_vector_type(2)));
+typedef float F8v __attribute__((ext_vector_type(8)));
+typedef const __attribute__((address_space(4))) F8v* CF8;
+
+template <typename T>
+__device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0, int nf, const PassModel<T>& m,
+                                                 const HullRow* __restrict__ ht,
+                                                 const typename Row4<T>::type* __restrict__ lp, bool active,
+                                                 T& hA, int& iA) {
+  const F4 sp = ht[k].sphere;
+  const float qx = (float)(px - (T)sp[0]), qy = (float)(py - (T)sp[1]), qz = (float)(pz - (T)sp[2]);
+  // 2E, plus an absolute term for the fp64 rounding of h_f itself (~1e-15 |p|)
+  const float E2 = 32.0f * 5.9604645e-8f * (((fabsf(qx) + fabsf(qy)) + fabsf(qz)) + sp[3]) * 1.0001f +
+                   1e-12f * (1.0f + fabsf((float)px) + fabsf((float)py) + fabsf((float)pz) + sp[3]);
+  const F2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
+  const CF8 gs = (CF8)(m.screen + 4 * (f0 + k));
+  const int np = (nf + 1) >> 1;
+  float b1 = -__builtin_huge_valf(), b2 = -__builtin_huge_valf();
+  int ib = 0;
+  auto batch = [&](int i, bool tail) {
+    F8v c[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c[q] = gs[tail ? min(i + q, np - 1) : i + q];
+    float mb = -__builtin_huge_valf();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const F2v nx = {c[q][0], c[q][1]}, ny = {c[q][2], c[q][3]}, nz = {c[q][4], c[q][5]}, nd = {c[q][6], c[q][7]};
+      const F2v h = __builtin_elementwise_fma(nx, qx2, __builtin_elementwise_fma(ny, qy2, __builtin_elementwise_fma(nz, qz2, nd)));
+      mb = fmaxf(mb, fmaxf(h[0], h[1]));
+    }
+    b2 = fmaxf(b2, fminf(b1, mb));
+    if (mb > b1) { b1 = mb; ib = i; }
+  };
+  int i0 = 0;
+  for (; i0 + 4 <= np; i0 += 4) batch(i0, false);
+  if (i0 < np) batch(i0, true);
+  // exact fp64 first-index argmax over the best batch's faces
+  const int fb = 2 * ib;
+  hA = -tinf<T>();
+  iA = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int f = min(fb + q, nf - 1);
+    const T h = plane_h<T>(lp[f], px, py, pz);
+    if (h > hA) { hA = h; iA = f; }
+  }
+  const bool safe = b2 < b1 - E2;
+  return !__any(active && !safe);
 }
 
 // ---------------------------------------------------------------------------
@@ -417,6 +570,8 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   const R* lv = lp + nf;
   const I4* lf = (const I4*)(lv + nv);
   const T scale = (T)ht[k].hscale;
+  const CRow<T> gp = scalar_rows<T>(m.planes + 4 * f0);  // uniform plane rows (SGPR)
+  auto uplane = [&](int f) -> R { return FSDF_SCALAR_PLANES ? (R)gp[f] : lp[f]; };
   // two independent running maxima (even / odd faces) shorten the serial
   // compare chain; merged with the first-index rule, identical to one chain
   // Batches of kPlaneBatch rows, all of a batch's LDS reads issued before the
@@ -426,11 +581,19 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   // operations, same bits) — the first-index argmax over all faces. Missing
   // rows of the last batch repeat the last face (same value, never first).
   T hA = -tinf<T>();
+  int iA = 0;
+  bool screened = (FSDF_ABLATE & 128) != 0;  // ablation: no plane max (face 0)
+  if (screened) hA = plane_h<T>(lp[0], px, py, pz);
+  if constexpr (sizeof(T) == 8) {
+    if (FSDF_SCREEN32 && !screened) screened = screen_plane_max(px, py, pz, k, f0, nf, m, ht, lp, active, hA, iA);
+  }
+  if (!screened) {
+  hA = -tinf<T>();
   int ib = 0;
   auto batch = [&](int i, bool tail) {
     R c[kPlaneBatch];
 #pragma unroll
-    for (int q = 0; q < kPlaneBatch; ++q) c[q] = lp[tail ? min(i + q, nf - 1) : i + q];
+    for (int q = 0; q < kPlaneBatch; ++q) c[q] = uplane(tail ? min(i + q, nf - 1) : i + q);
     T h[kPlaneBatch];
 #pragma unroll
     for (int q = 0; q < kPlaneBatch; ++q) h[q] = plane_h<T>(c[q], px, py, pz);
@@ -445,11 +608,12 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   if (i0 < nf) batch(i0, true);
   // faces before batch ib are all < hA, so the window may start earlier
   const int fb = nf >= kPlaneBatch ? min(ib, nf - kPlaneBatch) : ib;
-  int iA = min(fb + kPlaneBatch - 1, nf - 1);
+  iA = min(fb + kPlaneBatch - 1, nf - 1);
 #pragma unroll
   for (int q = kPlaneBatch - 1; q >= 0; --q) {
     const int f = nf >= kPlaneBatch ? fb + q : min(fb + q, nf - 1);
     if (plane_h<T>(lp[f], px, py, pz) == hA) iA = f;
+  }
   }
   phase_add(stats, 12, tp);
   tp = phase_clock();
@@ -486,47 +650,87 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
     atomicAdd(stats + 2, 1ull);
     atomicAdd(stats + 4, (unsigned long long)__builtin_popcountll(slow_mask));
   }
-  // stage A: closest point on triangle f*
+  // stage A: closest point on triangle f*, certified by the normal cone at
+  // its Voronoi feature
   const I4 frs = lf[fs];
   T qx, qy, qz;
-  closest_on_triangle<T>(px, py, pz, lv[fr_vert(frs, 0)], lv[fr_vert(frs, 1)], lv[fr_vert(frs, 2)], qx, qy, qz);
+  int rA;
+  closest_on_triangle<T>(px, py, pz, lv[fr_vert(frs, 0)], lv[fr_vert(frs, 1)], lv[fr_vert(frs, 2)], qx, qy, qz, rA);
   T ex = px - qx, ey = py - qy, ez = pz - qz;
   T best2 = mfma_(ex, ex, mfma_(ey, ey, ez * ez));
-  bool todo = slow && !certified(px, py, pz, qx, qy, qz, lv, nv, scale);
-  if (__any(todo)) {
-    // stage B: the neighbours across the violated edges of f*
-    if (count_events(stats) && (threadIdx.x & 63) == 0) atomicAdd(stats + 6, 1ull);
-    const T sv[3] = {s0, s1, s2};
+  // stage B: descent walk — certify the current point; on failure move to the
+  // face(s) the certificate names (each accepted step strictly lowers the
+  // distance, so the walk cannot cycle); lanes that stall or exceed the step
+  // cap keep `todo` for the exhaustive stage C.
+  bool todo = !(FSDF_ABLATE & 256) && slow;
+  int cf = fs, cr = rA;
+  bool walking = todo;
+  for (int step = 0; step < kWalkSteps && __any(walking); ++step) {
+    if (walking) {
+      int n1, n2;
+      if (cert_step<T>(px, py, pz, cf, cr, lp, lv, lf, scale, n1, n2)) {
+        todo = false;
+        walking = false;
+      } else {
+        bool moved = false;
 #pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      if (todo && sv[e] < (T)0) {
-        const I4 gr = lf[fr_nbr(frs, e)];
-        T cx, cy, cz;
-        closest_on_triangle<T>(px, py, pz, lv[fr_vert(gr, 0)], lv[fr_vert(gr, 1)], lv[fr_vert(gr, 2)], cx, cy, cz);
-        const T dx = px - cx, dy = py - cy, dz = pz - cz;
-        const T d2 = mfma_(dx, dx, mfma_(dy, dy, dz * dz));
-        if (d2 < best2) { best2 = d2; qx = cx; qy = cy; qz = cz; }
+        for (int t = 0; t < 2; ++t) {
+          const int g = t == 0 ? n1 : n2;
+          if (g >= 0) {
+            const I4 gr = lf[g];
+            T cx, cy, cz;
+            int rg;
+            closest_on_triangle<T>(px, py, pz, lv[fr_vert(gr, 0)], lv[fr_vert(gr, 1)], lv[fr_vert(gr, 2)], cx, cy, cz,
+                                   rg);
+            const T dx = px - cx, dy = py - cy, dz = pz - cz;
+            const T d2 = mfma_(dx, dx, mfma_(dy, dy, dz * dz));
+            if (d2 < best2) { best2 = d2; qx = cx; qy = cy; qz = cz; cf = g; cr = rg; moved = true; }
+          }
+        }
+        walking = moved;
       }
     }
-    todo = todo && !certified(px, py, pz, qx, qy, qz, lv, nv, scale);
+  }
+  if (__any(todo) && !(FSDF_ABLATE & 512)) {
+    if (count_events(stats) && (threadIdx.x & 63) == 0) atomicAdd(stats + 6, 1ull);
     const uint64_t scan_mask = __ballot(todo);
     if (scan_mask) {
       // stage C: exhaustive scan of the visible faces (the closest boundary
       // point of a convex polytope lies on one of them); a face whose plane
       // distance already exceeds the best distance cannot improve it.
       if (count_events(stats) && (threadIdx.x & 63) == 0) atomicAdd(stats + 7, (unsigned long long)__builtin_popcountll(scan_mask));
-      T b2 = tinf<T>();
-      T bx = (T)0, by = (T)0, bz = (T)0;
-      for (int ff = 0; ff < nf; ++ff) {
-        const T h = plane_h<T>(lp[ff], px, py, pz);
-        if (todo && h > (T)0 && h * h < b2) {
-          const I4 gr = lf[ff];
-          T cx, cy, cz;
-          closest_on_triangle<T>(px, py, pz, lv[fr_vert(gr, 0)], lv[fr_vert(gr, 1)], lv[fr_vert(gr, 2)], cx, cy,
-                                 cz);
-          const T dx = px - cx, dy = py - cy, dz = pz - cz;
-          const T d2 = mfma_(dx, dx, mfma_(dy, dy, dz * dz));
-          if (d2 < b2) { b2 = d2; bx = cx; by = cy; bz = cz; }
+      // starts from the stage-B point (strict < keeps it on ties): with b2
+      // already near the optimum, the plane-distance test h^2 < b2 leaves only
+      // the few faces around the closest feature for closest_on_triangle
+      T b2 = best2;
+      T bx = qx, by = qy, bz = qz;
+      // Per chunk of 64 faces: a wave-uniform pass marks, per lane, the faces
+      // that pass the test against the stage-B distance (broadcast plane rows,
+      // no branches); then each lane walks its own marks in index order,
+      // re-testing against its current b2 — the oracle's sequential scan,
+      // without running closest_on_triangle for faces no lane needs.
+      for (int c0 = 0; c0 < nf; c0 += 64) {
+        const int cn = min(64, nf - c0);
+        uint64_t mark = 0;
+        for (int j = 0; j < cn; ++j) {
+          const T h = plane_h<T>(uplane(c0 + j), px, py, pz);
+          if (h > (T)0 && h * h < b2) mark |= 1ull << j;
+        }
+        if (!todo) mark = 0;
+        while (mark) {
+          const int ff = c0 + __builtin_ctzll(mark);
+          mark &= mark - 1;
+          const T h = plane_h<T>(lp[ff], px, py, pz);
+          if (h * h < b2) {
+            const I4 gr = lf[ff];
+            T cx, cy, cz;
+            int rg;
+            closest_on_triangle<T>(px, py, pz, lv[fr_vert(gr, 0)], lv[fr_vert(gr, 1)], lv[fr_vert(gr, 2)], cx, cy,
+                                   cz, rg);
+            const T dx = px - cx, dy = py - cy, dz = pz - cz;
+            const T d2 = mfma_(dx, dx, mfma_(dy, dy, dz * dz));
+            if (d2 < b2) { b2 = d2; bx = cx; by = cy; bz = cz; }
+          }
         }
       }
       if (todo) { best2 = b2; qx = bx; qy = by; qz = bz; }
@@ -845,31 +1049,38 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   uint64_t done[SLOTS];
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) done[s] = 0;
-  if (CULL && K > 0) {
-    // Phase B: each lane's seed hull first (one evaluation per distinct seed
-    // in the wave) so that `best` is tight before the sweep.
-    uint64_t pend = __ballot(valid);
-    while (pend) {
-      const int kk = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(pend), 64));
-      pend &= ~__ballot(valid && kseed == kk);
-      evaluate(kk, needs(kk));
+  // ONE evaluation site (hull_sdf is large: two inlined copies doubled the
+  // kernel's code to ~40 KB): first each lane's seed hull (Phase B, one
+  // evaluation per distinct seed in the wave, so that `best` is tight), then
+  // the remaining candidates in index order (Phase C).
+  uint64_t pend = (CULL && K > 0) ? __ballot(valid) : 0ull;
+  int slot = -1;      // Phase C slot; -1 while seeds are pending
+  uint64_t cm = 0ull;  // Phase C candidates left in `slot`
+  for (;;) {
+    int k;
+    bool need;
+    if (pend) {
+      k = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(pend), 64));
+      pend &= ~__ballot(valid && kseed == k);
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s)
-        if ((kk >> 6) == s) done[s] |= 1ull << (kk & 63);
+        if ((k >> 6) == s) done[s] |= 1ull << (k & 63);
       if (count_events(stats) && lane == 0) atomicAdd(stats + 5, 1ull);
-    }
-  }
-  // Phase C: sweep the remaining candidates in index order.
+      need = needs(k);
+    } else {
+      while (!cm && slot < SLOTS - 1) {
+        ++slot;
 #pragma unroll
-  for (int s = 0; s < SLOTS; ++s) {
-    uint64_t cm = cand[s] & ~done[s];
-    while (cm) {
-      const int k = 64 * s + __builtin_ctzll(cm);
+        for (int s = 0; s < SLOTS; ++s)
+          if (s == slot) cm = cand[s] & ~done[s];
+      }
+      if (!cm) break;
+      k = 64 * slot + __builtin_ctzll(cm);
       cm &= cm - 1;
-      const bool need = needs(k);
+      need = needs(k);
       if (!__any(need)) continue;
-      evaluate(k, need);
     }
+    evaluate(k, need);
   }
   if (count_events(stats) && lane == 0) atomicAdd(stats + 0, 1ull);
 }
@@ -1100,10 +1311,11 @@ hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_pose
   const int grid = (total + kBlock - 1) / kBlock;
   if (precision == 64) {
     hipLaunchKernelGGL(pose_kernel<double>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses,
-                       (double*)pm.planes_w, pm.spheres_w, (double*)pm.verts_w, (double*)pm.hscale_w);
+                       (double*)pm.planes_w, pm.spheres_w, (double*)pm.verts_w, (double*)pm.hscale_w,
+                       pm.screen_w);
   } else {
     hipLaunchKernelGGL(pose_kernel<float>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses, (float*)pm.planes_w,
-                       pm.spheres_w, (float*)pm.verts_w, (float*)pm.hscale_w);
+                       pm.spheres_w, (float*)pm.verts_w, (float*)pm.hscale_w, (float*)nullptr);
   }
   return hipGetLastError();
 }
@@ -1128,6 +1340,7 @@ static PassModel<T> pass_model(const LocalModel& lm, const PosedModel& pm) {
   m.verts = (const T*)pm.verts_w;
   m.hscale = (const T*)pm.hscale_w;
   m.spheres = pm.spheres_w;
+  m.screen = pm.screen_w;
   return m;
 }
 
@@ -1158,9 +1371,19 @@ static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void
   else launch_lds(pass_kernel<T, 4, CULL, RBF>, nblocks, lds, s, pts, n, m, out);
 }
 
+// FSDF_BENCH_ONLY=1: A/B timing builds instantiate only the bench variant
+// (f64, culled, hulls only, <= 64 surfaces); every other pass is refused.
+#ifndef FSDF_BENCH_ONLY
+#define FSDF_BENCH_ONLY 0
+#endif
+
 template <typename T>
 static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm, const void* d_pts, int64_t n,
                           int nblocks, const PassOutputs& out, hipStream_t s) {
+#if FSDF_BENCH_ONLY
+  const PassModel<T> m = pass_model<T>(lm, pm);
+  launch_lds(pass_kernel<T, 1, true, false>, nblocks, pass_lds_bytes(lm, false), s, (const T*)d_pts, n, m, out);
+#else
   if (lm.R > 0) {
     if (cull) launch_pass_t<T, true, true>(lm, pm, d_pts, n, nblocks, out, s);
     else launch_pass_t<T, false, true>(lm, pm, d_pts, n, nblocks, out, s);
@@ -1168,12 +1391,18 @@ static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm,
     if (cull) launch_pass_t<T, true, false>(lm, pm, d_pts, n, nblocks, out, s);
     else launch_pass_t<T, false, false>(lm, pm, d_pts, n, nblocks, out, s);
   }
+#endif
 }
 
 hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const void* d_pts,
                        int64_t n, int nblocks, const PassOutputs& out, hipStream_t s) {
+#if FSDF_BENCH_ONLY
+  if (precision != 64 || !cull || lm.R > 0 || lm.S > 64) return hipErrorNotSupported;
+  launch_pass_p<double>(cull, lm, pm, d_pts, n, nblocks, out, s);
+#else
   if (precision == 64) launch_pass_p<double>(cull, lm, pm, d_pts, n, nblocks, out, s);
   else launch_pass_p<float>(cull, lm, pm, d_pts, n, nblocks, out, s);
+#endif
   return hipGetLastError();
 }
 
@@ -1204,8 +1433,12 @@ static void launch_raycast_p(bool cull, const LocalModel& lm, const PosedModel& 
 hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const double* origin,
                           const double* d_rays, int64_t n, double* d_depth, hipStream_t s) {
   if (n <= 0) return hipSuccess;
+#if FSDF_BENCH_ONLY
+  return hipErrorNotSupported;
+#else
   if (precision == 64) launch_raycast_p<double>(cull, lm, pm, origin, d_rays, n, d_depth, s);
   else launch_raycast_p<float>(cull, lm, pm, origin, d_rays, n, d_depth, s);
+#endif
   return hipGetLastError();
 }
 

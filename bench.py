@@ -54,32 +54,51 @@ def parse():
                    help="input order of the synthetic cloud (shuffled = adversarial)")
     p.add_argument("--no-sort", action="store_true", help="keep the input order resident (no Morton sort)")
     p.add_argument("--no-per-point", action="store_true", help="reduction-only pass (no per-point outputs)")
-    p.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of the CPU baseline leg")
+    p.add_argument("--cpu-seconds", type=float, default=4.0, help="target wall time of the CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--seed", type=int, default=1234)
     return p.parse_args()
 
 
 def cpu_baseline(manip, pts, q_eval, target_s):
-    """Oracle (test infrastructure, the checker/baseline only) on a bounded sample."""
+    """Oracle (test infrastructure, the checker/baseline only) on a bounded
+    sample: SURVEY.md §8d — all host threads (the box's OpenMP share) and one
+    thread, median of timed runs after a warm-up, CPU model recorded."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import statistics
     import flash
     import oracle
     om = oracle.OracleModel.from_manipulator(manip)
     poses = flash.hull_poses(manip, q_eval)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, os.cpu_count() or 1))
-    n = 2048
-    t = time.perf_counter()
-    om.skin(poses, pts[:n], threads=threads)
-    dt = time.perf_counter() - t
-    n = int(min(len(pts), max(n, n * target_s / max(dt, 1e-6))))
-    t = time.perf_counter()
-    om.skin(poses, pts[:n], threads=threads)
-    dt = time.perf_counter() - t
-    return {"value": n / dt, "unit": "point-evals/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} points of rank 0's cloud, M64 brute force over all 64 hulls "
-                      f"(reference loop order), {dt:.2f} s wall on {threads} threads"}
+
+    def rate(nt, per_run_s, runs):
+        n = 1024
+        t = time.perf_counter()
+        om.skin(poses, pts[:n], threads=nt)  # warm-up + sizing
+        dt = time.perf_counter() - t
+        n = int(min(len(pts), max(n, n * per_run_s / max(dt, 1e-6))))
+        ts = []
+        for _ in range(runs):
+            t = time.perf_counter()
+            om.skin(poses, pts[:n], threads=nt)
+            ts.append(time.perf_counter() - t)
+        return n, statistics.median(ts), sum(ts)
+
+    n, med, tot = rate(threads, target_s / 5, 5)
+    n1, med1, tot1 = rate(1, 1.0, 3)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    return {"value": n / med, "unit": "point-evals/s", "cores": threads, "kind": "port",
+            "single_thread_value": n1 / med1,
+            "sample": f"first {n} points of rank 0's cloud, M64 brute force over all 64 hulls (the reference's "
+                      f"loop), median of 5 runs ({tot:.1f} s wall, ~{tot * threads:.0f} CPU-s) on {threads} "
+                      f"threads; 1 thread: {n1} points, median of 3; host CPU: {model}"}
 
 
 def main():

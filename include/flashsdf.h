@@ -183,12 +183,15 @@ int fsdf_pass_time(fsdf_ctx* ctx, double* total_ms_out, int64_t* launches_out);
  *   [0] wave-iterations (64 points each)  [1] hull evaluations (per wave)
  *   [2] slow-path entries (per wave)      [3] lane-needs summed over evaluations
  *   [4] lanes on the slow path            [5] best-first seed evaluations
- *   [6] waves reaching stage B (neighbours) [7] lanes in the exhaustive scan
+ *   [6] waves reaching the exhaustive scan [7] lanes in the exhaustive scan
  *   [8] candidate hulls after wave culling [9] faces of the evaluated hulls
  *   [10..18] shader-clock cycles per phase (culling, hull staging, plane max,
  *   fast path, closest-feature search, whole wave-iteration, segmented
  *   reduction, per-point stores, scene evaluation) — only in diagnostic
- *   builds (-DFSDF_PHASE_TIMING=1), zero otherwise. 19 counters. */
+ *   builds (-DFSDF_PHASE_TIMING=1), zero otherwise.
+ *   [19] screened plane maxima that fell back to the full fp64 scan (per
+ *   wave) [20] evaluations rejected early by the screen [21] descent-walk
+ *   steps (per wave). 22 counters. */
 int fsdf_kernel_stats(fsdf_ctx* ctx, int32_t enable, uint64_t* counters_out);
 
 #ifdef __cplusplus

@@ -735,7 +735,7 @@ extern "C" int fsdf_pass_time(fsdf_ctx* c, double* total_ms, int64_t* launches) 
   return FSDF_OK;
 }
 
-static constexpr int kStatCount = 19;
+static constexpr int kStatCount = 22;
 
 extern "C" int fsdf_kernel_stats(fsdf_ctx* c, int32_t enable, uint64_t* counters) {
   if (!c) return FSDF_ERR_ARG;

@@ -35,7 +35,10 @@ namespace fsdf {
 constexpr int kBlock = 256;        // 4 waves of 64
 constexpr int kMaxLds = 163840;    // LDS a workgroup may declare (gfx950)
 constexpr int kMaxHulls = 256;     // 4 accumulator slots per lane
-constexpr int kMaxBlocks = 2048;
+#ifndef FSDF_MAX_BLOCKS
+#define FSDF_MAX_BLOCKS 16384
+#endif
+constexpr int kMaxBlocks = FSDF_MAX_BLOCKS;  // pass grid cap (grid-stride beyond)
 constexpr int kMaxRbfAccum = 512;  // Σ (4n+4) over RBF skins (= kMaxRbfAcc in the kernel)
 
 struct LocalModel {

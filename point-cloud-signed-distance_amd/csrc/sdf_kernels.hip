@@ -379,7 +379,7 @@ __device__ __forceinline__ void stage_hull(T* __restrict__ lw, const T* __restri
 // VALU takes as a broadcast operand — no LDS bandwidth (the plane max was
 // LDS-bound: two broadcast ds_read_b128 per face and wave, 4 waves per LDS).
 #ifndef FSDF_SCALAR_PLANES
-#define FSDF_SCALAR_PLANES 1
+#define FSDF_SCALAR_PLANES 0
 #endif
 template <typename T>
 using CRow = const __attribute__((address_space(4))) typename Row4<T>::type*;
@@ -498,7 +498,7 @@ template <typename T>
 __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0, int nf, const PassModel<T>& m,
                                                  const HullRow* __restrict__ ht,
                                                  const typename Row4<T>::type* __restrict__ lp, bool active,
-                                                 T& hA, int& iA) {
+                                                 T bound, T& hA, int& iA, bool& rejected) {
   const F4 sp = ht[k].sphere;
   const float qx = (float)(px - (T)sp[0]), qy = (float)(py - (T)sp[1]), qz = (float)(pz - (T)sp[2]);
   // 2E, plus an absolute term for the fp64 rounding of h_f itself (~1e-15 |p|)
@@ -523,9 +523,19 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
     b2 = fmaxf(b2, fminf(b1, mb));
     if (mb > b1) { b1 = mb; ib = i; }
   };
+  // Early rejection: h_max >= b1 − E, so once b1 − E exceeds a lane's best
+  // distance the hull can neither win nor tie for it (d >= h_max). When that
+  // holds for every lane that needs the hull, the scan stops (d = +inf).
+  const float bf = (float)bound;
+  const float thr = bf + E2 + 2.5e-7f * fabsf(bf);
+  rejected = false;
   int i0 = 0;
-  for (; i0 + 4 <= np; i0 += 4) batch(i0, false);
+  for (; i0 + 4 <= np; i0 += 4) {
+    batch(i0, false);
+    if (!__any(active && !(b1 > thr))) { rejected = true; return true; }
+  }
   if (i0 < np) batch(i0, true);
+  if (!__any(active && !(b1 > thr))) { rejected = true; return true; }
   // exact fp64 first-index argmax over the best batch's faces
   const int fb = 2 * ib;
   hA = -tinf<T>();
@@ -563,6 +573,7 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   const int v0 = __builtin_amdgcn_readfirstlane(ht[k].v0);
   const int nv = __builtin_amdgcn_readfirstlane(ht[k + 1].v0) - v0;
   uint64_t tp = phase_clock();
+  if (FSDF_ABLATE & 65536) stage_hull(lw, m.planes + 4 * f0, m.verts + 4 * v0, m.face_rows + f0, nf, nv);  // 2x (marginal cost)
   stage_hull(lw, m.planes + 4 * f0, m.verts + 4 * v0, m.face_rows + f0, nf, nv);
   phase_add(stats, 11, tp);
   tp = phase_clock();
@@ -585,7 +596,19 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   bool screened = (FSDF_ABLATE & 128) != 0;  // ablation: no plane max (face 0)
   if (screened) hA = plane_h<T>(lp[0], px, py, pz);
   if constexpr (sizeof(T) == 8) {
-    if (FSDF_SCREEN32 && !screened) screened = screen_plane_max(px, py, pz, k, f0, nf, m, ht, lp, active, hA, iA);
+    bool rejected = false;
+    if (FSDF_SCREEN32 && !screened)
+      screened = screen_plane_max(px, py, pz, k, f0, nf, m, ht, lp, active, bound, hA, iA, rejected);
+    if (count_events(stats) && lane_id() == 0) {
+      if (rejected) atomicAdd(stats + 20, 1ull);
+      else if (!screened) atomicAdd(stats + 19, 1ull);
+    }
+    if (rejected) {  // cannot win nor tie for any lane that needs it
+      d = tinf<T>();
+      gx = gy = gz = (T)0;
+      phase_add(stats, 12, tp);
+      return;
+    }
   }
   if (!screened) {
   hA = -tinf<T>();
@@ -666,6 +689,7 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   int cf = fs, cr = rA;
   bool walking = todo;
   for (int step = 0; step < kWalkSteps && __any(walking); ++step) {
+    if (count_events(stats) && lane_id() == 0) atomicAdd(stats + 21, 1ull);
     if (walking) {
       int n1, n2;
       if (cert_step<T>(px, py, pz, cf, cr, lp, lv, lf, scale, n1, n2)) {

@@ -254,8 +254,9 @@ class Context:
         return ms.value, n.value
 
     STAT_NAMES = ("wave_iters", "hull_evals", "slow_waves", "lane_needs", "slow_lanes", "seed_evals",
-                  "stageB_waves", "full_scan_lanes", "wave_candidates", "faces_evaluated", "cyc_cull", "cyc_stage",
-                  "cyc_plane", "cyc_fast", "cyc_slow", "cyc_iter", "cyc_reduce", "cyc_store", "cyc_scene")
+                  "scan_waves", "full_scan_lanes", "wave_candidates", "faces_evaluated", "cyc_cull", "cyc_stage",
+                  "cyc_plane", "cyc_fast", "cyc_slow", "cyc_iter", "cyc_reduce", "cyc_store", "cyc_scene",
+                  "screen_fallbacks", "screen_rejects", "walk_steps")
 
     def kernel_stats(self, enable: bool):
         """enable=True: start counting; enable=False: stop, return the counters."""

@@ -146,11 +146,28 @@ class ManipulatorState:
         self.q[:] = q
 
 
+def _posed(manip: Manipulator, q: np.ndarray, surfaces) -> np.ndarray:
+    """[n,12] T_world_body · T_body_geometry for the given convex surfaces (batched)."""
+    if not surfaces:
+        return np.zeros((0, 12))
+    R, t, _, _ = manip.mechanism.body_transform_arrays(q)
+    key = tuple(id(s) for s in surfaces)
+    cache = getattr(manip, "_frame_cache", None)
+    if cache is None or cache[0] != key:
+        cache = (key, np.array([s.body for s in surfaces]), np.stack([s.frame.R for s in surfaces]),
+                 np.stack([s.frame.t for s in surfaces])[:, :, None])
+        manip._frame_cache = cache
+    _, b, FR, Ft = cache
+    out = np.empty((len(surfaces), 12))
+    out[:, :9] = (R[b] @ FR).reshape(-1, 9)
+    out[:, 9:] = (R[b] @ Ft)[:, :, 0] + t[b]
+    return out
+
+
 def hull_poses(manip: Manipulator, q: np.ndarray) -> np.ndarray:
     """[K,12] world poses of the convex surfaces: transform_to_root(state, frame)
     (src/Flash.jl:248) = T_world_body · T_body_geometry."""
-    T = manip.mechanism.body_transforms(q)
-    return np.stack([(T[s.body] @ s.frame).as_pose12() for s in manip.convex_surfaces()])
+    return _posed(manip, q, manip.convex_surfaces())
 
 
 _IDENTITY12 = np.concatenate([np.eye(3).ravel(), np.zeros(3)])
@@ -159,9 +176,10 @@ _IDENTITY12 = np.concatenate([np.eye(3).ravel(), np.zeros(3)])
 def surface_poses(manip: Manipulator, q: np.ndarray) -> np.ndarray:
     """[S,12] one pose per surface in surface order (identity for RBF skins,
     whose centres travel separately)."""
-    T = manip.mechanism.body_transforms(q)
-    return np.stack([(T[s.body] @ s.frame).as_pose12() if isinstance(s, ConvexGeometry) else _IDENTITY12
-                     for s in manip.surfaces])
+    out = np.tile(_IDENTITY12, (len(manip.surfaces), 1))
+    idx = [i for i, s in enumerate(manip.surfaces) if isinstance(s, ConvexGeometry)]
+    out[idx] = _posed(manip, q, [manip.surfaces[i] for i in idx])
+    return out
 
 
 def prepare_pass(ctx, manip: Manipulator, q_normalized: np.ndarray, deformation_data: np.ndarray):

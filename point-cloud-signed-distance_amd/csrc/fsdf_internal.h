@@ -32,6 +32,13 @@
 
 namespace fsdf {
 
+// fp32-screened plane max in f64 contexts (sdf_kernels.hip screen_plane_max);
+// it also fixes the f64 LDS stage layout (screening pairs instead of planes),
+// so fsdf_set_surfaces sizes the stage from the same switch.
+#ifndef FSDF_SCREEN32
+#define FSDF_SCREEN32 1
+#endif
+
 constexpr int kBlock = 256;        // 4 waves of 64
 constexpr int kMaxLds = 163840;    // LDS a workgroup may declare (gfx950)
 constexpr int kMaxHulls = 256;     // 4 accumulator slots per lane

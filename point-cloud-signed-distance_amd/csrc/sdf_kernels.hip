@@ -341,19 +341,14 @@ __device__ __forceinline__ void stage_rows(T* __restrict__ lds, const T* __restr
 #ifndef FSDF_PLANE_BATCH
 #define FSDF_PLANE_BATCH 8
 #endif
-constexpr int kPlaneBatch = FSDF_PLANE_BATCH;
-constexpr int kWalkSteps = 24;  // descent-walk cap before the exhaustive stage C  // plane rows per LDS batch (power of 2, >= 2)
+constexpr int kPlaneBatch = FSDF_PLANE_BATCH;  // plane rows per LDS batch (power of 2, >= 2)
+constexpr int kWalkSteps = 24;  // descent-walk cap before the exhaustive stage C
 
-template <typename T>
-__device__ __forceinline__ void stage_hull(T* __restrict__ lw, const T* __restrict__ planes,
-                                           const T* __restrict__ verts, const I4* __restrict__ frows, int nf,
-                                           int nv) {
-  typedef typename Row4<T>::type R;
-  constexpr int cpr = (int)sizeof(T) / 4;  // 16-byte chunks per row of 4 T
-  const int P = nf * cpr, Q = P + nv * cpr, N = Q + nf;
+// Three consecutive regions of 16-byte chunks: n0 from s0, n1 from s1, n2 from s2.
+__device__ __forceinline__ void stage_hull(void* __restrict__ lw, const I4* __restrict__ s0, int n0,
+                                           const I4* __restrict__ s1, int n1, const I4* __restrict__ s2, int n2) {
+  const int P = n0, Q = P + n1, N = Q + n2;
   const int lane = threadIdx.x & 63;
-  const I4* sp = (const I4*)planes;
-  const I4* sv = (const I4*)verts;
   I4* dst = (I4*)lw;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   for (int c0 = 0; c0 < N; c0 += 8 * 64) {
@@ -361,7 +356,7 @@ __device__ __forceinline__ void stage_hull(T* __restrict__ lw, const T* __restri
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = min(c0 + 64 * j + lane, N - 1);
-      const I4* src = c < P ? sp + c : (c < Q ? sv + (c - P) : frows + (c - Q));
+      const I4* src = c < P ? s0 + c : (c < Q ? s1 + (c - P) : s2 + (c - Q));
       if (!(FSDF_ABLATE & 64)) v[j] = *src;
       else v[j] = I4{c, c, c, 0};
     }
@@ -487,16 +482,17 @@ __device__ __forceinline__ bool cert_step(T px, T py, T pz, int f, int reg,
 //   margin (near-ties across batches) return false and take the full scan.
 // Returns true iff the result is final for every lane that needs it.
 // ---------------------------------------------------------------------------
-#ifndef FSDF_SCREEN32
-#define FSDF_SCREEN32 1
+template <typename T>
+constexpr bool kStagePairs = sizeof(T) == 8 && FSDF_SCREEN32;
+#ifndef FSDF_SCREEN_ILP
+#define FSDF_SCREEN_ILP 4
 #endif
+constexpr int kScreenIlp = FSDF_SCREEN_ILP;  // independent 8-face batches per loop iteration  // see hull_sdf / fsdf_internal.h
 typedef float F2v __attribute__((ext_vector_type(2)));
-typedef float F8v __attribute__((ext_vector_type(8)));
-typedef const __attribute__((address_space(4))) F8v* CF8;
 
 template <typename T>
 __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0, int nf, const PassModel<T>& m,
-                                                 const HullRow* __restrict__ ht,
+                                                 const HullRow* __restrict__ ht, const void* __restrict__ lw,
                                                  const typename Row4<T>::type* __restrict__ lp, bool active,
                                                  T bound, T& hA, int& iA, bool& rejected) {
   const F4 sp = ht[k].sphere;
@@ -505,21 +501,30 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
   const float E2 = 32.0f * 5.9604645e-8f * (((fabsf(qx) + fabsf(qy)) + fabsf(qz)) + sp[3]) * 1.0001f +
                    1e-12f * (1.0f + fabsf((float)px) + fabsf((float)py) + fabsf((float)pz) + sp[3]);
   const F2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
-  const CF8 gs = (CF8)(m.screen + 4 * (f0 + k));
+  const F4* ls = (const F4*)lw;  // staged pairs: two 16-byte chunks each
   const int np = (nf + 1) >> 1;
   float b1 = -__builtin_huge_valf(), b2 = -__builtin_huge_valf();
   int ib = 0;
-  auto batch = [&](int i, bool tail) {
-    F8v c[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) c[q] = gs[tail ? min(i + q, np - 1) : i + q];
-    float mb = -__builtin_huge_valf();
+  // maximum of the 8 faces in pairs i..i+3 (tail: indices clamped to the last pair)
+  auto batch_max = [&](int i, bool tail) -> float {
+    F4 c[8];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const F2v nx = {c[q][0], c[q][1]}, ny = {c[q][2], c[q][3]}, nz = {c[q][4], c[q][5]}, nd = {c[q][6], c[q][7]};
-      const F2v h = __builtin_elementwise_fma(nx, qx2, __builtin_elementwise_fma(ny, qy2, __builtin_elementwise_fma(nz, qz2, nd)));
-      mb = fmaxf(mb, fmaxf(h[0], h[1]));
+      const int j = tail ? min(i + q, np - 1) : i + q;
+      c[2 * q] = ls[2 * j];
+      c[2 * q + 1] = ls[2 * j + 1];
     }
+    float hm[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const F4 u = c[2 * q], w = c[2 * q + 1];
+      const F2v nx = {u[0], u[1]}, ny = {u[2], u[3]}, nz = {w[0], w[1]}, nd = {w[2], w[3]};
+      const F2v h = __builtin_elementwise_fma(nx, qx2, __builtin_elementwise_fma(ny, qy2, __builtin_elementwise_fma(nz, qz2, nd)));
+      hm[q] = fmaxf(h[0], h[1]);
+    }
+    return fmaxf(fmaxf(hm[0], hm[1]), fmaxf(hm[2], hm[3]));
+  };
+  auto update = [&](float mb, int i) {
     b2 = fmaxf(b2, fminf(b1, mb));
     if (mb > b1) { b1 = mb; ib = i; }
   };
@@ -530,11 +535,16 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
   const float thr = bf + E2 + 2.5e-7f * fabsf(bf);
   rejected = false;
   int i0 = 0;
-  for (; i0 + 4 <= np; i0 += 4) {
-    batch(i0, false);
+  // two independent batches per iteration (ILP); rejection tested once per pair
+  for (; i0 + 4 * kScreenIlp <= np; i0 += 4 * kScreenIlp) {
+    float mx[kScreenIlp];
+#pragma unroll
+    for (int u = 0; u < kScreenIlp; ++u) mx[u] = batch_max(i0 + 4 * u, false);
+#pragma unroll
+    for (int u = 0; u < kScreenIlp; ++u) update(mx[u], i0 + 4 * u);
     if (!__any(active && !(b1 > thr))) { rejected = true; return true; }
   }
-  if (i0 < np) batch(i0, true);
+  for (; i0 < np; i0 += 4) update(batch_max(i0, i0 + 4 > np), i0);
   if (!__any(active && !(b1 > thr))) { rejected = true; return true; }
   // exact fp64 first-index argmax over the best batch's faces
   const int fb = 2 * ib;
@@ -573,12 +583,19 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   const int v0 = __builtin_amdgcn_readfirstlane(ht[k].v0);
   const int nv = __builtin_amdgcn_readfirstlane(ht[k + 1].v0) - v0;
   uint64_t tp = phase_clock();
-  if (FSDF_ABLATE & 65536) stage_hull(lw, m.planes + 4 * f0, m.verts + 4 * v0, m.face_rows + f0, nf, nv);  // 2x (marginal cost)
-  stage_hull(lw, m.planes + 4 * f0, m.verts + 4 * v0, m.face_rows + f0, nf, nv);
+  // Stage layout: f64 contexts stage the fp32 screening pairs (16 B per face)
+  // and read the fp64 planes — needed per lane only for the batch fix-up, the
+  // max face and the certificates — from global memory (L1/L2); f32 contexts
+  // stage the planes themselves. Then vertex rows and packed face rows.
+  constexpr int cpr = (int)sizeof(T) / 4;  // 16-byte chunks per row of 4 T
+  const int np2 = kStagePairs<T> ? 2 * ((nf + 1) >> 1) : nf * cpr;  // chunks of region 0
+  const I4* src0 = kStagePairs<T> ? (const I4*)(m.screen + 4 * (f0 + k)) : (const I4*)(m.planes + 4 * f0);
+  for (int rep = (FSDF_ABLATE & 65536) ? 2 : 1; rep > 0; --rep)  // (2x: marginal-cost ablation)
+    stage_hull(lw, src0, np2, (const I4*)(m.verts + 4 * v0), nv * cpr, m.face_rows + f0, nf);
   phase_add(stats, 11, tp);
   tp = phase_clock();
-  const R* lp = (const R*)lw;
-  const R* lv = lp + nf;
+  const R* lp = kStagePairs<T> ? (const R*)(m.planes + 4 * f0) : (const R*)lw;
+  const R* lv = (const R*)((const I4*)lw + np2);
   const I4* lf = (const I4*)(lv + nv);
   const T scale = (T)ht[k].hscale;
   const CRow<T> gp = scalar_rows<T>(m.planes + 4 * f0);  // uniform plane rows (SGPR)
@@ -598,7 +615,12 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   if constexpr (sizeof(T) == 8) {
     bool rejected = false;
     if (FSDF_SCREEN32 && !screened)
-      screened = screen_plane_max(px, py, pz, k, f0, nf, m, ht, lp, active, bound, hA, iA, rejected);
+      screened = screen_plane_max(px, py, pz, k, f0, nf, m, ht, lw, lp, active, bound, hA, iA, rejected);
+    if (FSDF_ABLATE & 131072) {  // 2x screen (marginal cost; identical result)
+      T h2; int i2; bool r2;
+      const bool s2 = screen_plane_max(px + (T)0 * hA, py, pz, k, f0, nf, m, ht, lw, lp, active, bound, h2, i2, r2);
+      screened = screened && s2; rejected = rejected && r2;
+    }
     if (count_events(stats) && lane_id() == 0) {
       if (rejected) atomicAdd(stats + 20, 1ull);
       else if (!screened) atomicAdd(stats + 19, 1ull);

@@ -54,7 +54,7 @@ def parse():
                    help="input order of the synthetic cloud (shuffled = adversarial)")
     p.add_argument("--no-sort", action="store_true", help="keep the input order resident (no Morton sort)")
     p.add_argument("--no-per-point", action="store_true", help="reduction-only pass (no per-point outputs)")
-    p.add_argument("--cpu-seconds", type=float, default=4.0, help="target wall time of the CPU baseline leg")
+    p.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of the CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--seed", type=int, default=1234)
     return p.parse_args()

@@ -11,16 +11,19 @@
 //  termination-simplex estimate and is replaced by the exact one — DESIGN.md §2).
 //
 // Kernel design:
-//   * one lane per point; each wave owns 64 consecutive resident points;
-//   * the posed model is read with wave-uniform (scalar) loads: every lane of a
-//     wave walks the same face list, so plane data is broadcast, never gathered;
-//   * exact-safe culling: a hull is skipped by a lane when the bounding-sphere
-//     lower bound |p−c_k|−r_k exceeds min(centroid upper bound, best so far) by a
-//     rounding margin; a wave evaluates hull k iff any lane needs it;
+//   * one lane per point; each wave owns 64 consecutive (Morton-ordered)
+//     resident points;
+//   * exact-safe culling: hulls are dropped for the whole wave from its
+//     bounding sphere, then per lane by |p−c_k|−r_k against min(upper bound,
+//     best so far) plus a rounding margin; a wave evaluates hull k iff any
+//     lane needs it, each lane's best-first seed first;
+//   * a hull evaluation stages the hull once into the wave's LDS stage; the
+//     plane max is an fp32 screen (packed FMA, two faces per instruction) with
+//     an exact fp64 fix-up, and the closest feature a certified descent walk;
 //   * per-hull wrench sums are segmented by k* inside the wave (ballot loop +
-//     xor-shuffle tree), owned in registers by lane k mod 64, combined per block
-//     in LDS in fixed wave order, then reduced over blocks in fixed order: the
-//     whole reduction is deterministic for a given (n, grid).
+//     DPP sums), owned in LDS rows by lane k mod 64, combined per block in
+//     fixed wave order, then reduced over blocks in fixed order: the whole
+//     reduction is deterministic for a given (n, grid).
 //
 // All arithmetic is written with explicit fma() and compiled with
 // -ffp-contract=off so that oracle/flash_oracle.c reproduces every per-hull
@@ -562,12 +565,12 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
 
 // ---------------------------------------------------------------------------
 // Exact signed distance of p to posed hull k, with its unit gradient.
-//   inside / on the surface: max_f h_f, gradient n_{f*} (first max face);
+//   inside / on the surface: max_f h_f, gradient n_{f*} (first max face; f64
+//     contexts find it with the fp32 screen above);
 //   outside: if the projection on f* lies in triangle f*, d = h_{f*};
-//     otherwise the closest point is searched locally (triangle f*, then the
-//     neighbours across its violated edges), certified optimal by the support
-//     test over the hull's vertices, and only uncertified lanes fall back to the
-//     exhaustive scan of the visible faces.
+//     otherwise the closest point on triangle f* and a descent walk certified
+//     by the hull's normal cone at the closest feature (cert_step); a stalled
+//     walk falls back to the exhaustive scan of the visible faces.
 // `active`: this lane's result is used (gates the wave-uniform slow branches).
 // `bound`: the lane's best distance so far (only a result below it matters).
 // `lw`: this wave's LDS stage (m.stage_bytes). Whole wave active.

@@ -162,3 +162,27 @@ def test_rbf_skin_with_many_centres(oracle_mod):
         assert np.array_equal(d, od), np.abs(d - od).max()
         assert np.array_equal(g, og), np.abs(g - og).max()
         assert np.allclose(acc, oacc, rtol=1e-9, atol=1e-9 * np.abs(oacc).max())
+
+
+def test_cone_fallback_paths(oracle_mod):
+    """An apex of valence 48 (the descent walk's fan test stops at 32 faces, so
+    those lanes take the exhaustive scan) over a coplanar triangulated base (fp32
+    screen near-ties across batches -> the full fp64 scan): bit for bit vs the
+    oracle, and the kernel counters show both fallbacks ran."""
+    from flash import _lib
+    from test_oracle import _cone_cloud, _cone_hull
+    hull = _cone_hull()
+    r = rng(714)
+    poses = np.array([[1.0, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0], [1.0, 0, 0, 0, 1, 0, 0, 0, 1, 0.4, 0, 0]])
+    pts = np.vstack([_cone_cloud(r, 3000), _cone_cloud(r, 3000) + [0.4, 0, 0]])
+    _parity([hull, hull], poses, pts, oracle_mod)
+    c = _lib.Context(device=0)
+    try:
+        c.set_model([hull, hull])
+        c.set_points(pts)
+        c.kernel_stats(True)
+        c.eval(poses)
+        st = c.kernel_stats(False)
+    finally:
+        c.close()
+    assert st["full_scan_lanes"] > 0 and st["screen_fallbacks"] > 0 and st["walk_steps"] > 0, st

@@ -104,3 +104,36 @@ def test_oracle_reproduces_golden(name, oracle_mod):
     acc = om.cost_accum(poses, z["points"])
     assert np.allclose(acc, z["accum"], rtol=1e-13, atol=1e-13)
     assert acc[0] == pytest.approx(np.dot(d, d), rel=1e-12)
+
+
+def _cone_hull(n=48, radius=0.08, height=0.12):
+    """n-gon base (its triangulation is coplanar) + apex of valence n > 32."""
+    from flash import _lib
+    a = 2 * np.pi * np.arange(n) / n
+    pts = np.vstack([np.stack([radius * np.cos(a), radius * np.sin(a), np.zeros(n)], 1), [[0.0, 0.0, height]]])
+    return _lib.convex_hull(pts)
+
+
+def _cone_cloud(r, n):
+    """points over the apex (its normal cone: the walk's fan test exceeds 32
+    faces), above and below the coplanar base facets, and around."""
+    apex = np.array([0.0, 0.0, 0.12])
+    up = apex + np.abs(r.normal(size=(n // 3, 3))) * [0.01, 0.01, 0.05] * r.choice([-1, 1], size=(n // 3, 3)) * [1, 1, 0] \
+        + [0, 0, 0.02]
+    base = np.stack([r.uniform(-0.07, 0.07, n // 3), r.uniform(-0.07, 0.07, n // 3), r.normal(scale=0.01, size=n // 3)], 1)
+    rest = r.normal(size=(n - 2 * (n // 3), 3)) * 0.1
+    return np.vstack([up, base, rest])
+
+
+def test_oracle_matches_numpy_on_high_valence_cone(oracle_mod):
+    """The descent walk's fallbacks (fan > 32 faces -> exhaustive scan) and the
+    coplanar base still give the exact distance (independent numpy, 1e-12)."""
+    v, f, p = _cone_hull()
+    assert len(f) >= 90
+    om = oracle_mod.OracleModel([(v, f, p)])
+    pose = np.array([[1.0, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0]])
+    pts = _cone_cloud(rng(31), 3000)
+    d, k, g = om.skin(pose, pts)
+    ref = oracle_mod.numpy_hull_sdf(*om.world_hull(pose, 0), pts)
+    assert np.abs(d - ref).max() < 1e-12
+    assert np.allclose(np.linalg.norm(g, axis=1), 1.0, atol=1e-12)

@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <map>
 #include <utility>
 #include <string>
@@ -335,7 +336,14 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
       std::map<std::pair<int, int>, int> owner;
       for (int f = 0; f < h.n_faces; ++f)
         for (int e = 0; e < 3; ++e) owner[{h.faces[3 * f + e], h.faces[3 * f + (e + 1) % 3]}] = f;
+      // exact duplicate planes (coplanar triangles of one facet): a later face
+      // with the bitwise plane of an earlier one can never be the first-index
+      // maximum, so the fp32 screen leaves it out (no near-tie fallbacks)
+      std::map<std::array<uint64_t, 4>, int> seen_plane;
       for (int f = 0; f < h.n_faces; ++f) {
+        std::array<uint64_t, 4> key;
+        memcpy(key.data(), planes.data() + planes.size() - 4 * (size_t)(h.n_faces - f), sizeof(key));
+        const bool dup = !seen_plane.emplace(key, f).second;
         int nb[3];
         for (int e = 0; e < 3; ++e) {
           auto it = owner.find({h.faces[3 * f + (e + 1) % 3], h.faces[3 * f + e]});
@@ -345,7 +353,7 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
         face_rows.push_back((int32_t)((uint32_t)fv[0] | ((uint32_t)fv[1] << 16)));
         face_rows.push_back((int32_t)((uint32_t)fv[2] | ((uint32_t)nb[0] << 16)));
         face_rows.push_back((int32_t)((uint32_t)nb[1] | ((uint32_t)nb[2] << 16)));
-        face_rows.push_back(0);
+        face_rows.push_back(dup ? 1 : 0);
       }
       // per-wave LDS stage: plane rows (f64 contexts: the fp32 screening
       // pairs, 32 B per two faces) and vertex rows of 4 T, one 16-byte face row

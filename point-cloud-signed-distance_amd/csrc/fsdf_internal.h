@@ -11,8 +11,9 @@
 //     face_off  [K+1]   i32     faces of hull k are [face_off[k], face_off[k+1])
 //     vert_hull [V]     i32     owning hull of each vertex
 //     vert_off  [K+1]   i32     vertices of hull k are [vert_off[k], vert_off[k+1])
-//     face_rows [F][4]  i32     packed hull-local (v0|v1<<16, v2|n0<<16, n1|n2<<16, 0):
-//                               vertex indices and the face across edge i (v_i -> v_{i+1})
+//     face_rows [F][4]  i32     packed hull-local (v0|v1<<16, v2|n0<<16, n1|n2<<16, dup):
+//                               vertex indices, the face across edge i (v_i -> v_{i+1}),
+//                               dup = 1 if an earlier face of the hull has the same plane
 //
 //   posed model (rewritten by every evaluation; T = double or float)
 //     planes_w  [F][4]  T       world plane

@@ -97,7 +97,11 @@ __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const doubl
       const double c0 = (double)(float)cw[0], c1 = (double)(float)cw[1], c2 = (double)(float)cw[2];
       const double dc = dw - __builtin_fma(nw[0], c0, __builtin_fma(nw[1], c1, nw[2] * c2));
       float* pair = screen_w + 4 * (lm.face_off[h] + h + (j & ~1));
-      const float v[4] = {(float)nw[0], (float)nw[1], (float)nw[2], (float)(-dc)};
+      // an exact duplicate of an earlier face's plane (face row word 3) is
+      // screened out: h = -1e30, never a maximum nor a near-tie
+      const bool dup = lm.face_rows[4 * f + 3] != 0;
+      const float v[4] = {dup ? 0.0f : (float)nw[0], dup ? 0.0f : (float)nw[1], dup ? 0.0f : (float)nw[2],
+                          dup ? -1e30f : (float)(-dc)};
 #pragma unroll
       for (int c = 0; c < 4; ++c) pair[2 * c + (j & 1)] = v[c];
       if ((nf & 1) && j == nf - 1)  // odd count: the last pair repeats its face

@@ -582,6 +582,7 @@ static int ensure_partials(fsdf_ctx* c, int nblocks) {
 static int upload_poses(fsdf_ctx* c, const double* poses) {
   for (int i = 0; i < 12 * c->lm.S; ++i)
     if (!std::isfinite(poses[i])) return fail(c, FSDF_ERR_ARG, "poses: entry %d is not finite", i);
+  if (c->lm.S <= fsdf::kPoseArgMax) return FSDF_OK;  // they ride in the pose kernel's arguments
   const int s = c->pose_slot;
   c->pose_slot = (s + 1) % kPoseRing;
   HIPCHECK(c, hipEventSynchronize(c->pose_ev[s]));  // slot free once its last copy ran
@@ -598,7 +599,8 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
     return fail(c, FSDF_ERR_STATE, "eval: the scene has RBF surfaces: call fsdf_set_rbf_params first");
   int rc = upload_poses(c, poses);
   if (rc) return rc;
-  HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, c->d_poses, c->pm, c->stream));
+  HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, c->d_poses, c->pm, c->stream,
+                                c->lm.S <= fsdf::kPoseArgMax ? poses : nullptr));
   const int nblocks = fsdf::pass_blocks(n);
   rc = ensure_partials(c, nblocks);
   if (rc) return rc;
@@ -785,7 +787,8 @@ extern "C" int fsdf_raycast(fsdf_ctx* c, const double* poses, const double* orig
   rc = upload_poses(c, poses);
   if (rc) return rc;
   HIPCHECK(c, hipMemcpyAsync(c->d_q64, rays, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, c->d_poses, c->pm, c->stream));
+  HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, c->d_poses, c->pm, c->stream,
+                                c->lm.S <= fsdf::kPoseArgMax ? poses : nullptr));
   HIPCHECK(c, fsdf::launch_raycast(c->precision, c->cull != 0, c->lm, c->pm, origin, c->d_q64, n, c->d_d, c->stream));
   HIPCHECK(c, hipMemcpyAsync(depth_out, c->d_d, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(c, hipStreamSynchronize(c->stream));

@@ -89,9 +89,17 @@ struct PassOutputs {
   unsigned long long* stats = nullptr;  // optional kernel counters (fsdf_debug_stats)
 };
 
-// precision: 64 or 32. Points are AoS of the matching precision.
+// Surfaces whose poses ride in the pose kernel's arguments (12·64 doubles =
+// 6 KiB of kernarg; larger scenes upload them with a copy).
+constexpr int kPoseArgMax = 64;
+struct PoseArgs {
+  double v[12 * kPoseArgMax];
+};
+
+// precision: 64 or 32. Points are AoS of the matching precision. h_poses (host,
+// S <= kPoseArgMax) are passed by value in the launch; otherwise d_poses is read.
 hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_poses,
-                       const PosedModel& pm, hipStream_t s);
+                       const PosedModel& pm, hipStream_t s, const double* h_poses = nullptr);
 
 hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm,
                        const void* d_pts, int64_t n, int nblocks, const PassOutputs& out,

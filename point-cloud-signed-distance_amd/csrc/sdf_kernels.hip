@@ -32,6 +32,7 @@
 #include "fsdf_internal.h"
 
 #include <math.h>
+#include <string.h>
 
 namespace fsdf {
 
@@ -65,10 +66,10 @@ __device__ __forceinline__ void rot_vec(const double* P, const double* v, double
   o[2] = __builtin_fma(P[6], v[0], __builtin_fma(P[7], v[1], P[8] * v[2]));
 }
 template <typename T>
-__global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const double* __restrict__ poses,
-                                                      T* __restrict__ planes_w, float* __restrict__ spheres_w,
-                                                      T* __restrict__ verts_w, T* __restrict__ hscale_w,
-                                                      float* __restrict__ screen_w) {
+__device__ __forceinline__ void pose_body(const LocalModel& lm, const double* __restrict__ poses,
+                                          T* __restrict__ planes_w, float* __restrict__ spheres_w,
+                                          T* __restrict__ verts_w, T* __restrict__ hscale_w,
+                                          float* __restrict__ screen_w) {
   int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int fv = lm.F + lm.V, fv_pad = (fv + 63) & ~63;
   if (tid >= fv && tid < fv_pad) return;  // padding: hull waves start wave-aligned
@@ -144,6 +145,27 @@ __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const doubl
       hscale_w[k] = sc;
     }
   }
+}
+
+// Poses from global memory (uploaded by a copy), or — for up to kPoseArgMax
+// surfaces — straight from the kernel arguments: the launch carries the 12·S
+// doubles, each workgroup copies them into LDS, and the per-pass host-to-device
+// copy (a blit kernel of its own) disappears from the step.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const double* __restrict__ poses,
+                                                      T* __restrict__ planes_w, float* __restrict__ spheres_w,
+                                                      T* __restrict__ verts_w, T* __restrict__ hscale_w,
+                                                      float* __restrict__ screen_w) {
+  pose_body<T>(lm, poses, planes_w, spheres_w, verts_w, hscale_w, screen_w);
+}
+template <typename T>
+__global__ __launch_bounds__(kBlock) void pose_kernel_args(LocalModel lm, PoseArgs pa, T* __restrict__ planes_w,
+                                                           float* __restrict__ spheres_w, T* __restrict__ verts_w,
+                                                           T* __restrict__ hscale_w, float* __restrict__ screen_w) {
+  __shared__ double sp[12 * kPoseArgMax];
+  for (int i = threadIdx.x; i < 12 * lm.S; i += kBlock) sp[i] = pa.v[i];
+  __syncthreads();
+  pose_body<T>(lm, sp, planes_w, spheres_w, verts_w, hscale_w, screen_w);
 }
 
 // ---------------------------------------------------------------------------
@@ -1358,10 +1380,21 @@ int pass_blocks(int64_t n) {
 }
 
 hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_poses, const PosedModel& pm,
-                       hipStream_t s) {
+                       hipStream_t s, const double* h_poses) {
   const int total = ((lm.F + lm.V + 63) & ~63) + 64 * lm.K;
   if (total == 0) return hipSuccess;  // RBF-only scene: nothing to pose
   const int grid = (total + kBlock - 1) / kBlock;
+  if (h_poses) {
+    PoseArgs pa;
+    memcpy(pa.v, h_poses, (size_t)12 * lm.S * sizeof(double));
+    if (precision == 64)
+      hipLaunchKernelGGL(pose_kernel_args<double>, dim3(grid), dim3(kBlock), 0, s, lm, pa, (double*)pm.planes_w,
+                         pm.spheres_w, (double*)pm.verts_w, (double*)pm.hscale_w, pm.screen_w);
+    else
+      hipLaunchKernelGGL(pose_kernel_args<float>, dim3(grid), dim3(kBlock), 0, s, lm, pa, (float*)pm.planes_w,
+                         pm.spheres_w, (float*)pm.verts_w, (float*)pm.hscale_w, (float*)nullptr);
+    return hipGetLastError();
+  }
   if (precision == 64) {
     hipLaunchKernelGGL(pose_kernel<double>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses,
                        (double*)pm.planes_w, pm.spheres_w, (double*)pm.verts_w, (double*)pm.hscale_w,

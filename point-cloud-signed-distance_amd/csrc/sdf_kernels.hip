@@ -1349,19 +1349,27 @@ raycast_kernel(RayOrigin o, const double* __restrict__ rays, int64_t n, PassMode
   }
 }
 
+// One workgroup per accumulator entry: each thread sums its strided blocks with
+// 4 independent loads in flight, then a DPP wave sum and a 4-wave combine in
+// fixed order (deterministic for a given grid).
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict__ partials, int nblocks,
                                                         double* __restrict__ accum) {
   const int j = blockIdx.x;
-  double s = 0.0;
-  for (int b = threadIdx.x; b < nblocks; b += kBlock) s += partials[(int64_t)j * nblocks + b];
-  __shared__ double sh[kBlock];
-  sh[threadIdx.x] = s;
-  __syncthreads();
-  for (int w = kBlock / 2; w > 0; w >>= 1) {
-    if (threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
-    __syncthreads();
+  const double* row = partials + (int64_t)j * nblocks;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int b = threadIdx.x;
+  for (; b + 3 * kBlock < nblocks; b += 4 * kBlock) {
+    s0 += row[b];
+    s1 += row[b + kBlock];
+    s2 += row[b + 2 * kBlock];
+    s3 += row[b + 3 * kBlock];
   }
-  if (threadIdx.x == 0) accum[j] = sh[0];
+  for (; b < nblocks; b += kBlock) s0 += row[b];
+  double s = wave_sum((s0 + s1) + (s2 + s3));
+  __shared__ double sh[kBlock / 64];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) accum[j] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
 }
 
 __global__ void to_f32_kernel(const double* __restrict__ src, float* __restrict__ dst, int64_t count) {

@@ -187,7 +187,7 @@ def main():
         flops_per_launch = f_alg * n
         achieved = flops_per_launch / (pass_avg_ms / 1e3) / 1e12
         peak = FP64_VALU_PEAK_TFLOPS if args.precision == 64 else FP32_VALU_PEAK_TFLOPS
-        traffic, traffic_src = None, None
+        traffic, traffic_src, executed = None, None, None
         pmc = os.path.join(ROOT, "profiles", "latest_pmc.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
@@ -195,6 +195,7 @@ def main():
             if rec.get("workload") == "bench.py default" and args.precision == 64 and not args.no_cull \
                     and not args.no_sort and not args.no_per_point and args.order == "shuffled":
                 traffic, traffic_src = rec.get("traffic_bytes_per_launch"), rec.get("source")
+                executed = rec.get("executed")
         out = {
             "metric": "SDF+grad point-evals/sec, 1M-pt cloud x 64-prim model (M64)",
             "value": value,
@@ -224,6 +225,7 @@ def main():
                 "flop_per_eval": f_alg, "algorithmic_flops_per_launch": flops_per_launch,
                 "hbm": {"achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": hbm_achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": bytes_per_launch},
+                "executed_pmc": executed,
                 "note": "F_alg counts every plane test of all 64 hulls (the reference's brute force, SURVEY.md "
                         "§8d); the kernel's exact-safe culling executes ~2.2 hull evaluations per 64-point "
                         "wave, so this effective fraction can exceed 1 — executed-VALU utilisation from PMC "

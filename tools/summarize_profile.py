@@ -53,8 +53,17 @@ def main(src, tag, dst):
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         rel = os.path.relpath(os.path.join(dst, "pmc_summary.json"), root)
         with open(os.path.join(root, "profiles", "latest_pmc.json"), "w") as f:
-            json.dump({"workload": "bench.py default", "kernel": pk[0],
-                       "traffic_bytes_per_launch": hb["traffic_bytes"], "source": rel}, f, indent=1)
+            rec = {"workload": "bench.py default", "kernel": pk[0],
+                   "traffic_bytes_per_launch": hb["traffic_bytes"], "source": rel}
+            pc = out[pk[0]]
+            m = lambda c: pc[c]["mean_per_launch"] if c in pc else None  # noqa: E731
+            if m("SQ_WAVE_CYCLES"):
+                rec["executed"] = {
+                    "valu_insts_per_launch": m("SQ_INSTS_VALU"),
+                    "fp64_fma_insts_per_launch": m("SQ_INSTS_VALU_FMA_F64"),
+                    "valu_active_frac_of_wave_time": (m("SQ_ACTIVE_INST_VALU") or 0) / m("SQ_WAVE_CYCLES"),
+                    "wait_frac_of_wave_time": (m("SQ_WAIT_ANY") or 0) / m("SQ_WAVE_CYCLES")}
+            json.dump(rec, f, indent=1)
     print(json.dumps(hb, indent=1))
 
 

@@ -218,3 +218,24 @@ def test_sort_points_preserves_caller_order(m64, oracle_mod, ctx_factory):
     ctx.set_points(pts2)
     _, _, (k2, d2, _) = ctx.eval(poses, per_point=True)
     assert np.abs(d2 - ref[0][::-1]).max() < 2e-5
+
+
+def test_grid_stride_beyond_max_grid(irb, ctx_factory):
+    """More points than one wave-iteration per wave covers (16,384 blocks x 256):
+    the pass grid-strides; culled == brute force bit for bit, the sorted run
+    returns the same per-point values in caller order, cost == Σ d²."""
+    import flash
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(irb, 211)
+    n = 16384 * 256 + 12345
+    pts = synthetic.depth_cloud(irb, qt, n, seed=212, order="shuffled")
+    poses = flash.hull_poses(irb, qe)
+    out = {}
+    for cull, srt in ((True, True), (False, False)):
+        ctx = ctx_factory(irb, cull=cull, sort_points=srt)
+        ctx.set_points(pts)
+        out[cull] = ctx.eval(poses, per_point=True)
+    (c1, a1, (k1, d1, g1)), (c0, a0, (k0, d0, g0)) = out[True], out[False]
+    assert np.array_equal(k1, k0) and np.array_equal(d1, d0) and np.array_equal(g1, g0)
+    assert c1 == pytest.approx(np.dot(d1, d1), rel=1e-10)
+    assert np.allclose(a1, a0, rtol=1e-9, atol=1e-9 * np.abs(a0).max())

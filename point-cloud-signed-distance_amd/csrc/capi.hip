@@ -57,6 +57,7 @@ struct fsdf_ctx {
   double* d_planes_l = nullptr;
   int32_t* d_face_hull = nullptr;
   double* d_sphere_l = nullptr;
+  double* d_box_l = nullptr;
   int32_t* d_face_off = nullptr;
   int32_t* d_vert_hull = nullptr;
   int32_t* d_vert_off = nullptr;
@@ -126,6 +127,7 @@ static void free_model(fsdf_ctx* c) {
   dfree(c->d_planes_l);
   dfree(c->d_face_hull);
   dfree(c->d_sphere_l);
+  dfree(c->d_box_l);
   dfree(c->d_face_off);
   dfree(c->d_vert_hull);
   dfree(c->d_vert_off);
@@ -262,7 +264,7 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
     return fail(c, FSDF_ERR_ARG, "set_surfaces: RBF skins need %d accumulators, limit %d", rbf_acc_off.back(),
                 fsdf::kMaxRbfAccum);
   const int K = (int)hulls.size();
-  std::vector<double> verts, planes, sph;
+  std::vector<double> verts, planes, sph, box;
   std::vector<int32_t> faces, face_hull, face_off, vert_hull, vert_off, face_rows;
   int stage_bytes = 0;
   const int tsz_ = c->precision == 64 ? (int)sizeof(double) : (int)sizeof(float);
@@ -300,6 +302,21 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
     sph.push_back(cen[1]);
     sph.push_back(cen[2]);
     sph.push_back((double)rf);
+    // body-frame bounding box, half extents padded and rounded up to float
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = 0; i < h.n_vertices; ++i)
+      for (int j = 0; j < 3; ++j) {
+        lo[j] = std::min(lo[j], h.vertices[3 * i + j]);
+        hi[j] = std::max(hi[j], h.vertices[3 * i + j]);
+      }
+    for (int j = 0; j < 3; ++j) box.push_back(0.5 * (lo[j] + hi[j]));
+    box.push_back(0.0);
+    for (int j = 0; j < 3; ++j) {
+      const double c = 0.5 * (lo[j] + hi[j]);
+      const double e = std::max(hi[j] - c, c - lo[j]);
+      box.push_back((double)nextafterf((float)(e * (1.0 + 1e-9) + 1e-12), INFINITY));
+    }
+    box.push_back(0.0);
     for (int f = 0; f < h.n_faces; ++f) {
       for (int j = 0; j < 3; ++j) {
         const int vi = h.faces[3 * f + j];
@@ -389,6 +406,7 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   HIPCHECK(c, dalloc(&c->d_planes_l, planes.size() * sizeof(double)));
   HIPCHECK(c, dalloc(&c->d_face_hull, face_hull.size() * sizeof(int32_t)));
   HIPCHECK(c, dalloc(&c->d_sphere_l, sph.size() * sizeof(double)));
+  HIPCHECK(c, dalloc(&c->d_box_l, box.size() * sizeof(double)));
   HIPCHECK(c, dalloc(&c->d_face_off, face_off.size() * sizeof(int32_t)));
   HIPCHECK(c, dalloc(&c->d_vert_hull, vert_hull.size() * sizeof(int32_t)));
   HIPCHECK(c, dalloc(&c->d_vert_off, vert_off.size() * sizeof(int32_t)));
@@ -396,7 +414,7 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   HIPCHECK(c, dalloc((char**)&c->pm.verts_w, (size_t)V * 4 * tsz));
   HIPCHECK(c, dalloc((char**)&c->pm.hscale_w, (size_t)K * tsz));
   HIPCHECK(c, dalloc((char**)&c->pm.planes_w, (size_t)std::max(F, 1) * 4 * tsz));
-  HIPCHECK(c, dalloc(&c->pm.spheres_w, (size_t)K * 4 * sizeof(float)));
+  HIPCHECK(c, dalloc(&c->pm.spheres_w, (size_t)K * fsdf::kBoundFloats * sizeof(float)));
   HIPCHECK(c, dalloc(&c->pm.screen_w, (size_t)std::max(F + K, 1) * 4 * sizeof(float)));
   HIPCHECK(c, dalloc(&c->d_poses, (size_t)S * 12 * sizeof(double)));
   const int R = (int)rbf_surface.size();
@@ -431,6 +449,7 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   HIPCHECK(c, hipMemcpy(c->d_planes_l, planes.data(), planes.size() * sizeof(double), hipMemcpyHostToDevice));
   HIPCHECK(c, hipMemcpy(c->d_face_hull, face_hull.data(), face_hull.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   HIPCHECK(c, hipMemcpy(c->d_sphere_l, sph.data(), sph.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHECK(c, hipMemcpy(c->d_box_l, box.data(), box.size() * sizeof(double), hipMemcpyHostToDevice));
   HIPCHECK(c, hipMemcpy(c->d_face_off, face_off.data(), face_off.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   HIPCHECK(c, hipMemcpy(c->d_vert_hull, vert_hull.data(), vert_hull.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   HIPCHECK(c, hipMemcpy(c->d_vert_off, vert_off.data(), vert_off.size() * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -451,6 +470,7 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   c->lm.planes_l = c->d_planes_l;
   c->lm.face_hull = c->d_face_hull;
   c->lm.sphere_l = c->d_sphere_l;
+  c->lm.box_l = c->d_box_l;
   c->lm.face_off = c->d_face_off;
   c->lm.vert_hull = c->d_vert_hull;
   c->lm.vert_off = c->d_vert_off;
@@ -747,7 +767,11 @@ extern "C" int fsdf_pass_time(fsdf_ctx* c, double* total_ms, int64_t* launches) 
   return FSDF_OK;
 }
 
-static constexpr int kStatCount = 22;
+#ifndef FSDF_WAVE_TIMES
+#define FSDF_WAVE_TIMES 0
+#endif
+// 22 counters; diagnostic builds with -DFSDF_WAVE_TIMES=1 append per-wave clocks
+static constexpr int kStatCount = FSDF_WAVE_TIMES ? 32 + 2 * 4 * fsdf::kMaxBlocks : 22;
 
 extern "C" int fsdf_kernel_stats(fsdf_ctx* c, int32_t enable, uint64_t* counters) {
   if (!c) return FSDF_ERR_ARG;

@@ -8,6 +8,8 @@
 //     planes_l  [F][4]  f64     (n, d), n·x <= d inside
 //     face_hull [F]     i32     owning hull of each face
 //     sphere_l  [K][4]  f64     vertex centroid (inside the hull) + radius
+//     box_l     [K][8]  f64     body-frame bounding box: centre xyz, 0, half extents xyz
+//                               (rounded up to f32), 0
 //     face_off  [K+1]   i32     faces of hull k are [face_off[k], face_off[k+1])
 //     vert_hull [V]     i32     owning hull of each vertex
 //     vert_off  [K+1]   i32     vertices of hull k are [vert_off[k], vert_off[k+1])
@@ -17,7 +19,8 @@
 //
 //   posed model (rewritten by every evaluation; T = double or float)
 //     planes_w  [F][4]  T       world plane
-//     spheres_w [K][4]  f32     world centroid + radius (culling only)
+//     spheres_w [K][20] f32     culling bounds: world centroid + radius, then the world
+//                               oriented box: (centre, 0), 3 x (body axis i, half extent i)
 //     verts_w   [V][4]  T       world vertices (support/optimality certificate)
 //     hscale_w  [K]     T       max_v |v|_1 over the hull's world vertices
 //     screen_w  [F+K][4] f32    fp32 screening planes, hull-centred, in face pairs:
@@ -40,7 +43,8 @@ namespace fsdf {
 #define FSDF_SCREEN32 1
 #endif
 
-constexpr int kBlock = 256;        // 4 waves of 64
+constexpr int kBlock = 256;
+constexpr int kBoundFloats = 20;   // spheres_w row (sphere + oriented box)        // 4 waves of 64
 constexpr int kMaxLds = 163840;    // LDS a workgroup may declare (gfx950)
 constexpr int kMaxHulls = 256;     // 4 accumulator slots per lane
 #ifndef FSDF_MAX_BLOCKS
@@ -64,6 +68,7 @@ struct LocalModel {
   const double* planes_l = nullptr;
   const int32_t* face_hull = nullptr;
   const double* sphere_l = nullptr;
+  const double* box_l = nullptr;       // [K][8]
   const int32_t* face_off = nullptr;
   const int32_t* vert_hull = nullptr;
   const int32_t* vert_off = nullptr;

@@ -137,11 +137,27 @@ __device__ __forceinline__ void pose_body(const LocalModel& lm, const double* __
     if (lane == 0) {
       double cw[3];
       xf_point(P, lm.sphere_l + 4 * k, cw);
-      spheres_w[4 * k + 0] = (float)cw[0];
-      spheres_w[4 * k + 1] = (float)cw[1];
-      spheres_w[4 * k + 2] = (float)cw[2];
-      // radius was rounded up to float on the host (exact-safe)
-      spheres_w[4 * k + 3] = (float)lm.sphere_l[4 * k + 3];
+      float* bw = spheres_w + kBoundFloats * k;
+      bw[0] = (float)cw[0];
+      bw[1] = (float)cw[1];
+      bw[2] = (float)cw[2];
+      // radius and half extents were rounded up to float on the host (exact-safe)
+      bw[3] = (float)lm.sphere_l[4 * k + 3];
+      // oriented box: body axis i is column i of R
+      const double* B = lm.box_l + 8 * k;
+      double cb[3];
+      xf_point(P, B, cb);
+      bw[4] = (float)cb[0];
+      bw[5] = (float)cb[1];
+      bw[6] = (float)cb[2];
+      bw[7] = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        bw[8 + 4 * i + 0] = (float)P[i];
+        bw[8 + 4 * i + 1] = (float)P[3 + i];
+        bw[8 + 4 * i + 2] = (float)P[6 + i];
+        bw[8 + 4 * i + 3] = (float)B[4 + i];
+      }
       hscale_w[k] = sc;
     }
   }
@@ -272,10 +288,45 @@ struct PassModel {
 typedef float F4 __attribute__((ext_vector_type(4)));
 struct HullRow {
   F4 sphere;      // world centroid + radius (f32, exact-safe culling)
+  F4 box[4];      // world oriented box: (centre, 0), 3 x (body axis, half extent)
   int f0, v0;     // first face / vertex of the hull
   double hscale;  // certificate scale max_v |v|_1
 };
-static_assert(sizeof(HullRow) == 32, "HullRow is 32 bytes");
+static_assert(sizeof(HullRow) == 96, "HullRow is 96 bytes");
+
+// Lower bound of hull k's signed distance at x from its oriented box (the hull
+// lies inside the box): with u_i = |a_i·(x − c)| − e_i, outside the box
+// d_k(x) >= |max(u, 0)| (distance to the box); inside, the hull's inner ball
+// around x fits in the box, so d_k(x) >= max_i u_i. 1-Lipschitz in x. f32
+// rounding (~1e-6 of |x|_1 + |c|_1 + the bound, |c|_1 <= |c_k|_1 + 3 r_k) is
+// inside the culling margins. Returns max_i u_i and s = |max(u, 0)|^2: the
+// bound is sqrt(s) when max_i u_i > 0, else max_i u_i.
+__device__ __forceinline__ float box_bound(const HullRow& h, float x, float y, float z, float& s) {
+  const F4 c = h.box[0];
+  const float qx = x - c[0], qy = y - c[1], qz = z - c[2];
+  float mx = -__builtin_huge_valf();
+  s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const F4 a = h.box[1 + i];
+    const float u = fabsf(__builtin_fmaf(a[0], qx, __builtin_fmaf(a[1], qy, a[2] * qz))) - a[3];
+    mx = fmaxf(mx, u);
+    const float pu = fmaxf(u, 0.0f);
+    s = __builtin_fmaf(pu, pu, s);
+  }
+  return mx;
+}
+// box lower bound <= t
+__device__ __forceinline__ bool box_within(const HullRow& h, float x, float y, float z, float t) {
+  float s;
+  const float mx = box_bound(h, x, y, z, s);
+  return mx <= 0.0f ? mx <= t : (t >= 0.0f && s <= t * t);
+}
+__device__ __forceinline__ float box_lower(const HullRow& h, float x, float y, float z) {
+  float s;
+  const float mx = box_bound(h, x, y, z, s);
+  return mx <= 0.0f ? mx : __builtin_sqrtf(s);
+}
 
 // Bounding sphere of the wave's points (f32, wave-uniform): every valid lane's
 // point p satisfies |p - c| <= r up to f32 rounding (covered by the margins).
@@ -289,7 +340,10 @@ template <typename T>
 __device__ __forceinline__ float load_hull_table(const PassModel<T>& m, HullRow* __restrict__ ht) {
   for (int k = threadIdx.x; k <= m.K; k += kBlock) {
     HullRow r;
-    r.sphere = k < m.K ? ((const F4*)m.spheres)[k] : F4{0.f, 0.f, 0.f, 0.f};
+    const F4* b = (const F4*)(m.spheres + kBoundFloats * k);  // row K (sentinel) is not read
+    r.sphere = k < m.K ? b[0] : F4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r.box[i] = k < m.K ? b[1 + i] : F4{0.f, 0.f, 0.f, 0.f};
     r.f0 = m.face_off[k];
     r.v0 = m.vert_off[k];
     r.hscale = k < m.K ? (double)m.hscale[k] : 0.0;
@@ -311,6 +365,9 @@ constexpr int kMaxRbfAcc = kMaxRbfAccum;
 // shader-clock deltas to stats[10..18]: culling, hull staging, plane max, fast
 // path, closest-feature search, whole wave-iteration, segmented reduction,
 // per-point stores, scene evaluation.
+#ifndef FSDF_WAVE_TIMES
+#define FSDF_WAVE_TIMES 0
+#endif
 #ifndef FSDF_PHASE_TIMING
 #define FSDF_PHASE_TIMING 0
 #endif
@@ -337,7 +394,7 @@ __device__ __forceinline__ void phase_add(unsigned long long* stats, int slot, u
 // the event counters (stats[0..9]) are off in phase-timing builds: their
 // contended atomics would dominate the timed windows
 __device__ __forceinline__ bool count_events(const unsigned long long* stats) {
-  return !FSDF_PHASE_TIMING && stats != nullptr;
+  return !FSDF_PHASE_TIMING && !FSDF_WAVE_TIMES && stats != nullptr;
 }  // RBF adjoint doubles per wave (Σ 4n+4)
 // Diagnostic ablations (timing-only builds via -DFSDF_ABLATE=mask; results are
 // wrong): 4 no slow path, 16 no segmented reduction, 32 no per-point stores,
@@ -996,10 +1053,11 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   const int K = m.K;
   const int lane = threadIdx.x & 63;
   // Phase A (fp32, exact-safe): with c_k inside hull k and r_k its bounding
-  // radius, d_k(p) >= |p-c_k| - r_k (lower bound) and d_k(p) <= |p-c_k|
-  // (upper bound). ub = min_k |p-c_k|; the best-first seed is the hull of
-  // least power distance |p-c_k|^2 - r_k^2 (a heuristic: any seed is exact).
-  float ub2 = __builtin_huge_valf(), pw_min = __builtin_huge_valf();
+  // radius, d_k(p) >= |p-c_k| - r_k and d_k(p) >= the oriented-box bound
+  // (lower bounds), d_k(p) <= |p-c_k| (upper bound). ub = min_k |p-c_k|; the
+  // best-first seed is the hull of least lower bound (a heuristic: any seed
+  // is exact).
+  float ub2 = __builtin_huge_valf(), lb_min = __builtin_huge_valf();
   int kseed = 0;
   float pxf = 0.f, pyf = 0.f, pzf = 0.f;
   // candidate hulls of the wave (bit k&63 of cand[k>>6]); all hulls without culling
@@ -1046,10 +1104,12 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     }
     ubw = wave_minmax<false>(ubw);
     const float mrgw = 1e-5f * (1.0f + fabsf(cwx) + fabsf(cwy) + fabsf(cwz) + smax + 4.0f * rw + 2.0f * ubw);
+    // ... and so does one whose box bound at c_w (1-Lipschitz) minus r_w does
 #pragma unroll
     for (int s = 0; s < SLOTS; ++s) {
       const int k = 64 * s + lane;
-      const bool c = k < K && Dk[s] - rw - ht[k < K ? k : 0].sphere[3] <= ubw + mrgw;
+      const HullRow& h = ht[k < K ? k : 0];
+      const bool c = k < K && Dk[s] - rw - h.sphere[3] <= ubw + mrgw && box_within(h, cwx, cwy, cwz, ubw + mrgw + rw);
       cand[s] = __ballot(c);
     }
     if (count_events(stats) && lane == 0) {
@@ -1069,8 +1129,9 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
         const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
         const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
         ub2 = fminf(ub2, dist2);
-        const float pwr = __builtin_fmaf(-sp[3], sp[3], dist2);
-        if (pwr < pw_min) { pw_min = pwr; kseed = k; }
+        // seed: the least lower bound (sphere or box)
+        const float lb = fmaxf(__builtin_sqrtf(dist2) - sp[3], box_lower(ht[k], pxf, pyf, pzf));
+        if (lb < lb_min) { lb_min = lb; kseed = k; }
       }
     }
   }
@@ -1104,8 +1165,9 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     const F4 sp = ht[k].sphere;
     const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
     const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
-    const float t = fminf(ub, (float)best) + mrg + sp[3];
-    return valid && t >= 0.0f && dist2 <= t * t;
+    const float tb = fminf(ub, (float)best) + mrg;
+    const float t = tb + sp[3];
+    return valid && t >= 0.0f && dist2 <= t * t && box_within(ht[k], pxf, pyf, pzf, tb);
   };
   // evaluations may run out of index order: ties keep the smaller k
   auto evaluate = [&](int k, bool need) {
@@ -1203,6 +1265,9 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
     const int64_t ii = valid ? i : n - 1;
     const T px = pts[3 * ii + 0], py = pts[3 * ii + 1], pz = pts[3 * ii + 2];
     const uint64_t t_iter = phase_clock();
+#if FSDF_WAVE_TIMES
+    const uint64_t w_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
     T best, gx, gy, gz;
     int bk;
@@ -1265,6 +1330,15 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
     }
     phase_add(out.stats, 17, t_st);
     phase_add(out.stats, 15, t_iter);
+#if FSDF_WAVE_TIMES
+    // diagnostic: 100 MHz wall clock around each wave-iteration of the first
+    // grid pass (stats + 32 + 2 * wave), written by lane 0
+    if (out.stats && lane == 0 && base < (int64_t)64 * 4 * kMaxBlocks) {
+      const int64_t wv = base / 64;
+      out.stats[32 + 2 * wv] = w_t0;
+      out.stats[33 + 2 * wv] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
   }
 
 #if FSDF_PHASE_TIMING

@@ -188,3 +188,38 @@ def test_cone_fallback_paths(oracle_mod):
     finally:
         c.close()
     assert st["full_scan_lanes"] > 0 and st["screen_fallbacks"] > 0 and st["walk_steps"] > 0, st
+
+
+@pytest.mark.parametrize("precision", [64, 32])
+def test_needles_oriented_box_culling(precision, oracle_mod):
+    """Thin rods at random orientations, packed so that their bounding spheres
+    overlap everywhere: the oriented-box lower bound does the culling. Some
+    rods have body frames far from their vertices (box centre offset 3 m in
+    the body frame, undone by the pose) and one sits 50 m from the origin:
+    the f32 box transform and its margins at large coordinates. Culled and
+    sorted results equal the oracle's brute force."""
+    from flash import _lib
+    r = rng(733)
+    K = 24
+    hulls, offs = [], []
+    for k in range(K):
+        off = np.array([3.0, -2.0, 1.0]) if k % 3 == 0 else np.zeros(3)
+        ax = r.normal(size=(30, 3)) * np.array([0.2, 0.006, 0.004]) + off
+        hulls.append(_lib.convex_hull(ax))
+        offs.append(off)
+    poses = _poses(r, K, spread=0.12)
+    for k in range(K):
+        R = poses[k, :9].reshape(3, 3)
+        poses[k, 9:] -= R @ offs[k]
+    poses[K - 1, 9:] += np.array([50.0, 0.0, 0.0])
+    # points along the rods' world axes (surface, inside, near) plus a haze
+    n = 8000
+    kk = r.integers(0, K, n)
+    t = r.uniform(-0.25, 0.25, n)
+    axis = poses[kk][:, [0, 3, 6]]
+    centre = poses[kk, 9:] + np.einsum("nij,nj->ni", poses[kk, :9].reshape(n, 3, 3), np.asarray(offs)[kk])
+    pts = centre + axis * t[:, None] + r.normal(size=(n, 3)) * 0.01
+    pts[: n // 8] = r.uniform(-0.3, 0.3, size=(n // 8, 3))
+    for sort_points in (False, True):
+        k = _parity(hulls, poses, pts, oracle_mod, precision=precision, cull=True, sort_points=sort_points)
+    assert len(np.unique(k)) == K

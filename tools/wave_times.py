@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Per-wave wall-clock timeline of one pass (GPU box, diagnostic build):
+
+    make -C point-cloud-signed-distance_amd/csrc dev DEV_OUT=../../ab/lib_wt.so EXTRA=-DFSDF_WAVE_TIMES=1
+    FLASHSDF_LIB=$PWD/ab/lib_wt.so python tools/wave_times.py [--points N] [--json out.json]
+
+Each wave-iteration of the first grid pass records s_memrealtime (100 MHz)
+at its start and end. Prints the pass span, the wave-duration distribution,
+and how much of the span the last-started waves occupy (the tail).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "point-cloud-signed-distance_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--points", type=int, default=1 << 20)
+    ap.add_argument("--order", default="shuffled")
+    ap.add_argument("--json", default=None)
+    args = ap.parse_args()
+    import flash
+    from flash import Models, synthetic, _lib
+
+    m = Models.arm_grid()
+    qt, qe = synthetic.perturbed_configuration(m, 1234)
+    poses = flash.hull_poses(m, qe)
+    pts = synthetic.depth_cloud(m, qt, args.points, seed=1234 + 17, order=args.order)
+    c = _lib.Context(device=0, precision=64, cull=True, sort_points=True)
+    c.set_model([(s.hull.vertices, s.hull.faces, s.hull.planes) for s in m.surfaces])
+    c.set_points(pts)
+    for _ in range(3):
+        c.eval(poses)
+    lib = _lib.load()
+    nw = -(-args.points // 64)
+    buf = np.zeros(32 + 2 * 4 * 16384, np.uint64)
+    assert lib.fsdf_kernel_stats(c._ctx, 1, None) == 0
+    c.eval(poses)
+    assert lib.fsdf_kernel_stats(c._ctx, 0, buf.ctypes.data_as(ctypes.c_void_p)) == 0
+    c.close()
+    t = buf[32:32 + 2 * min(nw, 4 * 16384)].reshape(-1, 2).astype(np.int64)
+    if not t[:, 0].any():
+        print("no wave times recorded (not a -DFSDF_WAVE_TIMES=1 build?)")
+        return 1
+    t0 = t[:, 0].min()
+    start = (t[:, 0] - t0) * 0.01  # us
+    end = (t[:, 1] - t0) * 0.01
+    dur = end - start
+    span = end.max()
+    q = np.percentile(dur, [10, 50, 90, 99, 100])
+    # busy fraction of wave slots over time (1024 WG slots x 4 waves)
+    grid = np.linspace(0, span, 41)
+    live = [int(((start <= g) & (end > g)).sum()) for g in grid[:-1]]
+    order = np.argsort(start)
+    late = order[-len(order) // 20:]  # last 5 % of waves to start
+    res = {"points": args.points, "waves": int(len(dur)), "span_us": float(span),
+           "dur_us_p10_p50_p90_p99_max": [float(x) for x in q], "dur_us_mean": float(dur.mean()),
+           "sum_dur_us": float(dur.sum()),
+           "last5pct_start_us": float(start[late].min()), "last5pct_end_max_us": float(end[late].max()),
+           "live_waves_over_time": live,
+           "corr_dur_vs_index": float(np.corrcoef(dur, np.arange(len(dur)))[0, 1])}
+    print(json.dumps(res))
+    if args.json:
+        np.savez_compressed(args.json.replace(".json", ".npz"), start=start, end=end)
+        with open(args.json, "w") as f:
+            json.dump(res, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -85,6 +85,11 @@ struct fsdf_ctx {
   // work
   double* d_partials = nullptr;
   size_t partials_cap = 0;
+  // cost-ordered schedule of resident-cloud passes (fsdf::PassOutputs::order)
+  uint32_t* d_block_cost = nullptr;  // [kMaxBlocks]
+  int32_t* d_block_order = nullptr;  // [kMaxBlocks]
+  int order_nblocks = 0;             // grid the order was built for (0: none yet)
+  int order_age = 0;                 // passes since the order was rebuilt
   double* d_accum = nullptr;
   int32_t* d_kstar = nullptr;
   double* d_d = nullptr;
@@ -199,6 +204,8 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   dfree(c->d_q);
   dfree(c->d_q64);
   dfree(c->d_stats);
+  dfree(c->d_block_cost);
+  dfree(c->d_block_order);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (int i = 0; i < kPoseRing; ++i) {
     if (c->pose_ev[i]) (void)hipEventDestroy(c->pose_ev[i]);
@@ -613,8 +620,12 @@ static int upload_poses(fsdf_ctx* c, const double* poses) {
   return FSDF_OK;
 }
 
+static constexpr int kOrderEvery = 16;
+
+// schedule: resident-cloud passes (repeated over the same cloud) launch their
+// workgroups heaviest-first by the previous pass's durations
 static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t n, double* d_accum,
-                    int32_t* d_kstar, double* d_d, double* d_grad, const int64_t* d_perm) {
+                    int32_t* d_kstar, double* d_d, double* d_grad, const int64_t* d_perm, bool schedule) {
   if (c->lm.R > 0 && !c->rbf_ready)
     return fail(c, FSDF_ERR_STATE, "eval: the scene has RBF surfaces: call fsdf_set_rbf_params first");
   int rc = upload_poses(c, poses);
@@ -631,6 +642,14 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
   out.grad = d_grad;
   out.perm = d_perm;
   out.stats = c->stats_on ? c->d_stats : nullptr;
+  if (schedule && n > 0) {
+    if (!c->d_block_cost) {
+      HIPCHECK(c, hipMalloc(&c->d_block_cost, fsdf::kMaxBlocks * sizeof(uint32_t)));
+      HIPCHECK(c, hipMalloc(&c->d_block_order, fsdf::kMaxBlocks * sizeof(int32_t)));
+    }
+    out.cost = c->d_block_cost;
+    out.order = c->order_nblocks == nblocks ? c->d_block_order : nullptr;
+  }
   if (n > 0) {
     const bool prof = c->profiling && c->prof_used + 2 <= c->prof_ev.size();
     if (prof) HIPCHECK(c, hipEventRecord(c->prof_ev[c->prof_used], c->stream));
@@ -639,7 +658,16 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
       HIPCHECK(c, hipEventRecord(c->prof_ev[c->prof_used + 1], c->stream));
       c->prof_used += 2;
     }
-    HIPCHECK(c, fsdf::launch_reduce(c->d_partials, nblocks, accum_len(c), d_accum, c->stream));
+    // the order is rebuilt on the first scheduled pass of a grid and then every
+    // kOrderEvery passes (the heavy blocks of a cloud stay heavy from pass to
+    // pass; the rebuild is a ~7 us single-workgroup sort on the reduce launch)
+    const bool rebuild = out.cost && (c->order_nblocks != nblocks || ++c->order_age >= kOrderEvery);
+    HIPCHECK(c, fsdf::launch_reduce(c->d_partials, nblocks, accum_len(c), d_accum, c->stream,
+                                    rebuild ? out.cost : nullptr, rebuild ? c->d_block_order : nullptr));
+    if (rebuild) {
+      c->order_nblocks = nblocks;
+      c->order_age = 0;
+    }
   } else {
     HIPCHECK(c, hipMemsetAsync(d_accum, 0, (size_t)accum_len(c) * sizeof(double), c->stream));
   }
@@ -652,7 +680,7 @@ extern "C" int fsdf_eval_device(fsdf_ctx* c, const double* poses, double* d_accu
   if (c->lm.S == 0) return fail(c, FSDF_ERR_STATE, "eval: no model (call fsdf_set_model first)");
   if (!poses || !d_accum) return fail(c, FSDF_ERR_ARG, "eval_device: poses and d_accum are required");
   HIPCHECK(c, hipSetDevice(c->device));
-  return run_pass(c, poses, c->d_pts, c->n, d_accum, d_kstar, d_d, d_grad, c->d_perm);
+  return run_pass(c, poses, c->d_pts, c->n, d_accum, d_kstar, d_d, d_grad, c->d_perm, true);
 }
 
 static int ensure_outputs(fsdf_ctx* c, int64_t n) {
@@ -698,7 +726,7 @@ extern "C" int fsdf_eval(fsdf_ctx* c, const double* poses, double* cost_out, dou
     if (rc) return rc;
   }
   int rc = run_pass(c, poses, c->d_pts, c->n, c->d_accum, want_pp ? c->d_kstar : nullptr,
-                    want_pp ? c->d_d : nullptr, want_pp ? c->d_grad : nullptr, c->d_perm);
+                    want_pp ? c->d_d : nullptr, want_pp ? c->d_grad : nullptr, c->d_perm, true);
   if (rc) return rc;
   return fetch(c, c->n, cost_out, accum_out, kstar_out, d_out, grad_out, want_pp);
 }
@@ -727,7 +755,7 @@ extern "C" int fsdf_skin(fsdf_ctx* c, const double* poses, const double* xyz, in
     if (rc) return rc;
     d_query = c->d_q;
   }
-  rc = run_pass(c, poses, d_query, n, c->d_accum, c->d_kstar, c->d_d, c->d_grad, nullptr);
+  rc = run_pass(c, poses, d_query, n, c->d_accum, c->d_kstar, c->d_d, c->d_grad, nullptr, false);
   if (rc) return rc;
   return fetch(c, n, nullptr, nullptr, kstar_out, d_out, grad_out, true);
 }

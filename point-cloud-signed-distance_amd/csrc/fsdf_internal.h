@@ -92,6 +92,12 @@ struct PassOutputs {
   double* grad = nullptr;      // optional [n][3]
   const int64_t* perm = nullptr;  // optional: resident index -> caller index
   unsigned long long* stats = nullptr;  // optional kernel counters (fsdf_debug_stats)
+  // optional cost-ordered schedule (resident-cloud passes): launch slot b runs
+  // logical block order[b] (a permutation of [0, nblocks)); every logical block
+  // writes its duration (100 MHz ticks) to cost[block]. Partial sums stay in
+  // logical-block columns, so results do not depend on the order.
+  const int32_t* order = nullptr;
+  uint32_t* cost = nullptr;
 };
 
 // Surfaces whose poses ride in the pose kernel's arguments (12·64 doubles =
@@ -114,8 +120,10 @@ hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const Pos
 hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const double* origin,
                           const double* d_rays, int64_t n, double* d_depth, hipStream_t s);
 
+// With cost/order: one extra workgroup also rebuilds order[] (heaviest logical
+// blocks first) from this pass's costs, for the next pass of the same grid.
 hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum,
-                         hipStream_t s);
+                         hipStream_t s, const uint32_t* cost = nullptr, int32_t* order = nullptr);
 
 hipError_t launch_to_f32(const double* src, float* dst, int64_t count, hipStream_t s);
 

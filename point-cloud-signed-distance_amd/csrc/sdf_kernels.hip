@@ -1254,12 +1254,15 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
   const int stage_cap = m.stage_bytes / (4 * (int)sizeof(T));
   if (RBF)
     for (int e = lane; e < m.rbf_acc_off[m.R]; e += 64) rbf_wave[e] = 0.0;
+  // logical block of this launch slot (cost-ordered schedule, see PassOutputs)
+  const int lb = out.order ? __builtin_amdgcn_readfirstlane(out.order[blockIdx.x]) : (int)blockIdx.x;
+  const uint64_t t_block = out.cost ? __builtin_amdgcn_s_memrealtime() : 0;
   const float smax = load_hull_table(m, ht);
 #if FSDF_PHASE_TIMING
   if (lane < 10) fsdf_phase_acc[wave][lane] = 0;
 #endif
   const int64_t stride = (int64_t)gridDim.x * kBlock;
-  for (int64_t base = (int64_t)blockIdx.x * kBlock + wave * 64; base < n; base += stride) {
+  for (int64_t base = (int64_t)lb * kBlock + wave * 64; base < n; base += stride) {
     const int64_t i = base + lane;
     const bool valid = i < n;
     const int64_t ii = valid ? i : n - 1;
@@ -1363,8 +1366,9 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
 #pragma unroll
       for (int w = 1; w < kBlock / 64; ++w) s += rbf_acc[w * kMaxRbfAcc + src];
     }
-    out.partials[(int64_t)t * gridDim.x + blockIdx.x] = s;
+    out.partials[(int64_t)t * gridDim.x + lb] = s;
   }
+  if (out.cost && threadIdx.x == 0) out.cost[lb] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_block);
 }
 
 // ---------------------------------------------------------------------------
@@ -1426,9 +1430,81 @@ raycast_kernel(RayOrigin o, const double* __restrict__ rays, int64_t n, PassMode
 // One workgroup per accumulator entry: each thread sums its strided blocks with
 // 4 independent loads in flight, then a DPP wave sum and a 4-wave combine in
 // fixed order (deterministic for a given grid).
+// Schedule for the next pass (one workgroup): the workgroups of a pass hold
+// their slot until their slowest wave ends and durations vary ~10x (waves
+// whose points span several hulls), so launching the logical blocks in index
+// order leaves a tail of late heavy blocks. Counting sort of this pass's
+// durations into 64 buckets, heaviest first (list scheduling, longest first).
+__device__ void build_order(const uint32_t* __restrict__ cost, int nb, int32_t* __restrict__ order) {
+  constexpr int kPer = 16;  // costs per thread and tile (tile = 4,096 blocks)
+  __shared__ uint8_t bkt[kMaxBlocks];
+  __shared__ unsigned hist[64][kBlock / 64];  // [bucket][wave]: 4x less atomic contention
+  __shared__ unsigned wmax[kBlock / 64];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  unsigned mx = 0;
+  for (int b0 = 0; b0 < nb; b0 += kPer * kBlock) {
+    unsigned c[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = b0 + u * kBlock + t;
+      c[u] = i < nb ? cost[i] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) mx = max(mx, c[u]);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, off, 64));
+  if (lane == 0) wmax[w] = mx;
+  hist[lane][w] = 0;
+  __syncthreads();
+  mx = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+  const float sc = 63.0f / (float)(mx ? mx : 1u);
+  for (int b0 = 0; b0 < nb; b0 += kPer * kBlock) {
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = b0 + u * kBlock + t;
+      if (i < nb) {
+        const int b = 63 - min(63, (int)((float)cost[i] * sc));  // 0 = heaviest
+        bkt[i] = (uint8_t)b;
+        atomicAdd(&hist[b][w], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  // exclusive scan over (bucket, wave) in bucket-major order: wave 0, lane = bucket
+  if (w == 0) {
+    const unsigned h0 = hist[lane][0], h1 = hist[lane][1], h2 = hist[lane][2], h3 = hist[lane][3];
+    const unsigned tot = h0 + h1 + h2 + h3;
+    unsigned inc = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned o = (unsigned)__shfl_up((int)inc, off, 64);
+      if (lane >= off) inc += o;
+    }
+    const unsigned ex = inc - tot;
+    hist[lane][0] = ex;
+    hist[lane][1] = ex + h0;
+    hist[lane][2] = ex + h0 + h1;
+    hist[lane][3] = ex + h0 + h1 + h2;
+  }
+  __syncthreads();
+  for (int b0 = 0; b0 < nb; b0 += kPer * kBlock) {
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int i = b0 + u * kBlock + t;
+      if (i < nb) order[atomicAdd(&hist[bkt[i]][w], 1u)] = i;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict__ partials, int nblocks,
-                                                        double* __restrict__ accum) {
+                                                        double* __restrict__ accum, const uint32_t* __restrict__ cost,
+                                                        int32_t* __restrict__ order) {
   const int j = blockIdx.x;
+  if (cost && j == (int)gridDim.x - 1) {  // the extra workgroup
+    build_order(cost, nblocks, order);
+    return;
+  }
   const double* row = partials + (int64_t)j * nblocks;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   int b = threadIdx.x;
@@ -1610,8 +1686,10 @@ hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const 
   return hipGetLastError();
 }
 
-hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum, hipStream_t s) {
-  hipLaunchKernelGGL(reduce_kernel, dim3(len), dim3(kBlock), 0, s, partials, nblocks, d_accum);
+hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum, hipStream_t s,
+                         const uint32_t* cost, int32_t* order) {
+  hipLaunchKernelGGL(reduce_kernel, dim3(len + (cost ? 1 : 0)), dim3(kBlock), 0, s, partials, nblocks, d_accum,
+                     cost, order);
   return hipGetLastError();
 }
 

@@ -239,3 +239,34 @@ def test_grid_stride_beyond_max_grid(irb, ctx_factory):
     assert np.array_equal(k1, k0) and np.array_equal(d1, d0) and np.array_equal(g1, g0)
     assert c1 == pytest.approx(np.dot(d1, d1), rel=1e-10)
     assert np.allclose(a1, a0, rtol=1e-9, atol=1e-9 * np.abs(a0).max())
+
+
+def test_cost_ordered_schedule_is_invisible(m64, oracle_mod, ctx_factory):
+    """Resident-cloud passes launch their workgroups heaviest-first by the
+    previous pass's durations (rebuilt on the first scheduled pass, then every
+    16): across 40 passes alternating two configurations, every pass equals the
+    first (unscheduled) pass of its configuration bit for bit — per-point
+    outputs AND the accumulator (partial sums stay in logical-block columns) —
+    and the oracle. A different grid (new cloud size) starts unscheduled."""
+    import flash
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(m64, 901)
+    pts = synthetic.depth_cloud(m64, qt, 300007, seed=902, order="shuffled")
+    poses = [flash.hull_poses(m64, qe), flash.hull_poses(m64, qe + 2e-3)]
+    ctx = ctx_factory(m64, sort_points=True)
+    ctx.set_points(pts)
+    first = [ctx.eval(p, per_point=True) for p in poses]
+    for it in range(40):
+        c, acc, pp = ctx.eval(poses[it % 2], per_point=True)
+        c0, acc0, pp0 = first[it % 2]
+        assert c == c0 and np.array_equal(acc, acc0), it
+        for x, y in zip(pp, pp0):
+            assert np.array_equal(x, y), it
+    om = oracle_mod.OracleModel.from_manipulator(m64)
+    _check_against(om.skin(poses[1], pts), first[1][2][1], first[1][2][0], first[1][2][2], first[1][1],
+                   om.cost_accum(poses[1], pts))
+    # a smaller cloud: another grid, the order of the old one is not used
+    ctx.set_points(pts[:100003])
+    for _ in range(3):
+        _, acc_s, (k_s, d_s, _) = ctx.eval(poses[0], per_point=True)
+        assert np.array_equal(k_s, first[0][2][0][:100003]) and np.array_equal(d_s, first[0][2][1][:100003])

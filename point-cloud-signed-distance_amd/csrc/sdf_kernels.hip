@@ -385,6 +385,9 @@ __device__ __forceinline__ uint64_t phase_clock() {
 #if FSDF_PHASE_TIMING
 __shared__ unsigned long long fsdf_phase_acc[kBlock / 64][10];  // per wave, flushed at kernel end
 #endif
+#if FSDF_WAVE_TIMES
+__shared__ unsigned fsdf_wave_ev[kBlock / 64][2];  // per wave-iteration: hull evaluations, seed evaluations
+#endif
 __device__ __forceinline__ void phase_add(unsigned long long* stats, int slot, uint64_t t0) {
 #if FSDF_PHASE_TIMING
   const uint64_t t1 = phase_clock();
@@ -1171,6 +1174,9 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   };
   // evaluations may run out of index order: ties keep the smaller k
   auto evaluate = [&](int k, bool need) {
+#if FSDF_WAVE_TIMES
+    if (lane == 0) ++fsdf_wave_ev[threadIdx.x >> 6][0];
+#endif
     T dk, hx, hy, hz;
     hull_sdf<T>(px, py, pz, k, m, ht, need, best, dk, hx, hy, hz, lw, stats);
     if (count_events(stats)) {
@@ -1203,6 +1209,9 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
       for (int s = 0; s < SLOTS; ++s)
         if ((k >> 6) == s) done[s] |= 1ull << (k & 63);
       if (count_events(stats) && lane == 0) atomicAdd(stats + 5, 1ull);
+#if FSDF_WAVE_TIMES
+      if (lane == 0) ++fsdf_wave_ev[threadIdx.x >> 6][1];
+#endif
       need = needs(k);
     } else {
       while (!cm && slot < SLOTS - 1) {
@@ -1270,6 +1279,7 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
     const uint64_t t_iter = phase_clock();
 #if FSDF_WAVE_TIMES
     const uint64_t w_t0 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) fsdf_wave_ev[wave][0] = fsdf_wave_ev[wave][1] = 0;
 #endif
 
     T best, gx, gy, gz;
@@ -1340,6 +1350,8 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
       const int64_t wv = base / 64;
       out.stats[32 + 2 * wv] = w_t0;
       out.stats[33 + 2 * wv] = __builtin_amdgcn_s_memrealtime();
+      out.stats[32 + 8 * kMaxBlocks + 2 * wv] = fsdf_wave_ev[wave][0];
+      out.stats[33 + 8 * kMaxBlocks + 2 * wv] = fsdf_wave_ev[wave][1];
     }
 #endif
   }

@@ -40,12 +40,13 @@ def main():
         c.eval(poses)
     lib = _lib.load()
     nw = -(-args.points // 64)
-    buf = np.zeros(32 + 2 * 4 * 16384, np.uint64)
+    buf = np.zeros(32 + 4 * 4 * 16384, np.uint64)
     assert lib.fsdf_kernel_stats(c._ctx, 1, None) == 0
     c.eval(poses)
     assert lib.fsdf_kernel_stats(c._ctx, 0, buf.ctypes.data_as(ctypes.c_void_p)) == 0
     c.close()
     t = buf[32:32 + 2 * min(nw, 4 * 16384)].reshape(-1, 2).astype(np.int64)
+    ev = buf[32 + 8 * 16384:32 + 8 * 16384 + 2 * min(nw, 4 * 16384)].reshape(-1, 2).astype(np.int64)
     if not t[:, 0].any():
         print("no wave times recorded (not a -DFSDF_WAVE_TIMES=1 build?)")
         return 1
@@ -65,10 +66,16 @@ def main():
            "sum_dur_us": float(dur.sum()),
            "last5pct_start_us": float(start[late].min()), "last5pct_end_max_us": float(end[late].max()),
            "live_waves_over_time": live,
-           "corr_dur_vs_index": float(np.corrcoef(dur, np.arange(len(dur)))[0, 1])}
+           "corr_dur_vs_index": float(np.corrcoef(dur, np.arange(len(dur)))[0, 1]),
+           "evals_mean": float(ev[:, 0].mean()), "evals_max": int(ev[:, 0].max()),
+           "corr_dur_vs_evals": float(np.corrcoef(dur, ev[:, 0])[0, 1]),
+           "us_per_eval_by_evals": {int(e): float(dur[ev[:, 0] == e].mean() / max(e, 1))
+                                    for e in np.unique(ev[:, 0])},
+           "waves_by_evals": {int(e): int((ev[:, 0] == e).sum()) for e in np.unique(ev[:, 0])},
+           "heaviest_waves": [[float(dur[i]), int(ev[i, 0]), int(ev[i, 1])] for i in np.argsort(-dur)[:12]]}
     print(json.dumps(res))
     if args.json:
-        np.savez_compressed(args.json.replace(".json", ".npz"), start=start, end=end)
+        np.savez_compressed(args.json.replace(".json", ".npz"), start=start, end=end, evals=ev)
         with open(args.json, "w") as f:
             json.dump(res, f, indent=1)
     return 0

@@ -799,7 +799,7 @@ extern "C" int fsdf_pass_time(fsdf_ctx* c, double* total_ms, int64_t* launches) 
 #define FSDF_WAVE_TIMES 0
 #endif
 // 22 counters; diagnostic builds with -DFSDF_WAVE_TIMES=1 append per-wave clocks
-static constexpr int kStatCount = FSDF_WAVE_TIMES ? 32 + 4 * 4 * fsdf::kMaxBlocks : 22;
+static constexpr int kStatCount = FSDF_WAVE_TIMES ? 32 + 4 * 4 * fsdf::kMaxBlocks + 2 * fsdf::kMaxBlocks : 22;
 
 extern "C" int fsdf_kernel_stats(fsdf_ctx* c, int32_t enable, uint64_t* counters) {
   if (!c) return FSDF_ERR_ARG;

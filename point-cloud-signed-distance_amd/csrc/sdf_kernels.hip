@@ -1266,6 +1266,9 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
   // logical block of this launch slot (cost-ordered schedule, see PassOutputs)
   const int lb = out.order ? __builtin_amdgcn_readfirstlane(out.order[blockIdx.x]) : (int)blockIdx.x;
   const uint64_t t_block = out.cost ? __builtin_amdgcn_s_memrealtime() : 0;
+#if FSDF_WAVE_TIMES
+  const uint64_t t_block0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const float smax = load_hull_table(m, ht);
 #if FSDF_PHASE_TIMING
   if (lane < 10) fsdf_phase_acc[wave][lane] = 0;
@@ -1381,6 +1384,12 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
     out.partials[(int64_t)t * gridDim.x + lb] = s;
   }
   if (out.cost && threadIdx.x == 0) out.cost[lb] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_block);
+#if FSDF_WAVE_TIMES
+  if (out.stats && threadIdx.x == 0 && lb < kMaxBlocks) {  // diagnostic: block start / end (100 MHz)
+    out.stats[32 + 16 * kMaxBlocks + 2 * lb] = t_block0;
+    out.stats[33 + 16 * kMaxBlocks + 2 * lb] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------

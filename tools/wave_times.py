@@ -40,13 +40,15 @@ def main():
         c.eval(poses)
     lib = _lib.load()
     nw = -(-args.points // 64)
-    buf = np.zeros(32 + 4 * 4 * 16384, np.uint64)
+    buf = np.zeros(32 + 4 * 4 * 16384 + 2 * 16384, np.uint64)
     assert lib.fsdf_kernel_stats(c._ctx, 1, None) == 0
     c.eval(poses)
     assert lib.fsdf_kernel_stats(c._ctx, 0, buf.ctypes.data_as(ctypes.c_void_p)) == 0
     c.close()
     t = buf[32:32 + 2 * min(nw, 4 * 16384)].reshape(-1, 2).astype(np.int64)
     ev = buf[32 + 8 * 16384:32 + 8 * 16384 + 2 * min(nw, 4 * 16384)].reshape(-1, 2).astype(np.int64)
+    nb = -(-args.points // 256)
+    bt = buf[32 + 16 * 16384:32 + 16 * 16384 + 2 * min(nb, 16384)].reshape(-1, 2).astype(np.int64)
     if not t[:, 0].any():
         print("no wave times recorded (not a -DFSDF_WAVE_TIMES=1 build?)")
         return 1
@@ -72,6 +74,9 @@ def main():
            "us_per_eval_by_evals": {int(e): float(dur[ev[:, 0] == e].mean() / max(e, 1))
                                     for e in np.unique(ev[:, 0])},
            "waves_by_evals": {int(e): int((ev[:, 0] == e).sum()) for e in np.unique(ev[:, 0])},
+           "block_us_mean": float((bt[:, 1] - bt[:, 0]).mean() * 0.01),
+           "block_minus_slowest_wave_us_mean": float(((bt[:, 1] - bt[:, 0]) * 0.01 - dur[:len(bt) * 4].reshape(-1, 4).max(1)).mean()),
+           "block_start_to_first_wave_us_mean": float(((t[:len(bt) * 4, 0].reshape(-1, 4).min(1) - bt[:, 0]) * 0.01).mean()),
            "heaviest_waves": [[float(dur[i]), int(ev[i, 0]), int(ev[i, 1])] for i in np.argsort(-dur)[:12]]}
     print(json.dumps(res))
     if args.json:

@@ -52,7 +52,7 @@ def parse():
     p.add_argument("--no-cull", action="store_true")
     p.add_argument("--order", default="shuffled", choices=("raster", "shuffled"),
                    help="input order of the synthetic cloud (shuffled = adversarial)")
-    p.add_argument("--no-sort", action="store_true", help="keep the input order resident (no Morton sort)")
+    p.add_argument("--no-sort", action="store_true", help="keep the input order resident (no Hilbert sort)")
     p.add_argument("--no-per-point", action="store_true", help="reduction-only pass (no per-point outputs)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of the CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -131,7 +131,7 @@ def main():
     torch.cuda.synchronize()
     ctx.set_points_device(d_pts.data_ptr(), len(pts))  # first upload (allocations)
     t_set = time.perf_counter()
-    ctx.set_points_device(d_pts.data_ptr(), len(pts))  # once per frame: copy (+ Morton sort)
+    ctx.set_points_device(d_pts.data_ptr(), len(pts))  # once per frame: copy (+ Hilbert sort)
     set_points_ms = (time.perf_counter() - t_set) * 1e3
     del d_pts
     n = len(pts)

@@ -574,7 +574,7 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
     }
     if (rc == FSDF_OK) {
       hipError_t e = hipMalloc(&c->d_perm, (size_t)n * sizeof(int64_t));
-      if (e == hipSuccess) e = fsdf::sort_points_morton(d_src, n, c->precision, c->d_pts, c->d_perm, c->stream);
+      if (e == hipSuccess) e = fsdf::sort_points_spatial(d_src, n, c->precision, c->d_pts, c->d_perm, c->stream);
       if (e != hipSuccess) rc = fail(c, FSDF_ERR_HIP, "set_points (sort): %s", hipGetErrorString(e));
     }
   } else {

@@ -132,9 +132,9 @@ int pass_blocks(int64_t n);
 // dynamic LDS of one pass (raycast=false) / raycast workgroup for this model
 size_t pass_lds_bytes(const LocalModel& lm, bool raycast);
 
-// Morton-order the f64 AoS cloud d_src into d_dst (context precision) and write
+// Hilbert-order (sort.hip) the f64 AoS cloud d_src into d_dst (context precision) and write
 // the permutation d_perm[resident i] = caller index. Synchronizes `s`.
-hipError_t sort_points_morton(const double* d_src, int64_t n, int precision, void* d_dst, int64_t* d_perm,
+hipError_t sort_points_spatial(const double* d_src, int64_t n, int precision, void* d_dst, int64_t* d_perm,
                               hipStream_t s);
 
 }  // namespace fsdf

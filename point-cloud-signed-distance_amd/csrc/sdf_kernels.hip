@@ -11,7 +11,7 @@
 //  termination-simplex estimate and is replaced by the exact one — DESIGN.md §2).
 //
 // Kernel design:
-//   * one lane per point; each wave owns 64 consecutive (Morton-ordered)
+//   * one lane per point; each wave owns 64 consecutive (Hilbert-ordered)
 //     resident points;
 //   * exact-safe culling: hulls are dropped for the whole wave from its
 //     bounding sphere, then per lane by |p−c_k|−r_k against min(upper bound,

@@ -84,7 +84,7 @@ class Manipulator:
     def engine(self, device: int = 0, precision: int = 64, cull: bool = True,
                sort_points: bool = True) -> "_lib.Context":
         """The native context holding this model on `device` (created once).
-        sort_points: the resident cloud is Morton-ordered on the device once per
+        sort_points: the resident cloud is Hilbert-ordered on the device once per
         frame (set_points); outputs still come back in caller order."""
         key = (device, precision, cull, sort_points)
         ctx = self._engines.get(key)

@@ -196,7 +196,7 @@ def test_cost_functor_gradient_and_tracking(irb):
 
 
 def test_sort_points_preserves_caller_order(m64, oracle_mod, ctx_factory):
-    """sort_points (device Morton order) changes only speed: per-point outputs
+    """sort_points (device Hilbert order) changes only speed: per-point outputs
     come back in caller order, bit-identical to the oracle."""
     import flash
     from flash import synthetic

@@ -20,6 +20,8 @@
  *     sensed_points held by reference             fsdf_set_points (once/frame)
  *   EnhancedGJK.NeighborMesh / conv(vertices)   src/models.jl:152
  *                                                     fsdf_convex_hull
+ *   transform_to_root(state, frame) src/Flash.jl:248  fsdf_tree_transforms
+ *     (RigidBodyDynamics forward kinematics)          (host, per pass)
  *
  * Conventions
  *   - All host buffers are caller-owned. Nothing is retained past a call
@@ -108,6 +110,20 @@ typedef struct fsdf_surface {
 int fsdf_convex_hull(const double* points, int32_t n, int32_t* n_vertices_out,
                      double* vertices_out, int32_t* n_faces_out, int32_t* faces_out,
                      double* planes_out);
+
+/* Forward kinematics of a mechanism tree (host only, no device): the body
+ * poses transform_to_root(state, body) that the per-pass surface poses are
+ * built from (src/Flash.jl:248; RigidBodyDynamics in the reference). Bodies in
+ * topological order (parent[b] < b, body 0 = root). Per body b >= 1:
+ * kind 0 fixed, 1 revolute about unit axis[b] by q[qoff[b]], 2 quaternion
+ * floating q[qoff[b] .. +7] = (w, x, y, z, tx, ty, tz) (normalized here);
+ * joint_to_parent (AR[b] row-major 3x3, At[b]) and body_to_joint (BR[b], Bt[b]).
+ * Out: R[b], t[b] = transform_to_root(body b); Rb[b], tb[b] = the parent's
+ * transform composed with joint_to_parent (the joint frame before its motion,
+ * where the chain rule's motion subspaces live). All arrays [nb][9] / [nb][3]. */
+int fsdf_tree_transforms(int32_t nb, const int32_t* parent, const int32_t* kind, const int32_t* qoff,
+                         const double* axis, const double* AR, const double* At, const double* BR,
+                         const double* Bt, const double* q, double* R, double* t, double* Rb, double* tb);
 
 /* ---- context ---------------------------------------------------------------- */
 int fsdf_create(fsdf_ctx** out, const fsdf_opts* opts);

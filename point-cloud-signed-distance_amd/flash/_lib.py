@@ -69,6 +69,7 @@ _PROTOS = {
     "fsdf_profile_pass": (c_int32, [c_void_p, c_int32]),
     "fsdf_pass_time": (c_int32, [c_void_p, POINTER(c_double), POINTER(c_int64)]),
     "fsdf_kernel_stats": (c_int32, [c_void_p, c_int32, c_void_p]),
+    "fsdf_tree_transforms": (c_int32, [c_int32] + [c_void_p] * 13),
 }
 SYMBOLS = tuple(_PROTOS)
 

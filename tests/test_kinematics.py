@@ -129,3 +129,25 @@ def test_fixture_json_is_data_only():
     d = json.load(open(os.path.join(DATA_DIR, "irb140.json")))
     assert set(d) == {"source", "urdf", "ati", "meshes"}
     assert len(d["urdf"]["joints"]) == 6
+
+
+def test_native_forward_kinematics_matches_numpy():
+    """fsdf_tree_transforms (csrc/kinematics.cpp) == the numpy level-batched FK
+    to the last bits (revolute chains, fixed joints, a quaternion-floating
+    base), and it rejects a tree that is not in topological order."""
+    from flash import Models, _lib
+    r = np.random.default_rng(41)
+    for m in (Models.arm_grid(), Models.table(), Models.irb140(), Models.irb_and_squishable()[0], Models.two_link_arm()):
+        mech = m.mechanism
+        for _ in range(5):
+            q = mech.normalize(mech.zero_configuration() + r.normal(size=mech.num_positions))
+            for a, b in zip(mech.body_transform_arrays(q), mech.body_transform_arrays_numpy(q)):
+                assert np.allclose(a, b, rtol=0, atol=1e-14)
+    P = Models.irb140().mechanism._kinematic_plan()
+    bad = P["native"][0].copy()
+    bad[2] = 3  # parent after child
+    out = [np.empty(len(bad) * k) for k in (9, 3, 9, 3)]
+    q = np.zeros(16)
+    st = _lib.load().fsdf_tree_transforms(len(bad), bad.ctypes.data, *P["native_ptrs"][1:], q.ctypes.data,
+                                          *[o.ctypes.data for o in out])
+    assert st == 1  # FSDF_ERR_ARG

@@ -44,6 +44,10 @@ namespace fsdf {
 #endif
 
 constexpr int kBlock = 256;
+#ifndef FSDF_PASS_BLOCK
+#define FSDF_PASS_BLOCK 256
+#endif
+constexpr int kPassBlock = FSDF_PASS_BLOCK;  // pass-kernel workgroup (64 or a multiple)
 constexpr int kBoundFloats = 20;   // spheres_w row (sphere + oriented box)        // 4 waves of 64
 constexpr int kMaxLds = 163840;    // LDS a workgroup may declare (gfx950)
 constexpr int kMaxHulls = 256;     // 4 accumulator slots per lane

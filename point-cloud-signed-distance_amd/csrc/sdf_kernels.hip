@@ -338,7 +338,7 @@ struct WaveSphere {
 // culling-margin scale smax = max_k |c_k|_1 + 2 r_k (wave-uniform)
 template <typename T>
 __device__ __forceinline__ float load_hull_table(const PassModel<T>& m, HullRow* __restrict__ ht) {
-  for (int k = threadIdx.x; k <= m.K; k += kBlock) {
+  for (int k = threadIdx.x; k <= m.K; k += (int)blockDim.x) {
     HullRow r;
     const F4* b = (const F4*)(m.spheres + kBoundFloats * k);  // row K (sentinel) is not read
     r.sphere = k < m.K ? b[0] : F4{0.f, 0.f, 0.f, 0.f};
@@ -1237,7 +1237,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
 extern __shared__ __attribute__((aligned(16))) char fsdf_lds[];
 
 template <typename T, int SLOTS, bool CULL, bool RBF>
-__global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)) void pass_kernel(
+__global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)) void pass_kernel(
     const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -1256,9 +1256,9 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
     for (int j = 0; j < 6; ++j) acc_row[s * 64 * 6 + j] = 0.0;
   double cost_acc = 0.0;
   // RBF adjoint sums of this wave (lane 0 adds)
-  double* rbf_acc = red + (kBlock / 64) * kRedStride;
+  double* rbf_acc = red + (kPassBlock / 64) * kRedStride;
   double* rbf_wave = rbf_acc + wave * kMaxRbfAcc;
-  HullRow* ht = (HullRow*)(fsdf_lds + ((kBlock / 64) * kRedStride + (RBF ? (kBlock / 64) * kMaxRbfAcc : 0)) * 8);
+  HullRow* ht = (HullRow*)(fsdf_lds + ((kPassBlock / 64) * kRedStride + (RBF ? (kPassBlock / 64) * kMaxRbfAcc : 0)) * 8);
   T* stage = (T*)((char*)(ht + m.K + 1) + wave * m.stage_bytes);
   const int stage_cap = m.stage_bytes / (4 * (int)sizeof(T));
   if (RBF)
@@ -1273,8 +1273,8 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
 #if FSDF_PHASE_TIMING
   if (lane < 10) fsdf_phase_acc[wave][lane] = 0;
 #endif
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
-  for (int64_t base = (int64_t)lb * kBlock + wave * 64; base < n; base += stride) {
+  const int64_t stride = (int64_t)gridDim.x * kPassBlock;
+  for (int64_t base = (int64_t)lb * kPassBlock + wave * 64; base < n; base += stride) {
     const int64_t i = base + lane;
     const bool valid = i < n;
     const int64_t ii = valid ? i : n - 1;
@@ -1368,18 +1368,18 @@ __global__ __launch_bounds__(kBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS ==
   __syncthreads();
   const int len6 = 1 + 6 * m.S;
   const int len = len6 + (RBF ? m.rbf_acc_off[m.R] : 0);
-  for (int t = threadIdx.x; t < len; t += kBlock) {
+  for (int t = threadIdx.x; t < len; t += kPassBlock) {
     double s;
     if (t < len6) {
       const int src = (t == 0) ? SLOTS * 64 * 6 : t - 1;
       s = red[src];
 #pragma unroll
-      for (int w = 1; w < kBlock / 64; ++w) s += red[w * kRedStride + src];
+      for (int w = 1; w < kPassBlock / 64; ++w) s += red[w * kRedStride + src];
     } else {
       const int src = RBF ? t - len6 : 0;
       s = rbf_acc[src];
 #pragma unroll
-      for (int w = 1; w < kBlock / 64; ++w) s += rbf_acc[w * kMaxRbfAcc + src];
+      for (int w = 1; w < kPassBlock / 64; ++w) s += rbf_acc[w * kMaxRbfAcc + src];
     }
     out.partials[(int64_t)t * gridDim.x + lb] = s;
   }
@@ -1552,7 +1552,7 @@ __global__ void to_f32_kernel(const double* __restrict__ src, float* __restrict_
 // Launchers
 // ---------------------------------------------------------------------------
 int pass_blocks(int64_t n) {
-  int64_t b = (n + kBlock - 1) / kBlock;
+  int64_t b = (n + kPassBlock - 1) / kPassBlock;
   if (b < 1) b = 1;
   if (b > kMaxBlocks) b = kMaxBlocks;
   return (int)b;
@@ -1612,17 +1612,18 @@ static PassModel<T> pass_model(const LocalModel& lm, const PosedModel& pm) {
 static int slots_for(int S) { return S <= 64 ? 1 : (S <= 128 ? 2 : 4); }
 
 size_t pass_lds_bytes(const LocalModel& lm, bool raycast) {
-  const size_t stage = (size_t)(kBlock / 64) * (size_t)lm.stage_bytes + (size_t)(lm.K + 1) * sizeof(HullRow);
+  const size_t waves = (size_t)(raycast ? kBlock : kPassBlock) / 64;
+  const size_t stage = waves * (size_t)lm.stage_bytes + (size_t)(lm.K + 1) * sizeof(HullRow);
   if (raycast) return stage;
-  const size_t red = (size_t)(kBlock / 64) * (size_t)(slots_for(lm.S) * 64 * 6 + 2) * sizeof(double);
-  const size_t rbf = lm.R > 0 ? (size_t)(kBlock / 64) * kMaxRbfAcc * sizeof(double) : 0;
+  const size_t red = waves * (size_t)(slots_for(lm.S) * 64 * 6 + 2) * sizeof(double);
+  const size_t rbf = lm.R > 0 ? waves * kMaxRbfAcc * sizeof(double) : 0;
   return red + rbf + stage;
 }
 
 template <typename K, typename... Args>
-static void launch_lds(K kernel, int grid, size_t lds, hipStream_t s, Args... args) {
+static void launch_lds(K kernel, int grid, int block, size_t lds, hipStream_t s, Args... args) {
   if (lds > 65536) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), lds, s, args...);
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), lds, s, args...);
 }
 
 template <typename T, bool CULL, bool RBF>
@@ -1631,9 +1632,9 @@ static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void
   const PassModel<T> m = pass_model<T>(lm, pm);
   const T* pts = (const T*)d_pts;
   const size_t lds = pass_lds_bytes(lm, false);
-  if (lm.S <= 64) launch_lds(pass_kernel<T, 1, CULL, RBF>, nblocks, lds, s, pts, n, m, out);
-  else if (lm.S <= 128) launch_lds(pass_kernel<T, 2, CULL, RBF>, nblocks, lds, s, pts, n, m, out);
-  else launch_lds(pass_kernel<T, 4, CULL, RBF>, nblocks, lds, s, pts, n, m, out);
+  if (lm.S <= 64) launch_lds(pass_kernel<T, 1, CULL, RBF>, nblocks, kPassBlock, lds, s, pts, n, m, out);
+  else if (lm.S <= 128) launch_lds(pass_kernel<T, 2, CULL, RBF>, nblocks, kPassBlock, lds, s, pts, n, m, out);
+  else launch_lds(pass_kernel<T, 4, CULL, RBF>, nblocks, kPassBlock, lds, s, pts, n, m, out);
 }
 
 // FSDF_BENCH_ONLY=1: A/B timing builds instantiate only the bench variant
@@ -1647,7 +1648,7 @@ static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm,
                           int nblocks, const PassOutputs& out, hipStream_t s) {
 #if FSDF_BENCH_ONLY
   const PassModel<T> m = pass_model<T>(lm, pm);
-  launch_lds(pass_kernel<T, 1, true, false>, nblocks, pass_lds_bytes(lm, false), s, (const T*)d_pts, n, m, out);
+  launch_lds(pass_kernel<T, 1, true, false>, nblocks, kPassBlock, pass_lds_bytes(lm, false), s, (const T*)d_pts, n, m, out);
 #else
   if (lm.R > 0) {
     if (cull) launch_pass_t<T, true, true>(lm, pm, d_pts, n, nblocks, out, s);
@@ -1676,11 +1677,11 @@ static void launch_raycast_t(const LocalModel& lm, const PosedModel& pm, const d
                              int64_t n, double* depth, hipStream_t s) {
   const PassModel<T> m = pass_model<T>(lm, pm);
   const RayOrigin o{origin[0], origin[1], origin[2]};
-  const int nb = pass_blocks(n);
+  const int nb = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, kMaxBlocks);
   const size_t lds = pass_lds_bytes(lm, true);
-  if (lm.S <= 64) launch_lds(raycast_kernel<T, 1, CULL, RBF>, nb, lds, s, o, rays, n, m, depth);
-  else if (lm.S <= 128) launch_lds(raycast_kernel<T, 2, CULL, RBF>, nb, lds, s, o, rays, n, m, depth);
-  else launch_lds(raycast_kernel<T, 4, CULL, RBF>, nb, lds, s, o, rays, n, m, depth);
+  if (lm.S <= 64) launch_lds(raycast_kernel<T, 1, CULL, RBF>, nb, kBlock, lds, s, o, rays, n, m, depth);
+  else if (lm.S <= 128) launch_lds(raycast_kernel<T, 2, CULL, RBF>, nb, kBlock, lds, s, o, rays, n, m, depth);
+  else launch_lds(raycast_kernel<T, 4, CULL, RBF>, nb, kBlock, lds, s, o, rays, n, m, depth);
 }
 
 template <typename T>

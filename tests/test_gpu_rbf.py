@@ -114,3 +114,25 @@ def test_tracking_deformable_beanbag():
     x = estimate_state(m, pts, x0, callback=lambda x, c: seen.append(c),
                        solver=NaiveSolver(len(x0), rate=0.05, max_step=0.05, iteration_limit=25))
     assert seen[-1] < 0.5 * c0
+
+
+@pytest.mark.parametrize("precision", [64, 32])
+def test_scheduled_passes_rbf_scene(precision):
+    """Config 5's scene (hulls + RBF skin + table) in the RBF pass variant, f64
+    and f32, sorted cloud: 20 repeated passes (scheduled from the second on,
+    the order rebuilt at the 16th) are bit-identical to the first."""
+    z = np.load(os.path.join(GOLDEN, "c5_scene.npz"))
+    c = _ctx(_scene("c5_scene"), precision=precision, sort_points=True)
+    pts = np.concatenate([z["points"]] * 40)  # > one block per wave-iteration round
+    c.set_points(pts)
+    c.set_rbf_params(z["rbf_rows"])
+    first = c.eval(z["poses"], per_point=True)
+    for it in range(20):
+        cost, acc, pp = c.eval(z["poses"], per_point=True)
+        assert cost == first[0] and np.array_equal(acc, first[1]), it
+        for a, b in zip(pp, first[2]):
+            assert np.array_equal(a, b), it
+    if precision == 64:
+        n0 = len(z["points"])
+        assert np.array_equal(first[2][0][:n0], z["kstar"]) and np.array_equal(first[2][1][:n0], z["d"])
+    c.close()

@@ -620,7 +620,10 @@ static int upload_poses(fsdf_ctx* c, const double* poses) {
   return FSDF_OK;
 }
 
-static constexpr int kOrderEvery = 16;
+#ifndef FSDF_ORDER_EVERY
+#define FSDF_ORDER_EVERY 16
+#endif
+static constexpr int kOrderEvery = FSDF_ORDER_EVERY;
 
 // schedule: resident-cloud passes (repeated over the same cloud) launch their
 // workgroups heaviest-first by the previous pass's durations

@@ -92,8 +92,11 @@ typedef struct fsdf_hull {
  *                      `n_centers` centres; its world centres and RBF
  *                      coefficients are supplied per pass (fsdf_set_rbf_params),
  *                      its pose is ignored. Value: s = f/|∇f| with
- *                      f(x) = Σ w_i |x-c_i|^3 + a + b·x (XCubed + affine;
- *                      pinned by test/runtests.jl:17). */
+ *                      f(x) = Σ w_i |x-c_i|^3 + a + b·x (XCubed + affine).
+ *                      Matches the reference KAT (test/runtests.jl:17) but NOT
+ *                      the costs printed by examples/manipulator.ipynb:5512,
+ *                      :14179 (ours 4.44x / 2.0x; no candidate formulation fits
+ *                      all three): a documented divergence, DESIGN.md §2. */
 #define FSDF_SURFACE_HULL 0
 #define FSDF_SURFACE_RBF 1
 typedef struct fsdf_surface {

@@ -19,7 +19,7 @@
  *       given as R|t per hull; world planes/vertices          -> oracle_pose_model
  *   s(x) for InterpolatingGeometry = SpatialFields surface     src/Flash.jl:207-213
  *       restated as f/|∇f| of the XCubed + affine RBF fit    -> oracle_rbf_skin
- *       (pinned by test/runtests.jl:17, see oracle/rbf.py)
+ *       (KAT test/runtests.jl:17 holds; the notebook costs do not: DESIGN.md §2)
  *   cost = Σ_p skin(p)^2                                      src/gradientdescent.jl:32
  *       plus the per-hull wrench sums that carry ∂cost/∂pose   -> oracle_cost_accum
  *

@@ -6,10 +6,14 @@ used by Flash.skin for InterpolatingGeometry (src/Flash.jl:207-213):
   f(x) = Σ_i w_i |x - c_i|^3 + a + b·x           (XCubed + affine polynomial)
   [A P; Pᵀ 0] [w; a; b] = [v; 0],  A_ik = |c_i - c_k|^3,  P_i = [1, c_iᵀ]
   s(x) = f(x) / |∇f(x)|                           (the field, made distance-like)
-SpatialFields @06046c27 is un-vendored. This formulation is pinned by the
+SpatialFields @06046c27 is un-vendored. This formulation satisfies the
 reference's only numeric test (test/runtests.jl:17): beanbag, default state,
-s(100, 0, 0) ≈ 99 (rtol 2e-2) — it gives 98.893. The r³+affine field without
-normalization gives 162.3.
+s(100, 0, 0) ≈ 99 (rtol 2e-2) — it gives 98.893 (the r³+affine field without
+normalization gives 162.3). It does NOT reproduce the two
+costs examples/manipulator.ipynb prints (:5512, :14179): 4.44× and 2.0× of
+them; a bounded search over 55 formulations found none fitting all three
+(tools/rbf_formulation_search.py, tests/test_notebook_pins.py). RBF parity is
+therefore partial: pinned by one KAT, contradicted by two notebook outputs.
 
 Also the cost gradient through the weight solve (adjoint): for cost
 c = Σ_p s(p)^2 over the points whose nearest surface is this skin,

@@ -11,7 +11,8 @@ the host
 and after the pass turns the RBF adjoint block of the accumulator
 (λ = Σ 2s ∂s/∂(w,a,b), E_i = Σ 2s ∂s/∂c_i) into ∂c/∂c_j through the solve
 (μ = M⁻ᵀλ), then into body wrenches (∂c/∂q) and ∂c/∂δ. The field value on the
-device is s = f/|∇f| (pinned by test/runtests.jl:17).
+device is s = f/|∇f| (matches the KAT test/runtests.jl:17; diverges from the
+examples/manipulator.ipynb costs by 4.44x / 2.0x — DESIGN.md §2).
 """
 from __future__ import annotations
 

@@ -136,3 +136,27 @@ def test_scheduled_passes_rbf_scene(precision):
         n0 = len(z["points"])
         assert np.array_equal(first[2][0][:n0], z["kstar"]) and np.array_equal(first[2][1][:n0], z["d"])
     c.close()
+
+
+def test_manipulator_notebook_on_gpu(oracle_mod):
+    """examples/manipulator.ipynb cells 2/6 through the product path (GPU
+    raycast of the true state, GPU CostFunctor at the two printed
+    configurations) == the CPU oracle; the divergence from the notebook's
+    printed costs is the measured one (tests/test_notebook_pins.py)."""
+    import flash
+    from flash import Models
+    from flash.depthsensors import Kinect, raycast
+    from flash.gradientdescent import CostFunctor
+    import test_notebook_pins as nb
+    m = Models.two_link_arm(False)
+    st = flash.ManipulatorState(m)
+    st.set_configuration(nb.PINS["x_true"])
+    pts = raycast(st, Kinect(nb.PINS["sensor"]["rows"], nb.PINS["sensor"]["cols"]), nb.camera())
+    opts, ocosts = nb.oracle_notebook(oracle_mod)
+    assert pts.shape == opts.shape == (nb.MEASURED_HITS, 3)
+    assert np.allclose(pts, opts, rtol=0, atol=1e-12)
+    cf = CostFunctor(m, pts)
+    for pin, oc, ratio in zip(nb.PINS["pins"], ocosts, nb.MEASURED_RATIO):
+        c = cf(np.asarray(pin["x"]))
+        assert c == pytest.approx(oc, rel=1e-9)
+        assert c / pin["cost"] == pytest.approx(ratio, rel=2e-3)

@@ -1,25 +1,38 @@
 #!/usr/bin/env python3
 """Benchmark: SDF+grad point-evals/s, 1M-point cloud x 64-primitive model (M64).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config m64|c2|c4]
+                    [--points P | --global-points G]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
-A step is ONE residual pass of the hot path over the resident cloud: ship the
-64 hull poses (pinned ring -> H2D), the pose kernel, the pass kernel (per point:
-nearest hull d*, k*, ∇d* written to HBM + the cost/wrench partial sums), the
-fixed-order reduce kernel and, for N > 1, the RCCL all-reduce of the 385-double
-accumulator. Weak scaling: every rank owns its own 2^20-point shard (BASELINE
-config 4 is 10M points over 8 GPUs = 1.31M per GPU), seeded per rank.
+A step is ONE residual pass of the hot path over the resident cloud: the pose
+kernel (the 12·S pose doubles ride in its arguments), the pass kernel (per
+point: nearest hull d*, k*, ∇d* written to HBM + the cost/wrench partial sums),
+the fixed-order reduce kernel and, for N > 1, the RCCL all-reduce of the
+1+6S-double accumulator.
+
+Sharding (contiguous ⌈N/W⌉ point ranges, uploaded once per frame):
+  --points P          weak scaling: every rank owns its own P-point cloud (the
+                      default: P = 2^20, the metric's 1M cloud on every GPU)
+  --global-points G   strong scaling: ONE G-point cloud (the same seed on every
+                      rank) split into W contiguous shards
+  --config c4         BASELINE config 4: IRB140, 10·2^20 points, strong scaling
+The metric's single-GPU workload is M64 with 2^20 points either way.
 
 Rank 0 prints one JSON line (contract in the task description) with:
-  roofline      the pass kernel on its binding roofline, fp64 VALU:
-                F_alg = Σ_hulls (21 + 7·F_k) + 15 FLOP per point-eval x points per
-                launch / the kernel's mean HIP-event time, against the FP64 vector
-                peak; the HBM fraction (60 B per eval) is reported beside it, and
-                `traffic` is the PMC-measured HBM bytes per launch of the committed
-                profile (profiles/latest_pmc.json, tools/rocprof_round.sh)
-  cpu_baseline  the C oracle (brute force over all hulls, the reference's loop)
-                on a bounded sample of the same cloud, on this host's cores
+  roofline      the pass kernel on the HBM roofline: algorithmic bytes per launch
+                (24 B in + 36 B out per point) / its mean HIP-event
+                time vs 8 TB/s; `traffic` = PMC bytes per launch of the committed
+                profile (profiles/latest_pmc.json); `valu_issue_frac` = executed
+                VALU wave-instructions (PMC) x 2 cycles / (1,024 SIMDs x 2.4 GHz x
+                kernel time); the brute-force-equivalent F_alg rate is under
+                `valu_effective` (it counts work the culling never executes)
+  cpu_baseline  the C oracle on a bounded sample of the same cloud, on this
+                host's cores: culled (sphere lower bounds, exact) as `value`,
+                brute force (the reference's loop) beside it
+  config        set-points (copy + Hilbert sort) per frame, a 30-iteration frame,
+                and the full CostFunctor iteration (host FK + pass + accumulator
+                read-back + chain rule) measured in the same run
 """
 from __future__ import annotations
 
@@ -35,11 +48,20 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "point-cloud-signed-distance_amd"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-# FP64 vector: 256 CUs x 4 SIMDs x 16 lanes x 2 FLOP x 2.4 GHz (MI355X_MICROARCH.md
-# CU count / clock; = AMD's 78.6 TF spec, half the 157.3 TF FP32 vector peak)
+# FP64 vector: 256 CUs x 4 SIMD-32 x 2.4 GHz, wave64 FMA at 16 lanes/clk = AMD's 78.6 TF
 FP64_VALU_PEAK_TFLOPS = 78.6
 FP32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md
-BYTES_PER_EVAL = 24 + 36        # xyz f64 in; d f64 + k* i32 + grad 3xf64 out
+SIMDS, CLOCK_HZ, CYCLES_PER_WAVE_OP = 1024, 2.4e9, 2   # MI355X_MICROARCH.md §Wave scheduling
+ITERS_PER_FRAME = 30           # examples/irb_and_squishable.ipynb: NaiveSolver iteration_limit
+
+CONFIGS = {
+    # name: (model, default points, scaling, description)
+    "m64": ("arm_grid", 1 << 20, "weak",
+            "M64: 8 IRB140 arms (7 link hulls + ATI hull each) on a 2x4 grid, 64 convex hulls, 48 DOF; seeded "
+            "synthetic depth cloud (SURVEY.md §8d generator G)"),
+    "c2": ("irb140", 1 << 20, "weak", "C2: IRB140 rigid model (7 hulls, 6 DOF), 2^20 synthetic points"),
+    "c4": ("irb140", 10 << 20, "strong", "C4: IRB140 rigid model, ONE 10*2^20-point cloud sharded over the GPUs"),
+}
 
 
 def parse():
@@ -47,23 +69,27 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--points", type=int, default=1 << 20, help="points per GPU")
+    p.add_argument("--config", default="m64", choices=sorted(CONFIGS))
+    g = p.add_mutually_exclusive_group()
+    g.add_argument("--points", type=int, default=None, help="points per GPU (weak scaling)")
+    g.add_argument("--global-points", type=int, default=None, help="one cloud split over the GPUs (strong scaling)")
     p.add_argument("--precision", type=int, default=64, choices=(64, 32))
     p.add_argument("--no-cull", action="store_true")
     p.add_argument("--order", default="shuffled", choices=("raster", "shuffled"),
                    help="input order of the synthetic cloud (shuffled = adversarial)")
     p.add_argument("--no-sort", action="store_true", help="keep the input order resident (no Hilbert sort)")
     p.add_argument("--no-per-point", action="store_true", help="reduction-only pass (no per-point outputs)")
-    p.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of the CPU baseline leg")
+    p.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of each CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-full-iteration", action="store_true")
     p.add_argument("--seed", type=int, default=1234)
     return p.parse_args()
 
 
 def cpu_baseline(manip, pts, q_eval, target_s):
     """Oracle (test infrastructure, the checker/baseline only) on a bounded
-    sample: SURVEY.md §8d — all host threads (the box's OpenMP share) and one
-    thread, median of timed runs after a warm-up, CPU model recorded."""
+    sample: SURVEY.md §8d — culled and brute force, all host threads (the box's
+    OpenMP share) and one thread, median of timed runs after a warm-up."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import statistics
     import flash
@@ -73,21 +99,22 @@ def cpu_baseline(manip, pts, q_eval, target_s):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, os.cpu_count() or 1))
 
-    def rate(nt, per_run_s, runs):
+    def rate(nt, per_run_s, runs, culled):
         n = 1024
         t = time.perf_counter()
-        om.skin(poses, pts[:n], threads=nt)  # warm-up + sizing
+        om.skin(poses, pts[:n], threads=nt, culled=culled)  # warm-up + sizing
         dt = time.perf_counter() - t
         n = int(min(len(pts), max(n, n * per_run_s / max(dt, 1e-6))))
         ts = []
         for _ in range(runs):
             t = time.perf_counter()
-            om.skin(poses, pts[:n], threads=nt)
+            om.skin(poses, pts[:n], threads=nt, culled=culled)
             ts.append(time.perf_counter() - t)
         return n, statistics.median(ts), sum(ts)
 
-    n, med, tot = rate(threads, target_s / 5, 5)
-    n1, med1, tot1 = rate(1, 1.0, 3)
+    n, med, tot = rate(threads, target_s / 5, 5, True)
+    nb, medb, totb = rate(threads, target_s / 5, 5, False)
+    n1, med1, _ = rate(1, 1.0, 3, True)
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -95,10 +122,29 @@ def cpu_baseline(manip, pts, q_eval, target_s):
     except OSError:
         pass
     return {"value": n / med, "unit": "point-evals/s", "cores": threads, "kind": "port",
-            "single_thread_value": n1 / med1,
-            "sample": f"first {n} points of rank 0's cloud, M64 brute force over all 64 hulls (the reference's "
-                      f"loop), median of 5 runs ({tot:.1f} s wall, ~{tot * threads:.0f} CPU-s) on {threads} "
-                      f"threads; 1 thread: {n1} points, median of 3; host CPU: {model}"}
+            "brute_force_value": nb / medb, "single_thread_value": n1 / med1,
+            "sample": f"first {n} points of rank 0's cloud, oracle with exact sphere-bound culling (same results "
+                      f"as brute force), median of 5 runs ({tot:.1f} s wall) on {threads} threads; brute force over "
+                      f"all {om.K} hulls (the reference's loop): {nb} points, median of 5 ({totb:.1f} s); "
+                      f"culled on 1 thread: {n1} points, median of 3; host CPU: {model}"}
+
+
+def full_iteration_ms(manip, ctx, q, iters=20):
+    """One CostFunctor.value_and_gradient iteration on the resident cloud, as
+    track! runs it: native FK + pose assembly, the pass, accumulator read-back,
+    chain rule to ∂c/∂q (the configuration moves every iteration, so the FK
+    cache never hits)."""
+    from flash.core import surface_poses
+    from flash.gradientdescent import gradient_from_accum
+    x = np.array(q, np.float64)
+    for i in range(iters + 3):
+        if i == 3:
+            t = time.perf_counter()
+        x = x + 1e-6
+        poses = surface_poses(manip, manip.mechanism.normalize(x))
+        _, acc, _ = ctx.eval(poses)
+        gradient_from_accum(manip, x, acc, [], 10)
+    return (time.perf_counter() - t) / iters * 1e3
 
 
 def main():
@@ -116,32 +162,50 @@ def main():
 
     import flash
     from flash import Models, synthetic
-    from flash.distributed import allreduce_accum
+    from flash.distributed import allreduce_accum, shard_range
 
-    m64 = Models.arm_grid()
-    q_true, q_eval = synthetic.perturbed_configuration(m64, args.seed)
-    pts = synthetic.depth_cloud(m64, q_true, args.points, seed=args.seed + 17 * (rank + 1), order=args.order)
+    model_name, default_points, scaling, workload = CONFIGS[args.config]
+    if args.global_points is not None:
+        scaling = "strong"
+    elif args.points is not None:
+        scaling = "weak"
+    manip = getattr(Models, model_name)()
+    q_true, q_eval = synthetic.perturbed_configuration(manip, args.seed)
+    if scaling == "strong":
+        g = args.global_points if args.global_points is not None else default_points
+        cloud = synthetic.depth_cloud(manip, q_true, g, seed=args.seed + 17, order=args.order)
+        a, b = shard_range(g, rank, world)
+        pts = np.ascontiguousarray(cloud[a:b])
+        del cloud
+        global_points = g
+    else:
+        p = args.points if args.points is not None else default_points
+        pts = synthetic.depth_cloud(manip, q_true, p, seed=args.seed + 17 * (rank + 1), order=args.order)
+        global_points = p * world
     q_alt = q_eval + 1e-3  # alternate between two configurations step to step
-    poses = [flash.hull_poses(m64, q_eval), flash.hull_poses(m64, q_alt)]
+    poses = [flash.hull_poses(manip, q_eval), flash.hull_poses(manip, q_alt)]
 
-    ctx = m64.engine(device=local, precision=args.precision, cull=not args.no_cull, sort_points=not args.no_sort)
+    ctx = manip.engine(device=local, precision=args.precision, cull=not args.no_cull, sort_points=not args.no_sort)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
     d_pts = torch.as_tensor(pts, device=dev)
     torch.cuda.synchronize()
     ctx.set_points_device(d_pts.data_ptr(), len(pts))  # first upload (allocations)
-    t_set = time.perf_counter()
-    ctx.set_points_device(d_pts.data_ptr(), len(pts))  # once per frame: copy (+ Hilbert sort)
-    set_points_ms = (time.perf_counter() - t_set) * 1e3
+    set_ms = []
+    for _ in range(3):  # once per frame: copy (+ Hilbert sort)
+        t_set = time.perf_counter()
+        ctx.set_points_device(d_pts.data_ptr(), len(pts))
+        set_ms.append((time.perf_counter() - t_set) * 1e3)
+    set_points_ms = float(np.median(set_ms))
     del d_pts
     n = len(pts)
-    accum = torch.zeros(1 + 6 * ctx.K, dtype=torch.float64, device=dev)
+    accum = torch.zeros(ctx.accum_len, dtype=torch.float64, device=dev)
     if args.no_per_point:
         outs = (0, 0, 0)
     else:
-        kstar = torch.empty(n, dtype=torch.int32, device=dev)
-        dd = torch.empty(n, dtype=torch.float64, device=dev)
-        gg = torch.empty((n, 3), dtype=torch.float64, device=dev)
+        kstar = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        dd = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+        gg = torch.empty((max(n, 1), 3), dtype=torch.float64, device=dev)
         outs = (kstar.data_ptr(), dd.data_ptr(), gg.data_ptr())
 
     def step(i):
@@ -168,34 +232,46 @@ def main():
     pass_ms, launches = ctx.pass_time()
     ctx.profile_pass(False)
     elapsed = max(wall, ev0.elapsed_time(ev1) / 1e3)
-    t = torch.tensor([elapsed, pass_ms / max(launches, 1)], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, pass_ms / max(launches, 1), set_points_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, pass_avg_ms = float(t[0]), float(t[1])
+    elapsed, pass_avg_ms, set_points_ms = float(t[0]), float(t[1]), float(t[2])
 
     # sanity: the last pass is finite and non-trivial
     acc = accum.cpu().numpy()
     assert np.isfinite(acc).all() and acc[0] > 0
 
+    iter_ms = None
+    if rank == 0 and world == 1 and not args.no_full_iteration:
+        ctx.set_stream(None)
+        iter_ms = full_iteration_ms(manip, ctx, q_eval)
+
     if rank == 0:
-        total_evals = n * world * args.steps
-        value = total_evals / elapsed
-        bytes_per_launch = BYTES_PER_EVAL * n if not args.no_per_point else 24 * n
+        ms_per_step = elapsed / args.steps * 1e3
+        value = global_points * args.steps / elapsed
+        tsz = 8 if args.precision == 64 else 4
+        bytes_in = 3 * tsz * n
+        bytes_per_launch = bytes_in + (0 if args.no_per_point else 36 * n)
         hbm_achieved = bytes_per_launch / (pass_avg_ms / 1e3) / 1e9
-        # F_alg per point-eval = Σ_hulls (21 + 7 F_k) + 15
-        f_alg = sum(21 + 7 * len(s.hull.faces) for s in m64.surfaces) + 15
-        flops_per_launch = f_alg * n
-        achieved = flops_per_launch / (pass_avg_ms / 1e3) / 1e12
-        peak = FP64_VALU_PEAK_TFLOPS if args.precision == 64 else FP32_VALU_PEAK_TFLOPS
-        traffic, traffic_src, executed = None, None, None
+        # F_alg per point-eval = Σ_hulls (21 + 7 F_k) + 15 (brute-force plane tests)
+        f_alg = sum(21 + 7 * len(s.hull.faces) for s in manip.surfaces) + 15
+        eff_tflops = f_alg * n / (pass_avg_ms / 1e3) / 1e12
+        peak_valu = FP64_VALU_PEAK_TFLOPS if args.precision == 64 else FP32_VALU_PEAK_TFLOPS
+        traffic, traffic_src, executed, issue = None, None, None, None
         pmc = os.path.join(ROOT, "profiles", "latest_pmc.json")
-        if os.path.exists(pmc):
+        default_run = (args.config == "m64" and scaling == "weak" and n == 1 << 20 and args.precision == 64
+                       and not args.no_cull and not args.no_sort and not args.no_per_point
+                       and args.order == "shuffled")
+        if os.path.exists(pmc) and default_run:
             with open(pmc) as f:
                 rec = json.load(f)
-            if rec.get("workload") == "bench.py default" and args.precision == 64 and not args.no_cull \
-                    and not args.no_sort and not args.no_per_point and args.order == "shuffled":
+            if rec.get("workload") == "bench.py default":
                 traffic, traffic_src = rec.get("traffic_bytes_per_launch"), rec.get("source")
                 executed = rec.get("executed")
+                if executed and executed.get("valu_insts_per_launch"):
+                    issue = executed["valu_insts_per_launch"] * CYCLES_PER_WAVE_OP / (
+                        SIMDS * CLOCK_HZ * pass_avg_ms / 1e3)
+        frame_ms = set_points_ms + ITERS_PER_FRAME * ms_per_step
         out = {
             "metric": "SDF+grad point-evals/sec, 1M-pt cloud x 64-prim model (M64)",
             "value": value,
@@ -203,37 +279,42 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f64" if args.precision == 64 else "f32",
             "data": "synthetic",
             "config": {
-                "workload": "M64: 8 IRB140 arms (7 link hulls + ATI hull each) on a 2x4 grid, 64 convex hulls, "
-                            "48 DOF; seeded synthetic depth cloud per GPU (SURVEY.md §8d generator G)",
-                "points_per_gpu": n, "global_points": n * world, "hulls": ctx.K, "dof": m64.mechanism.num_positions,
+                "workload": workload, "name": args.config,
+                "points_per_gpu": n, "global_points": global_points, "surfaces": ctx.K,
+                "dof": manip.mechanism.num_positions,
                 "input_order": args.order, "sort_points": not args.no_sort,
-                "set_points_ms_per_frame": set_points_ms,
                 "cull": not args.no_cull, "per_point_outputs": not args.no_per_point,
-                "parallelism": f"points sharded x{world}, RCCL all-reduce of {1 + 6 * ctx.K} f64 per pass",
+                "parallelism": f"points sharded x{world} ({scaling} scaling), RCCL all-reduce of "
+                               f"{ctx.accum_len} f64 per pass",
+                "set_points_ms_per_frame": set_points_ms,
+                "frame_ms_at_30_iterations": frame_ms,
+                "frame_note": "set_points (H2D-resident copy + Hilbert sort) once + 30 residual passes",
+                "full_iteration_ms": iter_ms,
+                "full_iteration_note": "CostFunctor.value_and_gradient on the resident cloud: host FK + pose "
+                                       "assembly, pass, accumulator read-back, chain rule (rank 0, N=1 only)",
             },
             "roofline": {
-                "bound": "valu", "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                "frac": achieved / peak, "traffic": traffic, "traffic_source": traffic_src,
+                "bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": hbm_achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": "pass_kernel", "kernel_ms": pass_avg_ms,
-                "flop_per_eval": f_alg, "algorithmic_flops_per_launch": flops_per_launch,
-                "hbm": {"achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": hbm_achieved / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": bytes_per_launch},
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "valu_issue_frac": issue,
+                "valu_effective": {"flop_per_eval": f_alg, "achieved_tflops": eff_tflops, "peak_tflops": peak_valu,
+                                   "ratio": eff_tflops / peak_valu,
+                                   "note": "brute-force F_alg (every plane of every hull, SURVEY.md §8d) per "
+                                           "launch / kernel time; culling skips most of it, so it can exceed 1"},
                 "executed_pmc": executed,
-                "note": "F_alg counts every plane test of all 64 hulls (the reference's brute force, SURVEY.md "
-                        "§8d); the kernel's exact-safe culling executes ~2.2 hull evaluations per 64-point "
-                        "wave, so this effective fraction can exceed 1 — executed-VALU utilisation from PMC "
-                        "is in DESIGN.md §5",
             },
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(m64, pts, q_eval, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(manip, pts, q_eval, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

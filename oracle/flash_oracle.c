@@ -416,6 +416,87 @@ static void skin_one(const oracle_posed* m, const double* p, double* d, int32_t*
   g[0] = gb[0]; g[1] = gb[1]; g[2] = gb[2];
 }
 
+/* Culled scene SDF (the CPU baseline's second leg, BASELINE.md §2 / SURVEY.md
+ * §8d "culling disabled and enabled"): the same per-surface values as
+ * skin_one, visited in order of a bounding-sphere lower bound
+ * d_k(p) >= |p − c_k| − r_k (c_k the world vertex centroid, r_k the largest
+ * vertex distance, padded), stopping once the bound exceeds the best value by
+ * a rounding margin; ties keep the smaller k whatever the visiting order, so
+ * the result equals the brute-force minimum bit for bit. RBF skins have no
+ * cheap bound and are always evaluated. */
+static void hull_spheres(const oracle_posed* m, double* sph) {
+  for (int32_t k = 0; k < m->K; ++k) {
+    double c[3] = {0, 0, 0}, r2 = 0;
+    const int v0 = m->vert_off[k], v1 = m->vert_off[k + 1];
+    for (int v = v0; v < v1; ++v)
+      for (int j = 0; j < 3; ++j) c[j] += m->verts_w[4 * v + j];
+    for (int j = 0; j < 3; ++j) c[j] /= (double)(v1 - v0);
+    for (int v = v0; v < v1; ++v) {
+      const double e2 = dist2_to(m->verts_w + 4 * v, c);
+      r2 = e2 > r2 ? e2 : r2;
+    }
+    sph[4 * k] = c[0]; sph[4 * k + 1] = c[1]; sph[4 * k + 2] = c[2];
+    sph[4 * k + 3] = sqrt(r2) * (1.0 + 1e-12) + 1e-12;
+  }
+}
+
+static void skin_one_culled(const oracle_posed* m, const double* sph, const double* p, double* d, int32_t* k,
+                            double* g) {
+  double best = INFINITY, gb[3] = {0, 0, 0};
+  int32_t bk = 0x7fffffff;
+  double lb[1024];
+  int32_t ord[1024], nh = 0;
+  for (int32_t kk = 0; kk < m->S; ++kk) {
+    const int32_t si = m->surf_index[kk];
+    double dk, gk[3];
+    if (si < 0) {
+      const int r = -si - 1, r0 = m->rbf_row_off[r];
+      oracle_rbf_skin(m->rbf_rows + 4 * r0, m->rbf_row_off[r + 1] - r0 - 1, p, &dk, gk);
+      if (dk < best || (dk == best && kk < bk)) { best = dk; bk = kk; gb[0] = gk[0]; gb[1] = gk[1]; gb[2] = gk[2]; }
+      continue;
+    }
+    const double* c = sph + 4 * si;
+    const double l = sqrt(dist2_to(p, c)) - c[3];
+    int32_t j = nh++;  /* insertion by lower bound */
+    while (j > 0 && lb[j - 1] > l) { lb[j] = lb[j - 1]; ord[j] = ord[j - 1]; --j; }
+    lb[j] = l;
+    ord[j] = kk;
+  }
+  const double mrg = 1e-9 * (1.0 + fabs(p[0]) + fabs(p[1]) + fabs(p[2]));
+  for (int32_t j = 0; j < nh; ++j) {
+    if (lb[j] - mrg > best) break;
+    const int32_t kk = ord[j];
+    double dk, gk[3];
+    oracle_hull_sdf(m, m->surf_index[kk], p, &dk, gk);
+    if (dk < best || (dk == best && kk < bk)) { best = dk; bk = kk; gb[0] = gk[0]; gb[1] = gk[1]; gb[2] = gk[2]; }
+  }
+  *d = best;
+  *k = bk == 0x7fffffff ? 0 : bk;
+  g[0] = gb[0]; g[1] = gb[1]; g[2] = gb[2];
+}
+
+/* oracle_skin with lower-bound culling (identical results; <= 1024 surfaces). */
+int32_t oracle_skin_culled(const oracle_posed* m, const double* pts, int64_t n, double* d_out, int32_t* k_out,
+                           double* g_out, int32_t threads) {
+  if (m->S > 1024) return -1;
+  double sph[4 * 1024];
+  hull_spheres(m, sph);
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 256)
+#endif
+  for (int64_t i = 0; i < n; ++i) {
+    double d, g[3];
+    int32_t k;
+    skin_one_culled(m, sph, pts + 3 * i, &d, &k, g);
+    if (d_out) d_out[i] = d;
+    if (k_out) k_out[i] = k;
+    if (g_out) { g_out[3 * i] = g[0]; g_out[3 * i + 1] = g[1]; g_out[3 * i + 2] = g[2]; }
+  }
+  (void)threads;
+  return 0;
+}
+
 /* Per-point skin over a cloud. Any output may be NULL. threads <= 0: all. */
 void oracle_skin(const oracle_posed* m, const double* pts, int64_t n, double* d_out, int32_t* k_out,
                  double* g_out, int32_t threads) {

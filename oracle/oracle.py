@@ -48,6 +48,9 @@ def load():
         lib.oracle_pose_model.argtypes = [c_int32, c_int32, c_int32] + [c_void_p] * 11
         lib.oracle_hull_sdf.argtypes = [ctypes.POINTER(Posed), c_int32, c_void_p, c_void_p, c_void_p]
         lib.oracle_skin.argtypes = [ctypes.POINTER(Posed), c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int32]
+        lib.oracle_skin_culled.argtypes = [ctypes.POINTER(Posed), c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                           c_int32]
+        lib.oracle_skin_culled.restype = c_int32
         lib.oracle_cost_accum.argtypes = [ctypes.POINTER(Posed), c_void_p, c_int64, c_void_p]
         lib.oracle_rbf_skin.argtypes = [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]
         lib.oracle_raycast.argtypes = [ctypes.POINTER(Posed), c_void_p, c_void_p, c_int64, c_void_p, c_int32]
@@ -152,14 +155,21 @@ class OracleModel:
                    rr.ctypes.data, self.faces.ctypes.data)
         return st, arrays
 
-    def skin(self, poses, pts, threads: int = 0, rbf_rows=None):
+    def skin(self, poses, pts, threads: int = 0, rbf_rows=None, culled: bool = False):
+        """Per-point (d*, k*, ∇d*). culled=True visits the hulls by a bounding-sphere
+        lower bound and stops early (same results bit for bit; the CPU baseline's
+        culled leg)."""
         pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
         st, _keep = self.pose(poses, rbf_rows)
         n = len(pts)
         d = np.empty(n)
         k = np.empty(n, np.int32)
         g = np.empty((n, 3))
-        load().oracle_skin(ctypes.byref(st), _p(pts), n, _p(d), _p(k), _p(g), threads)
+        if culled:
+            if load().oracle_skin_culled(ctypes.byref(st), _p(pts), n, _p(d), _p(k), _p(g), threads) != 0:
+                raise ValueError("oracle_skin_culled: more than 1024 surfaces")
+        else:
+            load().oracle_skin(ctypes.byref(st), _p(pts), n, _p(d), _p(k), _p(g), threads)
         return d, k, g
 
     def cost_accum(self, poses, pts, rbf_rows=None):
@@ -226,3 +236,29 @@ def numpy_hull_sdf(verts, faces, planes, pts):
         best = np.minimum(best, face_d2)
         d[out] = np.sqrt(best)
     return d
+
+
+def numpy_scene_sdf(om, poses, pts, chunk=4096):
+    """Independent scene minimum over the hulls (numpy_hull_sdf per hull), with
+    its own exact-safe pruning so that large samples stay cheap: c_k = vertex
+    centroid (inside conv(V_k), so d_k(p) <= |p − c_k|), r_k = max vertex
+    distance (d_k(p) >= |p − c_k| − r_k); hull k is evaluated for p only if
+    |p − c_k| − r_k <= min_j |p − c_j| + margin. Returns (d*, per-point minimum
+    set as a boolean matrix [n, K] of hulls within 1e-12 of d*)."""
+    pts = np.asarray(pts, np.float64).reshape(-1, 3)
+    world = [om.world_hull(poses, k) for k in range(om.K)]
+    cen = np.stack([v.mean(0) for v, _, _ in world])
+    rad = np.array([np.sqrt(((v - c) ** 2).sum(1).max()) for (v, _, _), c in zip(world, cen)])
+    n = len(pts)
+    per = np.full((n, om.K), np.inf)
+    for s in range(0, n, chunk):
+        p = pts[s:s + chunk]
+        dc = np.sqrt(((p[:, None, :] - cen[None]) ** 2).sum(-1))
+        ub = dc.min(1)
+        cand = dc - rad[None] <= ub[:, None] + 1e-9 * (1 + np.abs(p).sum(1))[:, None]
+        for k in range(om.K):
+            idx = np.nonzero(cand[:, k])[0]
+            if len(idx):
+                per[s + idx, k] = numpy_hull_sdf(*world[k], p[idx])
+    d = per.min(1)
+    return d, per <= d[:, None] + 1e-12

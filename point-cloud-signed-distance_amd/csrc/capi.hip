@@ -68,7 +68,9 @@ struct fsdf_ctx {
   int32_t* d_rbf_row_off = nullptr;
   int32_t* d_rbf_acc_off = nullptr;
   double* d_rbf64 = nullptr;     // per-pass RBF rows (f64)
-  double* h_rbf[kPoseRing] = {}; // pinned staging ring for RBF rows
+  double* h_rbf[kPoseRing] = {}; // pinned staging ring for RBF rows (own slots and events,
+  hipEvent_t rbf_ev[kPoseRing] = {};  // independent of the pose ring: poses of <= 64
+  int rbf_slot = 0;                   // surfaces never touch theirs)
   bool rbf_ready = false;
   // posed model
   fsdf::PosedModel pm;
@@ -146,9 +148,11 @@ static void free_model(fsdf_ctx* c) {
   c->pm.rbf_rows = nullptr;
   dfree(c->d_rbf64);
   for (int i = 0; i < kPoseRing; ++i) {
+    if (c->rbf_ev[i]) (void)hipEventSynchronize(c->rbf_ev[i]);
     if (c->h_rbf[i]) (void)hipHostFree(c->h_rbf[i]);
     c->h_rbf[i] = nullptr;
   }
+  c->rbf_slot = 0;
   c->rbf_ready = false;
   dfree(c->pm.verts_w);
   dfree(c->pm.hscale_w);
@@ -209,6 +213,7 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (int i = 0; i < kPoseRing; ++i) {
     if (c->pose_ev[i]) (void)hipEventDestroy(c->pose_ev[i]);
+    if (c->rbf_ev[i]) (void)hipEventDestroy(c->rbf_ev[i]);
     if (c->h_poses[i]) (void)hipHostFree(c->h_poses[i]);
   }
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -448,8 +453,10 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
     HIPCHECK(c, dalloc(&c->d_rbf64, (size_t)nrows * 4 * sizeof(double)));
     if (c->precision == 64) c->pm.rbf_rows = c->d_rbf64;
     else HIPCHECK(c, dalloc((char**)&c->pm.rbf_rows, (size_t)nrows * 4 * sizeof(float)));
-    for (int i = 0; i < kPoseRing; ++i)
+    for (int i = 0; i < kPoseRing; ++i) {
       HIPCHECK(c, hipHostMalloc((void**)&c->h_rbf[i], (size_t)nrows * 4 * sizeof(double), hipHostMallocDefault));
+      if (!c->rbf_ev[i]) HIPCHECK(c, hipEventCreateWithFlags(&c->rbf_ev[i], hipEventDisableTiming));
+    }
   }
   HIPCHECK(c, hipMemcpy(c->d_verts_l, verts.data(), verts.size() * sizeof(double), hipMemcpyHostToDevice));
   HIPCHECK(c, hipMemcpy(c->d_faces, faces.data(), faces.size() * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -515,10 +522,14 @@ extern "C" int fsdf_set_rbf_params(fsdf_ctx* c, const double* params, int64_t n)
   for (int64_t i = 0; i < n; ++i)
     if (!std::isfinite(params[i])) return fail(c, FSDF_ERR_ARG, "set_rbf_params: entry %lld not finite", (long long)i);
   HIPCHECK(c, hipSetDevice(c->device));
-  const int sl = c->pose_slot;  // shares the pose ring's slot/event (one upload pair per pass)
-  HIPCHECK(c, hipEventSynchronize(c->pose_ev[sl]));
+  // own ring: the slot is reused only after the copy that last read it ran
+  // (an asynchronous caller may queue several passes with different rows)
+  const int sl = c->rbf_slot;
+  c->rbf_slot = (sl + 1) % kPoseRing;
+  HIPCHECK(c, hipEventSynchronize(c->rbf_ev[sl]));
   memcpy(c->h_rbf[sl], params, (size_t)n * sizeof(double));
   HIPCHECK(c, hipMemcpyAsync(c->d_rbf64, c->h_rbf[sl], (size_t)n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPCHECK(c, hipEventRecord(c->rbf_ev[sl], c->stream));
   if (c->precision != 64) HIPCHECK(c, fsdf::launch_to_f32(c->d_rbf64, (float*)c->pm.rbf_rows, n, c->stream));
   c->rbf_ready = true;
   return FSDF_OK;

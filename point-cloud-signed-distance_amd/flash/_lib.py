@@ -84,6 +84,14 @@ def load() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise FlashNativeError(2, f"{LIB_PATH} not found: build it with `make -C point-cloud-signed-distance_amd/csrc`"
                                   " (or __graft_entry__.build())")
+    # ONE HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64
+    # (same soname, loaded under another name), and a process that loads ours
+    # first ends up with two runtimes, after which torch finds no GPU. With
+    # torch imported first, libflashsdf binds to the runtime torch loaded.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _PROTOS.items():
         fn = getattr(lib, name)

@@ -68,6 +68,21 @@ class ShardedCostFunctor:
         allreduce_accum(self.accum, self.group)
         return self.accum
 
+    def per_point(self, x):
+        """(k*, d*, ∇d*) of this rank's shard at x, like CostFunctor.per_point (device
+        outputs, caller order)."""
+        torch = self.torch
+        n = self.ctx.n
+        k = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)
+        d = torch.empty(max(n, 1), dtype=torch.float64, device=self.dev)
+        g = torch.empty((max(n, 1), 3), dtype=torch.float64, device=self.dev)
+        unflatten(self.state, x)
+        normalize(self.state)
+        poses, self._solves = prepare_pass(self.ctx, self.manipulator, self.state.q, self.state.deformation_data)
+        self.ctx.eval_device(poses, self.accum.data_ptr(), k.data_ptr(), d.data_ptr(), g.data_ptr())
+        allreduce_accum(self.accum, self.group)
+        return k[:n].cpu().numpy(), d[:n].cpu().numpy(), g[:n].cpu().numpy()
+
     def value_and_gradient(self, x):
         x = np.asarray(x, np.float64)
         acc = self.launch(x).cpu().numpy()

@@ -160,3 +160,60 @@ def test_manipulator_notebook_on_gpu(oracle_mod):
         c = cf(np.asarray(pin["x"]))
         assert c == pytest.approx(oc, rel=1e-9)
         assert c / pin["cost"] == pytest.approx(ratio, rel=2e-3)
+
+
+def test_async_rbf_rows_not_torn():
+    """fsdf_set_rbf_params + fsdf_eval_device queued several times with
+    different RBF rows and no host sync in between (ShardedCostFunctor's
+    pattern): each pass sees its own rows (the pinned staging slot of a row set
+    is reused only after its copy ran). Each accumulator == a synchronous
+    fsdf_eval with the same rows, bit for bit."""
+    import torch
+    z = np.load(os.path.join(GOLDEN, "c5_scene.npz"))
+    m = _scene("c5_scene")
+    c = _ctx(m)
+    c.set_points(np.concatenate([z["points"]] * 8))
+    rows0 = z["rbf_rows"]
+    variants = []
+    for j in range(12):  # > the 8-slot ring
+        r = rows0.copy()
+        r[:-1, 3] *= 1.0 + 0.01 * j  # scale the weights: a different field per pass
+        variants.append(r)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    c.set_stream(stream.cuda_stream)
+    accs = [torch.zeros(c.accum_len, dtype=torch.float64, device=dev) for _ in variants]
+    for r, a in zip(variants, accs):
+        c.set_rbf_params(r)
+        c.eval_device(z["poses"], a.data_ptr())
+    torch.cuda.synchronize()
+    got = [a.cpu().numpy() for a in accs]
+    for j, r in enumerate(variants):
+        c.set_rbf_params(r)
+        _, want, _ = c.eval(z["poses"])
+        assert np.array_equal(got[j], want), j
+    assert not np.array_equal(got[0], got[-1])
+    c.set_stream(None)
+    c.close()
+
+
+def test_c5_precision_sweep_vs_oracle():
+    """BASELINE config 5's fp32-vs-fp64 sweep (tools/precision_sweep.py) at
+    2^16 points of the deformed irb_and_squishable scene, both precisions
+    against the fp64 CPU oracle. Tolerances: f64 k*/d* exact (north-star bar:
+    k* exact, 1e-6 rel); f32 |Δd*| < 5e-5 m, k* flips on < 0.5 % of the points
+    and only at near-ties (|Δd*| < 5e-5 there), cost within 1e-4 rel, ∂c/∂x
+    within 1e-2 rel of the f64 gradient."""
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import precision_sweep
+    r = precision_sweep.sweep(1 << 16)
+    f64, f32 = r["f64"], r["f32"]
+    assert f64["max_abs_dd"] == 0.0 and f64["kstar_mismatch"] == 0
+    assert f64["cost_rel_err"] < 1e-9
+    assert f32["max_abs_dd"] < 5e-5
+    assert f32["kstar_mismatch_frac"] < 5e-3
+    assert f32.get("max_abs_dd_at_mismatch", 0.0) < 5e-5
+    assert f32["cost_rel_err"] < 1e-4
+    assert f32["dcdx_rel_err_vs_f64"] < 1e-2

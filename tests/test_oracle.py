@@ -139,3 +139,40 @@ def test_oracle_matches_numpy_on_high_valence_cone(oracle_mod):
     ref = oracle_mod.numpy_hull_sdf(*om.world_hull(pose, 0), pts)
     assert np.abs(d - ref).max() < 1e-12
     assert np.allclose(np.linalg.norm(g, axis=1), 1.0, atol=1e-12)
+
+
+def test_oracle_matches_independent_numpy_m64_large(m64, oracle_mod):
+    """40,000 shuffled M64 points (all 64 hulls in play): the C restatement ==
+    the independent numpy polytope SDF (its own pruning, no shared code) to
+    1e-12, and k* is a minimiser."""
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(m64, 21)
+    pts = synthetic.depth_cloud(m64, qt, 40000, seed=22, order="shuffled")
+    om = oracle_mod.OracleModel.from_manipulator(m64)
+    poses = _poses(m64, qe)
+    d, k, _ = om.skin(poses, pts)
+    nd, mins = oracle_mod.numpy_scene_sdf(om, poses, pts)
+    assert np.abs(d - nd).max() < 1e-12
+    assert mins[np.arange(len(pts)), k].all()
+    assert len(np.unique(k)) >= 48  # the arms' link hulls all win somewhere
+
+
+@pytest.mark.parametrize("scene", ["m64", "c5"])
+def test_oracle_culled_equals_brute_force(m64, oracle_mod, scene):
+    """The culled CPU leg (bench cpu_baseline) returns the brute-force minimum
+    bit for bit (ties to the smaller k), hull-only and with an RBF skin."""
+    from flash import synthetic
+    if scene == "m64":
+        qt, qe = synthetic.perturbed_configuration(m64, 23)
+        pts = synthetic.depth_cloud(m64, qt, 30000, seed=24, order="shuffled")
+        om = oracle_mod.OracleModel.from_manipulator(m64)
+        poses, rows = _poses(m64, qe), None
+    else:
+        from flash import Models
+        z = np.load(os.path.join(GOLDEN, "c5_scene.npz"))
+        om = oracle_mod.OracleModel.from_manipulator(Models.irb_and_squishable()[0])
+        pts, poses, rows = z["points"], z["poses"], z["rbf_rows"]
+    a = om.skin(poses, pts, rbf_rows=rows)
+    b = om.skin(poses, pts, rbf_rows=rows, culled=True)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)

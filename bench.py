@@ -79,6 +79,9 @@ def parse():
                    help="input order of the synthetic cloud (shuffled = adversarial)")
     p.add_argument("--no-sort", action="store_true", help="keep the input order resident (no Hilbert sort)")
     p.add_argument("--no-per-point", action="store_true", help="reduction-only pass (no per-point outputs)")
+    p.add_argument("--caller-order", action="store_true",
+                   help="per-point outputs scattered to the caller's order (default: resident order, coalesced; "
+                        "the permutation is fsdf_get_permutation)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of each CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-full-iteration", action="store_true")
@@ -186,6 +189,7 @@ def main():
     poses = [flash.hull_poses(manip, q_eval), flash.hull_poses(manip, q_alt)]
 
     ctx = manip.engine(device=local, precision=args.precision, cull=not args.no_cull, sort_points=not args.no_sort)
+    ctx.set_output_order(not args.caller_order)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
     d_pts = torch.as_tensor(pts, device=dev)
@@ -244,6 +248,7 @@ def main():
     iter_ms = None
     if rank == 0 and world == 1 and not args.no_full_iteration:
         ctx.set_stream(None)
+        ctx.set_output_order(False)
         iter_ms = full_iteration_ms(manip, ctx, q_eval)
 
     if rank == 0:
@@ -261,7 +266,7 @@ def main():
         pmc = os.path.join(ROOT, "profiles", "latest_pmc.json")
         default_run = (args.config == "m64" and scaling == "weak" and n == 1 << 20 and args.precision == 64
                        and not args.no_cull and not args.no_sort and not args.no_per_point
-                       and args.order == "shuffled")
+                       and args.order == "shuffled" and not args.caller_order)
         if os.path.exists(pmc) and default_run:
             with open(pmc) as f:
                 rec = json.load(f)
@@ -291,6 +296,7 @@ def main():
                 "dof": manip.mechanism.num_positions,
                 "input_order": args.order, "sort_points": not args.no_sort,
                 "cull": not args.no_cull, "per_point_outputs": not args.no_per_point,
+                "output_order": "caller" if args.caller_order else "resident (+ permutation)",
                 "parallelism": f"points sharded x{world} ({scaling} scaling), RCCL all-reduce of "
                                f"{ctx.accum_len} f64 per pass",
                 "set_points_ms_per_frame": set_points_ms,

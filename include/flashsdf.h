@@ -186,6 +186,21 @@ int fsdf_skin(fsdf_ctx* ctx, const double* poses, const double* xyz, int64_t n,
 int fsdf_raycast(fsdf_ctx* ctx, const double* poses, const double* origin, const double* rays, int64_t n,
                  double* depth_out);
 
+/* Order of the per-point outputs of fsdf_eval / fsdf_eval_device:
+ *   FSDF_ORDER_CALLER (default): output i belongs to input point i;
+ *   FSDF_ORDER_RESIDENT: output i belongs to resident point i — the device
+ *     order after fsdf_opts.sort_points (Hilbert order), written with
+ *     coalesced stores instead of a scatter through the permutation. Caller
+ *     point perm[i] (fsdf_get_permutation) is resident point i. Without
+ *     sort_points the two orders coincide. fsdf_skin always uses caller order. */
+#define FSDF_ORDER_CALLER 0
+#define FSDF_ORDER_RESIDENT 1
+int fsdf_set_output_order(fsdf_ctx* ctx, int32_t order);
+/* perm[i] = caller index of resident point i (n = fsdf_num_points int64s;
+ * identity without sort_points). Host / device destination. */
+int fsdf_get_permutation(fsdf_ctx* ctx, int64_t* perm_out);
+int fsdf_get_permutation_device(fsdf_ctx* ctx, int64_t* d_perm_out);
+
 /* Block until all work queued on the context stream has finished. */
 int fsdf_synchronize(fsdf_ctx* ctx);
 

@@ -46,6 +46,7 @@ struct fsdf_ctx {
   int precision = 64;
   int sort_points = 0;
   int cull = 1;
+  int out_order = FSDF_ORDER_CALLER;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
@@ -83,7 +84,11 @@ struct fsdf_ctx {
   int64_t n = 0;
   void* d_pts = nullptr;
   int64_t pts_cap = 0;
-  int64_t* d_perm = nullptr;
+  int32_t* d_perm = nullptr;        // resident i -> caller index (sorted clouds)
+  int64_t perm_cap = 0;
+  fsdf::SortScratch sort;            // per-frame sort scratch (grown only)
+  double* d_staging = nullptr;       // host-source clouds land here first
+  int64_t staging_cap = 0;
   // work
   double* d_partials = nullptr;
   size_t partials_cap = 0;
@@ -201,6 +206,8 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   free_model(c);
   dfree(c->d_pts);
   dfree(c->d_perm);
+  dfree(c->d_staging);
+  fsdf::free_sort_scratch(c->sort);
   dfree(c->d_partials);
   dfree(c->d_kstar);
   dfree(c->d_d);
@@ -393,8 +400,9 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
     }
     face_off.push_back((int32_t)(face_hull.size()));
   }
-  // the RBF centre rows are staged through the same buffer, 64 rows at a time at least
-  stage_bytes = (std::max(stage_bytes, 64 * 4 * tsz_) + 15) & ~15;
+  // the RBF centre rows are staged through the same buffer, 64 rows at a time
+  // at least; the resident-order gradient store transposes 64 x 3 doubles in it
+  stage_bytes = (std::max(stage_bytes, 64 * 4 * std::max(tsz_, 8)) + 15) & ~15;
   {
     fsdf::LocalModel probe;
     probe.K = K;
@@ -557,47 +565,50 @@ static int adopt_points_device(fsdf_ctx* c, const double* d_src, int64_t n, void
 static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool device_src) {
   if (!c) return FSDF_ERR_ARG;
   if (n < 0 || (n > 0 && !src)) return fail(c, FSDF_ERR_ARG, "set_points: bad buffer (n=%lld)", (long long)n);
+  if (c->sort_points && n > INT32_MAX)
+    return fail(c, FSDF_ERR_ARG, "set_points: sort_points supports < 2^31 points (n=%lld)", (long long)n);
   HIPCHECK(c, hipSetDevice(c->device));
+  // the previous frame's work may still read the staging buffer / the cloud
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   c->n = 0;
   const double* d_src = src;
-  double* staging = nullptr;
   if (!device_src && n > 0) {
-    HIPCHECK(c, hipMalloc(&staging, (size_t)n * 3 * sizeof(double)));
-    hipError_t e = hipMemcpy(staging, src, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-      (void)hipFree(staging);
-      return fail(c, FSDF_ERR_HIP, "set_points: %s", hipGetErrorString(e));
+    if (c->staging_cap < n) {
+      dfree(c->d_staging);
+      c->staging_cap = 0;
+      HIPCHECK(c, hipMalloc(&c->d_staging, (size_t)n * 3 * sizeof(double)));
+      c->staging_cap = n;
     }
-    d_src = staging;
+    HIPCHECK(c, hipMemcpyAsync(c->d_staging, src, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    d_src = c->d_staging;
   }
-  int rc = FSDF_OK;
-  dfree(c->d_perm);
   if (c->sort_points && n > 0) {
     // spatially coherent resident order + permutation back to caller order
     const size_t tsz = c->precision == 64 ? sizeof(double) : sizeof(float);
     if (c->pts_cap < n) {
       dfree(c->d_pts);
       c->pts_cap = 0;
-      hipError_t e = hipMalloc(&c->d_pts, (size_t)n * 3 * tsz);
-      if (e == hipSuccess) c->pts_cap = n;
-      else rc = fail(c, FSDF_ERR_HIP, "set_points: %s", hipGetErrorString(e));
+      HIPCHECK(c, hipMalloc(&c->d_pts, (size_t)n * 3 * tsz));
+      c->pts_cap = n;
     }
-    if (rc == FSDF_OK) {
-      hipError_t e = hipMalloc(&c->d_perm, (size_t)n * sizeof(int64_t));
-      if (e == hipSuccess) e = fsdf::sort_points_spatial(d_src, n, c->precision, c->d_pts, c->d_perm, c->stream);
-      if (e != hipSuccess) rc = fail(c, FSDF_ERR_HIP, "set_points (sort): %s", hipGetErrorString(e));
+    if (c->perm_cap < n || !c->d_perm) {
+      dfree(c->d_perm);
+      c->perm_cap = 0;
+      HIPCHECK(c, hipMalloc(&c->d_perm, (size_t)n * sizeof(int32_t)));
+      c->perm_cap = n;
     }
+    hipError_t e = fsdf::sort_points_spatial(d_src, n, c->precision, c->d_pts, c->d_perm, c->sort, c->stream);
+    if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "set_points (sort): %s", hipGetErrorString(e));
   } else {
-    rc = adopt_points_device(c, d_src, n, &c->d_pts, &c->pts_cap);
+    dfree(c->d_perm);
+    c->perm_cap = 0;
+    int rc = adopt_points_device(c, d_src, n, &c->d_pts, &c->pts_cap);
+    if (rc) return rc;
   }
-  if (rc == FSDF_OK) {
-    hipError_t e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) rc = fail(c, FSDF_ERR_HIP, "set_points: %s", hipGetErrorString(e));
-  }
-  if (staging) (void)hipFree(staging);
-  if (rc == FSDF_OK) c->n = n;
-  return rc;
+  // the caller may reuse its buffer once this returns
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  c->n = n;
+  return FSDF_OK;
 }
 
 extern "C" int fsdf_set_points(fsdf_ctx* c, const double* xyz, int64_t n) { return set_points_impl(c, xyz, n, false); }
@@ -639,7 +650,7 @@ static constexpr int kOrderEvery = FSDF_ORDER_EVERY;
 // schedule: resident-cloud passes (repeated over the same cloud) launch their
 // workgroups heaviest-first by the previous pass's durations
 static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t n, double* d_accum,
-                    int32_t* d_kstar, double* d_d, double* d_grad, const int64_t* d_perm, bool schedule) {
+                    int32_t* d_kstar, double* d_d, double* d_grad, const int32_t* d_perm, bool schedule) {
   if (c->lm.R > 0 && !c->rbf_ready)
     return fail(c, FSDF_ERR_STATE, "eval: the scene has RBF surfaces: call fsdf_set_rbf_params first");
   int rc = upload_poses(c, poses);
@@ -688,13 +699,54 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
   return FSDF_OK;
 }
 
+// per-point outputs of resident-cloud passes: scattered to caller order through
+// the sort permutation, or written in resident order (coalesced)
+static const int32_t* out_perm(const fsdf_ctx* c) { return c->out_order == FSDF_ORDER_RESIDENT ? nullptr : c->d_perm; }
+
+extern "C" int fsdf_set_output_order(fsdf_ctx* c, int32_t order) {
+  if (!c) return FSDF_ERR_ARG;
+  if (order != FSDF_ORDER_CALLER && order != FSDF_ORDER_RESIDENT)
+    return fail(c, FSDF_ERR_ARG, "set_output_order: unknown order %d", order);
+  c->out_order = order;
+  return FSDF_OK;
+}
+
+static int get_perm(fsdf_ctx* c, int64_t* out, bool device) {
+  if (!c) return FSDF_ERR_ARG;
+  if (c->n > 0 && !out) return fail(c, FSDF_ERR_ARG, "get_permutation: null output");
+  HIPCHECK(c, hipSetDevice(c->device));
+  if (c->n == 0) return FSDF_OK;
+  if (c->d_perm) {
+    std::vector<int32_t> p32;
+    if (device) {
+      HIPCHECK(c, fsdf::widen_permutation(c->d_perm, c->n, out, c->stream));
+    } else {
+      p32.resize((size_t)c->n);
+      HIPCHECK(c, hipMemcpyAsync(p32.data(), c->d_perm, (size_t)c->n * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                 c->stream));
+    }
+    HIPCHECK(c, hipStreamSynchronize(c->stream));
+    for (size_t i = 0; i < p32.size(); ++i) out[i] = p32[i];
+  } else if (device) {
+    std::vector<int64_t> id((size_t)c->n);
+    for (int64_t i = 0; i < c->n; ++i) id[(size_t)i] = i;
+    HIPCHECK(c, hipMemcpy(out, id.data(), (size_t)c->n * sizeof(int64_t), hipMemcpyHostToDevice));
+  } else {
+    for (int64_t i = 0; i < c->n; ++i) out[i] = i;
+  }
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_get_permutation(fsdf_ctx* c, int64_t* perm_out) { return get_perm(c, perm_out, false); }
+extern "C" int fsdf_get_permutation_device(fsdf_ctx* c, int64_t* d_perm_out) { return get_perm(c, d_perm_out, true); }
+
 extern "C" int fsdf_eval_device(fsdf_ctx* c, const double* poses, double* d_accum, int32_t* d_kstar, double* d_d,
                                 double* d_grad) {
   if (!c) return FSDF_ERR_ARG;
   if (c->lm.S == 0) return fail(c, FSDF_ERR_STATE, "eval: no model (call fsdf_set_model first)");
   if (!poses || !d_accum) return fail(c, FSDF_ERR_ARG, "eval_device: poses and d_accum are required");
   HIPCHECK(c, hipSetDevice(c->device));
-  return run_pass(c, poses, c->d_pts, c->n, d_accum, d_kstar, d_d, d_grad, c->d_perm, true);
+  return run_pass(c, poses, c->d_pts, c->n, d_accum, d_kstar, d_d, d_grad, out_perm(c), true);
 }
 
 static int ensure_outputs(fsdf_ctx* c, int64_t n) {
@@ -740,7 +792,7 @@ extern "C" int fsdf_eval(fsdf_ctx* c, const double* poses, double* cost_out, dou
     if (rc) return rc;
   }
   int rc = run_pass(c, poses, c->d_pts, c->n, c->d_accum, want_pp ? c->d_kstar : nullptr,
-                    want_pp ? c->d_d : nullptr, want_pp ? c->d_grad : nullptr, c->d_perm, true);
+                    want_pp ? c->d_d : nullptr, want_pp ? c->d_grad : nullptr, out_perm(c), true);
   if (rc) return rc;
   return fetch(c, c->n, cost_out, accum_out, kstar_out, d_out, grad_out, want_pp);
 }

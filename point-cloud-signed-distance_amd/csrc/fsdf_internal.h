@@ -94,7 +94,7 @@ struct PassOutputs {
   int32_t* kstar = nullptr;    // optional, caller order
   double* d = nullptr;         // optional
   double* grad = nullptr;      // optional [n][3]
-  const int64_t* perm = nullptr;  // optional: resident index -> caller index
+  const int32_t* perm = nullptr;  // optional: resident index -> caller index
   unsigned long long* stats = nullptr;  // optional kernel counters (fsdf_debug_stats)
   // optional cost-ordered schedule (resident-cloud passes): launch slot b runs
   // logical block order[b] (a permutation of [0, nblocks)); every logical block
@@ -136,9 +136,24 @@ int pass_blocks(int64_t n);
 // dynamic LDS of one pass (raycast=false) / raycast workgroup for this model
 size_t pass_lds_bytes(const LocalModel& lm, bool raycast);
 
-// Hilbert-order (sort.hip) the f64 AoS cloud d_src into d_dst (context precision) and write
-// the permutation d_perm[resident i] = caller index. Synchronizes `s`.
-hipError_t sort_points_spatial(const double* d_src, int64_t n, int precision, void* d_dst, int64_t* d_perm,
-                              hipStream_t s);
+// Scratch of the per-frame spatial sort, owned by the context and grown only
+// (a frame makes no allocation).
+struct SortScratch {
+  double* part = nullptr;  // bbox partials [256][6] + the final box [6]
+  uint32_t* k0 = nullptr;  // keys, double-buffered
+  uint32_t* k1 = nullptr;
+  int32_t* i1 = nullptr;   // alternate index buffer
+  void* tmp = nullptr;     // rocPRIM temporary storage
+  size_t part_cap = 0, k_cap0 = 0, k_cap1 = 0, i_cap1 = 0, tmp_cap = 0;
+};
+void free_sort_scratch(SortScratch& s);
+
+// Hilbert-order (sort.hip) the f64 AoS cloud d_src into d_dst (context
+// precision) and write the permutation d_perm[resident i] = caller index
+// (n < 2^31). Asynchronous on `st`.
+hipError_t sort_points_spatial(const double* d_src, int64_t n, int precision, void* d_dst, int32_t* d_perm,
+                              SortScratch& s, hipStream_t st);
+// d_out[i] = d_perm[i] as int64 (fsdf_get_permutation's layout)
+hipError_t widen_permutation(const int32_t* d_perm, int64_t n, int64_t* d_out, hipStream_t st);
 
 }  // namespace fsdf

@@ -1344,14 +1344,44 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
 
     phase_add(out.stats, 16, t_red);
     const uint64_t t_st = phase_clock();
-    if (valid && !(FSDF_ABLATE & 32)) {
-      const int64_t o = out.perm ? out.perm[i] : i;
-      if (out.kstar) out.kstar[o] = bk;
-      if (out.d) out.d[o] = (double)best;
-      if (out.grad) {
-        out.grad[3 * o + 0] = (double)gx;
-        out.grad[3 * o + 1] = (double)gy;
-        out.grad[3 * o + 2] = (double)gz;
+    if (!(FSDF_ABLATE & 32)) {
+      if (out.perm) {  // caller order: scattered through the sort permutation
+        if (valid) {
+          const int64_t o = out.perm[i];
+          if (out.kstar) out.kstar[o] = bk;
+          if (out.d) out.d[o] = (double)best;
+          if (out.grad) {
+            out.grad[3 * o + 0] = (double)gx;
+            out.grad[3 * o + 1] = (double)gy;
+            out.grad[3 * o + 2] = (double)gz;
+          }
+        }
+      } else {  // resident order: coalesced
+        if (valid) {
+          if (out.kstar) out.kstar[i] = bk;
+          if (out.d) out.d[i] = (double)best;
+        }
+        if (out.grad) {
+          // the wave's [64][3] gradient block is contiguous: transpose it
+          // through this wave's (now free) stage and store whole 16-B chunks —
+          // three strided 8-B stores per lane would each write a third of
+          // every 64-B granule (3x the bytes at the memory side)
+          double* sg = (double*)stage;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          sg[3 * lane + 0] = (double)gx;
+          sg[3 * lane + 1] = (double)gy;
+          sg[3 * lane + 2] = (double)gz;
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const int nvalid = (int)(n - base < 64 ? n - base : 64);
+          typedef double D2 __attribute__((ext_vector_type(2)));
+          D2* dst = (D2*)(out.grad + 3 * base);  // 16-B aligned: base is a multiple of 64
+          const D2* src = (const D2*)sg;
+          for (int c = lane; 2 * c < 3 * nvalid; c += 64) {
+            if (2 * c + 1 < 3 * nvalid) dst[c] = src[c];
+            else out.grad[3 * base + 2 * c] = sg[2 * c];  // odd tail (3 * nvalid odd)
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // stage reads before the next overwrite
+        }
       }
     }
     phase_add(out.stats, 17, t_st);

@@ -5,12 +5,16 @@
 // Depth sensors deliver raster order (src/depthdata.jl:19-30,
 // src/depthsensors.jl:99-113), which is already coherent; an arbitrary order
 // is made coherent here once per frame: 30-bit Hilbert keys (10 bits per axis)
-// over the cloud's bounding box, a device radix sort (rocPRIM), and a gather.
-// The permutation is kept so per-point outputs still land in the caller's
-// order. Hilbert rather than Morton order: a Morton curve jumps at every
-// octree boundary, so some 64-point chunks straddle two distant regions and
-// need the hulls of both; on the bench cloud the pass is 8.5 % faster
-// (0.144 -> 0.132 ms; -DFSDF_HILBERT=0 restores Morton keys).
+// over the cloud's bounding box, a device radix sort (rocPRIM) of (key, int32
+// index) pairs, and a gather. The permutation is kept so per-point outputs
+// still land in the caller's order. Hilbert rather than Morton order: a Morton
+// curve jumps at every octree boundary, so some 64-point chunks straddle two
+// distant regions and need the hulls of both; on the bench cloud the pass is
+// 8.5 % faster (0.144 -> 0.132 ms; -DFSDF_HILBERT=0 restores Morton keys).
+//
+// Per frame: bbox partials (<= 256 blocks) -> one-block finalize -> keys ->
+// radix sort -> gather. All scratch lives in the context (SortScratch, grown
+// only), so a frame makes no allocation and no implicit device sync.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -54,6 +58,27 @@ __global__ __launch_bounds__(kBlock) void bbox_partial_kernel(const double* __re
   if (threadIdx.x < 6) part[6 * blockIdx.x + threadIdx.x] = sh[threadIdx.x][0];
 }
 
+// one block: the <= 256 partials -> box[6] = (lo xyz, hi xyz)
+__global__ __launch_bounds__(kBlock) void bbox_final_kernel(const double* __restrict__ part, int nparts,
+                                                            double* __restrict__ box) {
+  __shared__ double sh[6][kBlock];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) sh[j][t] = t < nparts ? part[6 * t + j] : (j < 3 ? __builtin_huge_val() : -__builtin_huge_val());
+  __syncthreads();
+  for (int w = kBlock / 2; w > 0; w >>= 1) {
+    if (t < w) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        sh[j][t] = fmin(sh[j][t], sh[j][t + w]);
+        sh[3 + j][t] = fmax(sh[3 + j][t], sh[3 + j][t + w]);
+      }
+    }
+    __syncthreads();
+  }
+  if (t < 6) box[t] = sh[t][0];
+}
+
 __device__ __forceinline__ uint32_t spread10(uint32_t v) {
   v &= 0x3ff;
   v = (v | (v << 16)) & 0x030000ff;
@@ -95,26 +120,15 @@ __device__ __forceinline__ uint32_t hilbert10(const uint32_t* c) {
 }
 
 __global__ __launch_bounds__(kBlock) void curve_key_kernel(const double* __restrict__ pts, int64_t n,
-                                                        const double* __restrict__ part, int nparts,
-                                                        uint32_t* __restrict__ keys, int64_t* __restrict__ idx) {
-  __shared__ double box[6];
-  if (threadIdx.x < 6) {
-    const bool is_lo = threadIdx.x < 3;
-    double b = is_lo ? __builtin_huge_val() : -__builtin_huge_val();
-    for (int p = 0; p < nparts; ++p) {
-      const double v = part[6 * p + threadIdx.x];
-      b = is_lo ? fmin(b, v) : fmax(b, v);
-    }
-    box[threadIdx.x] = b;
-  }
-  __syncthreads();
+                                                        const double* __restrict__ box, uint32_t* __restrict__ keys,
+                                                        int32_t* __restrict__ idx) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   uint32_t q[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    const double ext = box[3 + j] - box[j];
-    const double u = ext > 0 ? (pts[3 * i + j] - box[j]) / ext : 0.0;
+    const double lo = box[j], ext = box[3 + j] - lo;
+    const double u = ext > 0 ? (pts[3 * i + j] - lo) / ext : 0.0;
     int c = (int)(u * 1024.0);
     q[j] = (uint32_t)(c < 0 ? 0 : (c > 1023 ? 1023 : c));
   }
@@ -123,12 +137,12 @@ __global__ __launch_bounds__(kBlock) void curve_key_kernel(const double* __restr
 #else
   keys[i] = spread10(q[0]) | (spread10(q[1]) << 1) | (spread10(q[2]) << 2);
 #endif
-  idx[i] = i;
+  idx[i] = (int32_t)i;
 }
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void gather_kernel(const double* __restrict__ src, int64_t n,
-                                                        const int64_t* __restrict__ order, T* __restrict__ dst) {
+                                                        const int32_t* __restrict__ order, T* __restrict__ dst) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const int64_t o = order[i];
@@ -136,49 +150,76 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const double* __restrict
   for (int j = 0; j < 3; ++j) dst[3 * i + j] = (T)src[3 * o + j];
 }
 
+__global__ __launch_bounds__(kBlock) void widen_kernel(const int32_t* __restrict__ src, int64_t n,
+                                                       int64_t* __restrict__ dst) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+
+template <typename P>
+hipError_t grow(P** p, size_t* cap, size_t need) {
+  if (*cap >= need && *p) return hipSuccess;
+  if (*p) {
+    hipError_t e = hipFree((void*)*p);
+    if (e != hipSuccess) return e;
+  }
+  *p = nullptr;
+  *cap = 0;
+  hipError_t e = hipMalloc((void**)p, need ? need : 1);
+  if (e == hipSuccess) *cap = need;
+  return e;
+}
+
 }  // namespace
 
-hipError_t sort_points_spatial(const double* d_src, int64_t n, int precision, void* d_dst, int64_t* d_perm,
-                              hipStream_t s) {
+void free_sort_scratch(SortScratch& s) {
+  if (s.part) (void)hipFree(s.part);
+  if (s.k0) (void)hipFree(s.k0);
+  if (s.k1) (void)hipFree(s.k1);
+  if (s.i1) (void)hipFree(s.i1);
+  if (s.tmp) (void)hipFree(s.tmp);
+  s = SortScratch();
+}
+
+hipError_t sort_points_spatial(const double* d_src, int64_t n, int precision, void* d_dst, int32_t* d_perm,
+                              SortScratch& s, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  double* part = nullptr;
-  uint32_t *k0 = nullptr, *k1 = nullptr;
-  int64_t* i0 = nullptr;
-  void* tmp = nullptr;
-  size_t tmp_bytes = 0;
-  hipError_t e = hipSuccess;
+  if (n > INT32_MAX) return hipErrorInvalidValue;
   const int nb = (int)std::min<int64_t>(kBoxBlocks, (n + kBlock - 1) / kBlock);
   const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
-#define FSDF_TRY(x) \
-  do {              \
-    e = (x);        \
-    if (e != hipSuccess) goto done; \
-  } while (0)
-  FSDF_TRY(hipMalloc(&part, (size_t)nb * 6 * sizeof(double)));
-  FSDF_TRY(hipMalloc(&k0, (size_t)n * sizeof(uint32_t)));
-  FSDF_TRY(hipMalloc(&k1, (size_t)n * sizeof(uint32_t)));
-  FSDF_TRY(hipMalloc(&i0, (size_t)n * sizeof(int64_t)));
-  hipLaunchKernelGGL(bbox_partial_kernel, dim3(nb), dim3(kBlock), 0, s, d_src, n, part);
-  FSDF_TRY(hipGetLastError());
-  hipLaunchKernelGGL(curve_key_kernel, dim3(grid), dim3(kBlock), 0, s, d_src, n, part, nb, k0, i0);
-  FSDF_TRY(hipGetLastError());
-  FSDF_TRY(rocprim::radix_sort_pairs(nullptr, tmp_bytes, k0, k1, i0, d_perm, (size_t)n, 0, 30, s));
-  FSDF_TRY(hipMalloc(&tmp, tmp_bytes));
-  FSDF_TRY(rocprim::radix_sort_pairs(tmp, tmp_bytes, k0, k1, i0, d_perm, (size_t)n, 0, 30, s));
+  hipError_t e;
+  if ((e = grow(&s.part, &s.part_cap, (size_t)(kBoxBlocks + 1) * 6 * sizeof(double))) != hipSuccess) return e;
+  if ((e = grow(&s.k0, &s.k_cap0, (size_t)n * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = grow(&s.k1, &s.k_cap1, (size_t)n * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = grow(&s.i1, &s.i_cap1, (size_t)n * sizeof(int32_t))) != hipSuccess) return e;
+  double* box = s.part + 6 * kBoxBlocks;
+  hipLaunchKernelGGL(bbox_partial_kernel, dim3(nb), dim3(kBlock), 0, st, d_src, n, s.part);
+  hipLaunchKernelGGL(bbox_final_kernel, dim3(1), dim3(kBlock), 0, st, s.part, nb, box);
+  // keys and the identity index go to (k0, d_perm); sorted pairs end in the
+  // double buffers' current halves
+  hipLaunchKernelGGL(curve_key_kernel, dim3(grid), dim3(kBlock), 0, st, d_src, n, box, s.k0, d_perm);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  rocprim::double_buffer<uint32_t> keys(s.k0, s.k1);
+  rocprim::double_buffer<int32_t> vals(d_perm, s.i1);
+  size_t need = 0;
+  if ((e = rocprim::radix_sort_pairs(nullptr, need, keys, vals, (size_t)n, 0, 30, st)) != hipSuccess) return e;
+  if ((e = grow((char**)&s.tmp, &s.tmp_cap, need)) != hipSuccess) return e;
+  if ((e = rocprim::radix_sort_pairs(s.tmp, need, keys, vals, (size_t)n, 0, 30, st)) != hipSuccess) return e;
+  if (vals.current() != d_perm)
+    if ((e = hipMemcpyAsync(d_perm, vals.current(), (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, st)) !=
+        hipSuccess)
+      return e;
   if (precision == 64)
-    hipLaunchKernelGGL(gather_kernel<double>, dim3(grid), dim3(kBlock), 0, s, d_src, n, d_perm, (double*)d_dst);
+    hipLaunchKernelGGL(gather_kernel<double>, dim3(grid), dim3(kBlock), 0, st, d_src, n, d_perm, (double*)d_dst);
   else
-    hipLaunchKernelGGL(gather_kernel<float>, dim3(grid), dim3(kBlock), 0, s, d_src, n, d_perm, (float*)d_dst);
-  FSDF_TRY(hipGetLastError());
-  FSDF_TRY(hipStreamSynchronize(s));
-#undef FSDF_TRY
-done:
-  if (part) (void)hipFree(part);
-  if (k0) (void)hipFree(k0);
-  if (k1) (void)hipFree(k1);
-  if (i0) (void)hipFree(i0);
-  if (tmp) (void)hipFree(tmp);
-  return e;
+    hipLaunchKernelGGL(gather_kernel<float>, dim3(grid), dim3(kBlock), 0, st, d_src, n, d_perm, (float*)d_dst);
+  return hipGetLastError();
+}
+
+hipError_t widen_permutation(const int32_t* d_perm, int64_t n, int64_t* d_out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(widen_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, d_perm, n, d_out);
+  return hipGetLastError();
 }
 
 }  // namespace fsdf

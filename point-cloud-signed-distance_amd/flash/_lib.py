@@ -64,6 +64,9 @@ _PROTOS = {
     "fsdf_eval": (c_int32, [c_void_p, c_void_p, POINTER(c_double), c_void_p, c_void_p, c_void_p, c_void_p]),
     "fsdf_eval_device": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "fsdf_skin": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "fsdf_set_output_order": (c_int32, [c_void_p, c_int32]),
+    "fsdf_get_permutation": (c_int32, [c_void_p, c_void_p]),
+    "fsdf_get_permutation_device": (c_int32, [c_void_p, c_void_p]),
     "fsdf_synchronize": (c_int32, [c_void_p]),
     "fsdf_raycast": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "fsdf_profile_pass": (c_int32, [c_void_p, c_int32]),
@@ -249,6 +252,22 @@ class Context:
         depth = np.empty(len(r), np.float64)
         check(self._lib.fsdf_raycast(self._ctx, ptr(p), ptr(o), ptr(r), len(r), ptr(depth)), self._ctx, "raycast")
         return depth
+
+    ORDER_CALLER, ORDER_RESIDENT = 0, 1
+
+    def set_output_order(self, resident: bool):
+        """Per-point outputs of eval / eval_device in resident (device, Hilbert)
+        order — coalesced stores — or in caller order (the default)."""
+        check(self._lib.fsdf_set_output_order(self._ctx, int(bool(resident))), self._ctx, "set_output_order")
+
+    def permutation(self) -> np.ndarray:
+        """perm[i] = caller index of resident point i."""
+        out = np.empty(self.n, np.int64)
+        check(self._lib.fsdf_get_permutation(self._ctx, ptr(out)), self._ctx, "get_permutation")
+        return out
+
+    def permutation_device(self, d_out: int):
+        check(self._lib.fsdf_get_permutation_device(self._ctx, c_void_p(d_out)), self._ctx, "get_permutation_device")
 
     def synchronize(self):
         check(self._lib.fsdf_synchronize(self._ctx), self._ctx, "synchronize")

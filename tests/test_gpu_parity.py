@@ -270,3 +270,40 @@ def test_cost_ordered_schedule_is_invisible(m64, oracle_mod, ctx_factory):
     for _ in range(3):
         _, acc_s, (k_s, d_s, _) = ctx.eval(poses[0], per_point=True)
         assert np.array_equal(k_s, first[0][2][0][:100003]) and np.array_equal(d_s, first[0][2][1][:100003])
+
+
+def test_resident_order_outputs(m64, oracle_mod, ctx_factory):
+    """FSDF_ORDER_RESIDENT: per-point outputs in the device (Hilbert) order,
+    coalesced; scattered through fsdf_get_permutation they are the caller-order
+    outputs bit for bit, and the accumulator does not change. Frames of other
+    sizes reuse / grow the sort scratch; device and host permutations agree."""
+    import torch
+    import flash
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(m64, 511)
+    poses = flash.hull_poses(m64, qe)
+    ctx = ctx_factory(m64, sort_points=True)
+    for n in (40009, 70001, 1000, 40009):
+        pts = synthetic.depth_cloud(m64, qt, n, seed=512 + n, order="shuffled")
+        ctx.set_points(pts)
+        ctx.set_output_order(False)
+        _, acc_c, (kc, dc, gc) = ctx.eval(poses, per_point=True)
+        ctx.set_output_order(True)
+        _, acc_r, (kr, dr, gr) = ctx.eval(poses, per_point=True)
+        perm = ctx.permutation()
+        assert np.array_equal(np.sort(perm), np.arange(n))
+        assert np.array_equal(acc_c, acc_r)
+        assert np.array_equal(kr, kc[perm]) and np.array_equal(dr, dc[perm]) and np.array_equal(gr, gc[perm])
+        dp = torch.empty(n, dtype=torch.int64, device="cuda:0")
+        ctx.permutation_device(dp.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(dp.cpu().numpy(), perm)
+    od, ok, _ = oracle_mod.OracleModel.from_manipulator(m64).skin(poses, pts)
+    assert np.array_equal(kc, ok) and np.array_equal(dc, od)
+    # without sort_points the two orders coincide and the permutation is the identity
+    plain = ctx_factory(m64)
+    plain.set_points(pts)
+    plain.set_output_order(True)
+    _, _, (k0, d0, _) = plain.eval(poses, per_point=True)
+    assert np.array_equal(plain.permutation(), np.arange(len(pts)))
+    assert np.array_equal(k0, kc) and np.array_equal(d0, dc)

@@ -96,6 +96,13 @@ class CostFunctor:
         self._resident = id(self)
         manipulator._resident_cloud = self._resident
 
+    def set_sensed_points(self, sensed_points):
+        """Swap the resident cloud (a new frame): one upload + device sort; the
+        functor, its state and the device model are kept."""
+        self.sensed_points = np.ascontiguousarray(sensed_points, np.float64).reshape(-1, 3)
+        self.ctx.set_points(self.sensed_points)
+        self.manipulator._resident_cloud = self._resident
+
     def _ensure_resident(self):
         if getattr(self.manipulator, "_resident_cloud", None) != self._resident:
             self.ctx.set_points(self.sensed_points)

@@ -1,0 +1,70 @@
+"""GPU: the track! frame loop (examples/irb_and_squishable.ipynb cells 11-12)
+on a moving IRB140 — per frame a new sensed cloud, estimate_state warm-started
+from the previous frame's solution, the resident cloud swapped in place.
+Solver kwargs as examples/irb140.ipynb cell 9 passes them (rate 20, a
+gradient-convergence tolerance); the update rule itself is unpinned
+(SimpleGradientDescent is un-vendored), so the checks are behavioural: the
+tracker follows the motion, warm starts beat cold starts, and every frame's
+cost falls."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _sequence(m, frames=12, n=4000, seed=70):
+    from flash import synthetic
+    qa, _ = synthetic.perturbed_configuration(m, seed)
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    qb = qa + rng.uniform(-0.08, 0.08, size=qa.shape)
+    qs = [qa + (qb - qa) * t / (frames - 1) for t in range(frames)]
+    clouds = [synthetic.depth_cloud(m, q, n, seed=seed + 10 + t, sigma=0.001, frac_surface=1.0, frac_box=0.0)
+              for t, q in enumerate(qs)]
+    return qs, clouds
+
+
+def test_track_follows_motion_with_warm_start():
+    import flash
+    from flash import Models
+    from flash.tracking import NaiveSolver, Tracker, track
+    from flash.gradientdescent import CostFunctor
+    m = Models.irb140()
+    qs, clouds = _sequence(m)
+    n = flash.num_states(m)
+    x0 = qs[0] + 0.05
+    state = flash.ManipulatorState(m)
+    state.q[:] = x0
+    seen = []
+    solver = NaiveSolver(n, rate=20.0, max_step=0.1, iteration_limit=30, gradient_convergence_tolerance=1e-6)
+    xs, tr = track(m, clouds, state=state, solver=solver, callback=lambda x, c: seen.append(c))
+    assert xs.shape == (len(clouds), n)
+    assert np.array_equal(state.q, xs[-1])  # unflatten!(state, x_star)
+    # the first three joints (the notebook ignores the wrist, examples/irb140.ipynb cell 9)
+    err = [np.abs(x[:3] - q[:3]).max() for x, q in zip(xs, qs)]
+    hold = np.abs(x0[:3] - qs[-1][:3]).max()  # error of not tracking at all
+    assert err[-1] < 0.5 * hold and np.mean(err) < 0.04, (err, hold)
+    # per frame the objective falls from the first to the last iteration
+    assert len(seen) == sum(tr.iterations) and tr.iteration_ms() > 0
+    k = 0
+    for its in tr.iterations:
+        assert seen[k + its - 1] <= seen[k]
+        k += its
+
+
+def test_notebook_frame_solver_single_iteration():
+    """gradient_descent!'s NaiveSolver(rate=0.5, max_step=0.1,
+    iteration_limit=1): one pass per frame, the step bounded by max_step."""
+    import flash
+    from flash import Models
+    from flash.tracking import Tracker, notebook_frame_solver
+    m = Models.irb140()
+    qs, clouds = _sequence(m, frames=3, n=2000, seed=80)
+    state = flash.ManipulatorState(m)
+    state.q[:] = qs[0] + 0.02
+    tr = Tracker(m, state, notebook_frame_solver(m))
+    prev = state.q.copy()
+    for pts in clouds:
+        x = tr.step(pts)
+        assert np.abs(x - prev).max() <= 0.1 + 1e-15
+        prev = x.copy()
+    assert tr.iterations == [1, 1, 1]

@@ -402,7 +402,8 @@ __device__ __forceinline__ bool count_events(const unsigned long long* stats) {
 // Diagnostic ablations (timing-only builds via -DFSDF_ABLATE=mask; results are
 // wrong): 4 no slow path, 16 no segmented reduction, 32 no per-point stores,
 // 64 no hull staging loads (LDS stage left as is), 128 no plane max (face 0),
-// 256 certificates skipped (stage A accepted), 512 no stage B/C.
+// 256 certificates skipped (stage A accepted), 512 no stage B/C; marginal-cost
+// doubles (same results): 65536 hull staging, 131072 fp32 screen, 262144 culling.
 #ifndef FSDF_ABLATE
 #define FSDF_ABLATE 0
 #endif
@@ -1085,6 +1086,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   // lanes (invalid lanes stand in for the first valid one)
   pxf = (float)px; pyf = (float)py; pzf = (float)pz;
   WaveSphere ws;
+  for (int rep = (FSDF_ABLATE & 262144) ? 2 : 1; rep > 0; --rep) {  // (2x: marginal-cost ablation)
   {
     const uint64_t vm = __ballot(valid);
     const int src = vm ? __builtin_ctzll(vm) : 0;
@@ -1147,6 +1149,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
         if (lb < lb_min) { lb_min = lb; kseed = k; }
       }
     }
+  }
   }
   const float ub = __builtin_sqrtf(ub2);
   phase_add(stats, 10, tc);

@@ -68,3 +68,38 @@ def test_notebook_frame_solver_single_iteration():
         assert np.abs(x - prev).max() <= 0.1 + 1e-15
         prev = x.copy()
     assert tr.iterations == [1, 1, 1]
+
+
+def test_track_lcm_log(tmp_path):
+    """examples/irb_and_squishable.ipynb cell 12 end to end: a log of
+    bot_core.pointcloud_t frames on KINECT_POINTS_REDUCED (plus an unrelated
+    channel), decoded, subsampled [1:200:end], tracked with the warm start
+    carried — identical to tracking the same clouds directly."""
+    import flash
+    from flash import Models, lcmlog
+    from flash.tracking import NaiveSolver, track
+    m = Models.irb140()
+    qs, clouds = _sequence(m, frames=4, n=40000, seed=90)
+    events = []
+    for t, c in enumerate(clouds):
+        msg = lcmlog.PointCloudMsg(utime=1000 * t, points=c, channel_names=["r", "g", "b"],
+                                   channels=np.zeros((3, len(c))))
+        events += [(1000 * t, "KINECT_POINTS_REDUCED", lcmlog.encode_pointcloud(msg)), (1000 * t + 1, "OTHER", b"x")]
+    path = tmp_path / "track.lcm"
+    lcmlog.write_log(path, events)
+    n = flash.num_states(m)
+
+    def run(frames):
+        st = flash.ManipulatorState(m)
+        st.q[:] = qs[0] + 0.03
+        return track(m, frames, state=st, solver=NaiveSolver(n, rate=20.0, max_step=0.1, iteration_limit=5))[0]
+
+    xs_log, tr = lcmlog.track_log(m, str(path), state=None, solver=NaiveSolver(n, rate=20.0, max_step=0.1,
+                                                                                 iteration_limit=5))
+    assert xs_log.shape == (4, n) and len(tr.frame_ms) == 4
+    st = flash.ManipulatorState(m)
+    st.q[:] = qs[0] + 0.03
+    xs_a, _ = lcmlog.track_log(m, str(path), state=st, solver=NaiveSolver(n, rate=20.0, max_step=0.1,
+                                                                            iteration_limit=5))
+    xs_b = run([c.astype(np.float32)[::200].astype(np.float64) for c in clouds])
+    assert np.array_equal(xs_a, xs_b)

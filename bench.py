@@ -82,6 +82,9 @@ def parse():
     p.add_argument("--caller-order", action="store_true",
                    help="per-point outputs scattered to the caller's order (default: resident order, coalesced; "
                         "the permutation is fsdf_get_permutation)")
+    p.add_argument("--split-budget", type=int, default=None,
+                   help="hull evaluations per wave before the pass splits it (fsdf_set_split_budget; 0 = never; "
+                        "default: the library's)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of each CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-full-iteration", action="store_true")
@@ -190,6 +193,8 @@ def main():
 
     ctx = manip.engine(device=local, precision=args.precision, cull=not args.no_cull, sort_points=not args.no_sort)
     ctx.set_output_order(not args.caller_order)
+    if args.split_budget is not None:
+        ctx.set_split_budget(args.split_budget)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
     d_pts = torch.as_tensor(pts, device=dev)
@@ -233,13 +238,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    pass_ms, launches = ctx.pass_time()
+    kernel_ms, pass_ms, launches = ctx.pass_times()
     ctx.profile_pass(False)
     elapsed = max(wall, ev0.elapsed_time(ev1) / 1e3)
-    t = torch.tensor([elapsed, pass_ms / max(launches, 1), set_points_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, pass_ms / max(launches, 1), set_points_ms, kernel_ms / max(launches, 1)],
+                     dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, pass_avg_ms, set_points_ms = float(t[0]), float(t[1]), float(t[2])
+    elapsed, pass_avg_ms, set_points_ms, kernel_avg_ms = float(t[0]), float(t[1]), float(t[2]), float(t[3])
 
     # sanity: the last pass is finite and non-trivial
     acc = accum.cpu().numpy()
@@ -297,6 +303,7 @@ def main():
                 "input_order": args.order, "sort_points": not args.no_sort,
                 "cull": not args.no_cull, "per_point_outputs": not args.no_per_point,
                 "output_order": "caller" if args.caller_order else "resident (+ permutation)",
+                "split_budget": args.split_budget if args.split_budget is not None else "library default (0: off)",
                 "parallelism": f"points sharded x{world} ({scaling} scaling), RCCL all-reduce of "
                                f"{ctx.accum_len} f64 per pass",
                 "set_points_ms_per_frame": set_points_ms,
@@ -309,7 +316,8 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": hbm_achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": "pass_kernel", "kernel_ms": pass_avg_ms,
+                "kernel": "pass (pass_kernel + split overflow/merge kernels)", "kernel_ms": pass_avg_ms,
+                "pass_kernel_ms": kernel_avg_ms,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "valu_issue_frac": issue,
                 "valu_effective": {"flop_per_eval": f_alg, "achieved_tflops": eff_tflops, "peak_tflops": peak_valu,

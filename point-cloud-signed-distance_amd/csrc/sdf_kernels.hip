@@ -328,6 +328,17 @@ __device__ __forceinline__ float box_lower(const HullRow& h, float x, float y, f
   return mx <= 0.0f ? mx : __builtin_sqrtf(s);
 }
 
+// Lane need test of hull k at threshold tb = min(ub, best) + margin: hull k is
+// needed unless |p-c_k| - r_k > tb (tested without a sqrt: |p-c_k|^2 <=
+// (tb + r_k)^2) or its box bound exceeds tb.
+__device__ __forceinline__ bool needs_at(const HullRow& h, float x, float y, float z, float tb) {
+  const F4 sp = h.sphere;
+  const float dx = x - sp[0], dy = y - sp[1], dz = z - sp[2];
+  const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
+  const float t = tb + sp[3];
+  return t >= 0.0f && dist2 <= t * t && box_within(h, x, y, z, tb);
+}
+
 // Bounding sphere of the wave's points (f32, wave-uniform): every valid lane's
 // point p satisfies |p - c| <= r up to f32 rounding (covered by the margins).
 struct WaveSphere {
@@ -1059,11 +1070,50 @@ __device__ __forceinline__ void rbf_adjoint(T px, T py, T pz, const T* __restric
 // gradient. Wave-cooperative (ballots, LDS staging): call with the whole wave
 // active; `valid` marks lanes whose result is used.
 // ---------------------------------------------------------------------------
-template <typename T, int SLOTS, bool CULL, bool RBF>
+// SPILL (pass kernel, SLOTS == 1, hulls only): a wave whose valid lanes have
+// more than sp->budget distinct seed hulls hands them over as one item per
+// seed group (split_wave) and returns with *spilled set; the overflow kernel
+// evaluates the groups in parallel and the merge kernel finishes the chunk.
+// Returns false (evaluate here) when the item buffer is full.
+__device__ __forceinline__ bool split_wave(uint64_t seeds, int kseed, bool valid, int64_t base,
+                                           const SpillBufs& sp) {
+  const int lane = threadIdx.x & 63;
+  const int m = __builtin_popcountll(seeds);
+  int old = 0;
+  if (lane == 0) old = atomicAdd(sp.ctr, m);
+  old = __builtin_amdgcn_readfirstlane(__shfl(old, 0, 64));
+  if (old + m > sp.cap_items) {
+    // no room: mark the reserved slots below the cap unused
+    if (lane < m && old + lane < sp.cap_items) sp.items[4 * (old + lane)] = -1;
+    return false;
+  }
+  const int64_t chunk = base >> 6;
+  int j = old;
+  for (uint64_t r = seeds; r; r &= r - 1, ++j) {
+    const int s = __builtin_ctzll(r);
+    const uint64_t mask = __ballot(valid && kseed == s);
+    if (lane == 0) {
+      int32_t* it = sp.items + 4 * j;
+      it[0] = (int32_t)chunk;
+      it[1] = s;
+      it[2] = (int32_t)(uint32_t)mask;
+      it[3] = (int32_t)(uint32_t)(mask >> 32);
+    }
+  }
+  if (lane == 0) {
+    sp.chunk_items[2 * chunk] = old;
+    sp.chunk_items[2 * chunk + 1] = m;
+  }
+  return true;
+}
+
+template <typename T, int SLOTS, bool CULL, bool RBF, bool SPILL = false>
 __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const PassModel<T>& m,
                                            const HullRow* __restrict__ ht, float smax, T* __restrict__ lw,
                                            unsigned long long* __restrict__ stats, T& best, int& bk, T& gx, T& gy,
-                                           T& gz) {
+                                           T& gz, const SpillBufs* sp = nullptr, int64_t base = 0,
+                                           bool* spilled = nullptr) {
+  static_assert(!SPILL || (SLOTS == 1 && CULL && !RBF), "split waves: culled hull-only <= 64 surfaces");
   const int K = m.K;
   const int lane = threadIdx.x & 63;
   // Phase A (fp32, exact-safe): with c_k inside hull k and r_k its bounding
@@ -1153,6 +1203,19 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   }
   const float ub = __builtin_sqrtf(ub2);
   phase_add(stats, 10, tc);
+  if (SPILL) {
+    // distinct seed hulls of the valid lanes (one wave-evaluation each)
+    uint64_t seeds = 0;
+    for (uint64_t rem = __ballot(valid); rem;) {
+      const int sd = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(rem), 64));
+      seeds |= 1ull << sd;
+      rem &= ~__ballot(valid && kseed == sd);
+    }
+    if (__builtin_popcountll(seeds) > sp->budget && split_wave(seeds, kseed, valid, base, *sp)) {
+      *spilled = true;
+      return;
+    }
+  }
   // one rounding margin per lane, >= 1e-5 x every magnitude in the test below
   const float mrg = 1e-5f * (1.0f + fabsf(pxf) + fabsf(pyf) + fabsf(pzf) + smax + 2.0f * ub);
 
@@ -1178,12 +1241,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   // tested without a sqrt: |p-c_k|^2 <= (min(ub, best) + mrg + r_k)^2
   auto needs = [&](int k) -> bool {
     if (!CULL) return valid;
-    const F4 sp = ht[k].sphere;
-    const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
-    const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
-    const float tb = fminf(ub, (float)best) + mrg;
-    const float t = tb + sp[3];
-    return valid && t >= 0.0f && dist2 <= t * t && box_within(ht[k], pxf, pyf, pzf, tb);
+    return valid && needs_at(ht[k], pxf, pyf, pzf, fminf(ub, (float)best) + mrg);
   };
   // evaluations may run out of index order: ties keep the smaller k
   auto evaluate = [&](int k, bool need) {
@@ -1244,16 +1302,115 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   if (count_events(stats) && lane == 0) atomicAdd(stats + 0, 1ull);
 }
 
+// Per-chunk epilogue (pass and merge kernels): this wave's contributions
+//   c += d^2;  F_k += 2 d g;  M_k += 2 d (p x g)   (RBF skins: adjoint sums)
+// segmented by k* (ballot loop + DPP wave sums) into the LDS rows owned by
+// lane k, then the per-point outputs. Whole wave active.
+template <typename T, int SLOTS, bool RBF>
+__device__ __forceinline__ void emit_chunk(T px, T py, T pz, bool valid, T best, int bk, T gx, T gy, T gz, int64_t i,
+                                           int64_t base, int64_t n, const PassModel<T>& m, const PassOutputs& out,
+                                           double* __restrict__ acc_row, double& cost_acc,
+                                           double* __restrict__ rbf_wave, T* __restrict__ stage, int stage_cap,
+                                           uint64_t t_iter) {
+  const int lane = threadIdx.x & 63;
+  // contributions: c += d^2; F_k += 2 d g; M_k += 2 d (p x g)
+  double cF[3] = {0.0, 0.0, 0.0}, cM[3] = {0.0, 0.0, 0.0};
+  if (valid) {
+    const double bd = (double)best;
+    const double dgx = gx, dgy = gy, dgz = gz;
+    const double dpx = px, dpy = py, dpz = pz;
+    cost_acc = __builtin_fma(bd, bd, cost_acc);
+    const double w = 2.0 * bd;
+    cF[0] = w * dgx; cF[1] = w * dgy; cF[2] = w * dgz;
+    cM[0] = w * __builtin_fma(dpy, dgz, -(dpz * dgy));
+    cM[1] = w * __builtin_fma(dpz, dgx, -(dpx * dgz));
+    cM[2] = w * __builtin_fma(dpx, dgy, -(dpy * dgx));
+  }
+  phase_add(out.stats, 18, t_iter);
+  const uint64_t t_red = phase_clock();
+  uint64_t pending = (FSDF_ABLATE & 16) ? 0 : __ballot(valid);
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const int kk = __builtin_amdgcn_readfirstlane(__shfl(bk, leader, 64));
+    const bool sel = valid && (bk == kk);
+    pending &= ~__ballot(sel);
+    if (RBF && m.surface_kind[kk] != 0) {
+      // RBF skin: adjoint sums instead of a rigid wrench
+      int r = 0;
+      while (m.rbf_surface[r] != kk) ++r;
+      const int r0 = m.rbf_row_off[r];
+      rbf_adjoint(px, py, pz, m.rbf_rows + 4 * r0, m.rbf_row_off[r + 1] - r0 - 1, stage, stage_cap, sel,
+                  rbf_wave + m.rbf_acc_off[r]);
+      continue;
+    }
+    double v[6];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) { v[j] = sel ? cF[j] : 0.0; v[3 + j] = sel ? cM[j] : 0.0; }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) v[j] = wave_sum(v[j]);
+    if (lane == (kk & 63)) {
+      double* r = acc_row + (kk >> 6) * 64 * 6;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) r[j] += v[j];
+    }
+  }
+
+  phase_add(out.stats, 16, t_red);
+  const uint64_t t_st = phase_clock();
+  if (!(FSDF_ABLATE & 32)) {
+    if (out.perm) {  // caller order: scattered through the sort permutation
+      if (valid) {
+        const int64_t o = out.perm[i];
+        if (out.kstar) out.kstar[o] = bk;
+        if (out.d) out.d[o] = (double)best;
+        if (out.grad) {
+          out.grad[3 * o + 0] = (double)gx;
+          out.grad[3 * o + 1] = (double)gy;
+          out.grad[3 * o + 2] = (double)gz;
+        }
+      }
+    } else {  // resident order: coalesced
+      if (valid) {
+        if (out.kstar) out.kstar[i] = bk;
+        if (out.d) out.d[i] = (double)best;
+      }
+      if (out.grad) {
+        // the wave's [64][3] gradient block is contiguous: transpose it
+        // through this wave's (now free) stage and store whole 16-B chunks —
+        // three strided 8-B stores per lane would each write a third of
+        // every 64-B granule (3x the bytes at the memory side)
+        double* sg = (double*)stage;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        sg[3 * lane + 0] = (double)gx;
+        sg[3 * lane + 1] = (double)gy;
+        sg[3 * lane + 2] = (double)gz;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int nvalid = (int)(n - base < 64 ? n - base : 64);
+        typedef double D2 __attribute__((ext_vector_type(2)));
+        D2* dst = (D2*)(out.grad + 3 * base);  // 16-B aligned: base is a multiple of 64
+        const D2* src = (const D2*)sg;
+        for (int c = lane; 2 * c < 3 * nvalid; c += 64) {
+          if (2 * c + 1 < 3 * nvalid) dst[c] = src[c];
+          else out.grad[3 * base + 2 * c] = sg[2 * c];  // odd tail (3 * nvalid odd)
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // stage reads before the next overwrite
+      }
+    }
+  }
+  phase_add(out.stats, 17, t_st);
+}
+
 // ---------------------------------------------------------------------------
 // Residual pass.
 // ---------------------------------------------------------------------------
 extern __shared__ __attribute__((aligned(16))) char fsdf_lds[];
 
-template <typename T, int SLOTS, bool CULL, bool RBF>
+template <typename T, int SLOTS, bool CULL, bool RBF, bool SPILL = false>
 __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)) void pass_kernel(
     const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
+  __shared__ int split_mask;  // SPILL: waves of this block that split their chunk
   // All LDS is one dynamic region (16-byte aligned carve, see pass_lds_bytes):
   //   red     [4 waves][kRedStride] f64  per-hull wrench sums + cost
   //   rbf_acc [4 waves][kMaxRbfAcc] f64  (RBF variants only)
@@ -1282,6 +1439,7 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
 #if FSDF_WAVE_TIMES
   const uint64_t t_block0 = __builtin_amdgcn_s_memrealtime();
 #endif
+  if (SPILL && threadIdx.x == 0) split_mask = 0;  // ordered by load_hull_table's barrier
   const float smax = load_hull_table(m, ht);
 #if FSDF_PHASE_TIMING
   if (lane < 10) fsdf_phase_acc[wave][lane] = 0;
@@ -1300,94 +1458,18 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
 
     T best, gx, gy, gz;
     int bk;
-    scene_eval<T, SLOTS, CULL, RBF>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz);
+    bool spilled = false;
+    scene_eval<T, SLOTS, CULL, RBF, SPILL>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz,
+                                           out.spill_dev, base, &spilled);
     if (!valid) bk = 0;
 
-    // contributions: c += d^2; F_k += 2 d g; M_k += 2 d (p x g)
-    double cF[3] = {0.0, 0.0, 0.0}, cM[3] = {0.0, 0.0, 0.0};
-    if (valid) {
-      const double bd = (double)best;
-      const double dgx = gx, dgy = gy, dgz = gz;
-      const double dpx = px, dpy = py, dpz = pz;
-      cost_acc = __builtin_fma(bd, bd, cost_acc);
-      const double w = 2.0 * bd;
-      cF[0] = w * dgx; cF[1] = w * dgy; cF[2] = w * dgz;
-      cM[0] = w * __builtin_fma(dpy, dgz, -(dpz * dgy));
-      cM[1] = w * __builtin_fma(dpz, dgx, -(dpx * dgz));
-      cM[2] = w * __builtin_fma(dpx, dgy, -(dpy * dgx));
+    if (SPILL && spilled) {
+      // the merge kernel finishes this chunk (one wave-iteration per wave)
+      if (lane == 0) atomicOr(&split_mask, 1 << wave);
+    } else {
+      emit_chunk<T, SLOTS, RBF>(px, py, pz, valid, best, bk, gx, gy, gz, i, base, n, m, out, acc_row, cost_acc,
+                                rbf_wave, stage, stage_cap, t_iter);
     }
-    phase_add(out.stats, 18, t_iter);
-    const uint64_t t_red = phase_clock();
-    uint64_t pending = (FSDF_ABLATE & 16) ? 0 : __ballot(valid);
-    while (pending) {
-      const int leader = __builtin_ctzll(pending);
-      const int kk = __builtin_amdgcn_readfirstlane(__shfl(bk, leader, 64));
-      const bool sel = valid && (bk == kk);
-      pending &= ~__ballot(sel);
-      if (RBF && m.surface_kind[kk] != 0) {
-        // RBF skin: adjoint sums instead of a rigid wrench
-        int r = 0;
-        while (m.rbf_surface[r] != kk) ++r;
-        const int r0 = m.rbf_row_off[r];
-        rbf_adjoint(px, py, pz, m.rbf_rows + 4 * r0, m.rbf_row_off[r + 1] - r0 - 1, stage, stage_cap, sel,
-                    rbf_wave + m.rbf_acc_off[r]);
-        continue;
-      }
-      double v[6];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) { v[j] = sel ? cF[j] : 0.0; v[3 + j] = sel ? cM[j] : 0.0; }
-#pragma unroll
-      for (int j = 0; j < 6; ++j) v[j] = wave_sum(v[j]);
-      if (lane == (kk & 63)) {
-        double* r = acc_row + (kk >> 6) * 64 * 6;
-#pragma unroll
-        for (int j = 0; j < 6; ++j) r[j] += v[j];
-      }
-    }
-
-    phase_add(out.stats, 16, t_red);
-    const uint64_t t_st = phase_clock();
-    if (!(FSDF_ABLATE & 32)) {
-      if (out.perm) {  // caller order: scattered through the sort permutation
-        if (valid) {
-          const int64_t o = out.perm[i];
-          if (out.kstar) out.kstar[o] = bk;
-          if (out.d) out.d[o] = (double)best;
-          if (out.grad) {
-            out.grad[3 * o + 0] = (double)gx;
-            out.grad[3 * o + 1] = (double)gy;
-            out.grad[3 * o + 2] = (double)gz;
-          }
-        }
-      } else {  // resident order: coalesced
-        if (valid) {
-          if (out.kstar) out.kstar[i] = bk;
-          if (out.d) out.d[i] = (double)best;
-        }
-        if (out.grad) {
-          // the wave's [64][3] gradient block is contiguous: transpose it
-          // through this wave's (now free) stage and store whole 16-B chunks —
-          // three strided 8-B stores per lane would each write a third of
-          // every 64-B granule (3x the bytes at the memory side)
-          double* sg = (double*)stage;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          sg[3 * lane + 0] = (double)gx;
-          sg[3 * lane + 1] = (double)gy;
-          sg[3 * lane + 2] = (double)gz;
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          const int nvalid = (int)(n - base < 64 ? n - base : 64);
-          typedef double D2 __attribute__((ext_vector_type(2)));
-          D2* dst = (D2*)(out.grad + 3 * base);  // 16-B aligned: base is a multiple of 64
-          const D2* src = (const D2*)sg;
-          for (int c = lane; 2 * c < 3 * nvalid; c += 64) {
-            if (2 * c + 1 < 3 * nvalid) dst[c] = src[c];
-            else out.grad[3 * base + 2 * c] = sg[2 * c];  // odd tail (3 * nvalid odd)
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // stage reads before the next overwrite
-        }
-      }
-    }
-    phase_add(out.stats, 17, t_st);
     phase_add(out.stats, 15, t_iter);
 #if FSDF_WAVE_TIMES
     // diagnostic: 100 MHz wall clock around each wave-iteration of the first
@@ -1426,6 +1508,10 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
     }
     out.partials[(int64_t)t * gridDim.x + lb] = s;
   }
+  if (SPILL && threadIdx.x == 0 && split_mask) {
+    out.spill_dev->blk_mask[lb] = split_mask;
+    out.spill_dev->blocks[atomicAdd(out.spill_dev->ctr + 1, 1)] = lb;
+  }
   if (out.cost && threadIdx.x == 0) out.cost[lb] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_block);
 #if FSDF_WAVE_TIMES
   if (out.stats && threadIdx.x == 0 && lb < kMaxBlocks) {  // diagnostic: block start / end (100 MHz)
@@ -1433,6 +1519,115 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
     out.stats[33 + 16 * kMaxBlocks + 2 * lb] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// Split pass, part 2: every item (chunk, seed group) handed over by the pass
+// kernel is one wave: a scene evaluation of the chunk's points restricted to
+// the group's lanes (its own wave culling, its lanes' seed first, then the
+// candidates they need), writing their final d*, k*, ∇d*. The items of a pass
+// run in parallel, so a chunk among many hulls no longer evaluates them in
+// sequence. LDS as the raycast: hull table, then one stage per wave.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBlock, kPassWavesPerSimd) void overflow_kernel(const T* __restrict__ pts, int64_t n,
+                                                                            PassModel<T> m, SpillBufs sp,
+                                                                            unsigned long long* __restrict__ stats) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  constexpr int kWaves = kBlock / 64;
+  const int count = min(sp.ctr[0], sp.cap_items);
+  if ((int)blockIdx.x * kWaves >= count) return;  // workgroup-uniform, before the table barrier
+  HullRow* ht = (HullRow*)fsdf_lds;
+  T* stage = (T*)((char*)(ht + m.K + 1) + wave * m.stage_bytes);
+  const float smax = load_hull_table(m, ht);
+  for (int it = blockIdx.x * kWaves + wave; it < count; it += gridDim.x * kWaves) {
+    const int32_t* item = sp.items + 4 * it;
+    const int chunk = __builtin_amdgcn_readfirstlane(item[0]);
+    if (chunk < 0) continue;  // a slot reserved past the capacity (never read)
+    const uint64_t mask = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(item[2]) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(item[3]) << 32);
+    const int64_t base = (int64_t)chunk * 64, i = base + lane;
+    const bool valid = ((mask >> lane) & 1) && i < n;
+    const int64_t ii = i < n ? i : n - 1;
+    const T px = pts[3 * ii + 0], py = pts[3 * ii + 1], pz = pts[3 * ii + 2];
+    T best, gx, gy, gz;
+    int bk;
+    scene_eval<T, 1, true, false>(px, py, pz, valid, m, ht, smax, stage, stats, best, bk, gx, gy, gz);
+    if (count_events(stats) && lane == 0) {
+      atomicAdd(stats + 22, 1ull);
+      atomicAdd(stats + 23, (unsigned long long)__builtin_popcountll(mask));
+    }
+    if (valid) {
+      T* r = (T*)sp.res + ((int64_t)it * 64 + lane) * 4;
+      r[0] = best;
+      r[1] = gx;
+      r[2] = gy;
+      r[3] = gz;
+      sp.res_k[(int64_t)it * 64 + lane] = bk;
+    }
+  }
+}
+
+// Split pass, part 3: one workgroup per logical block with a split wave. The
+// wave of each split chunk gathers its lanes' results from their seed-group
+// items (the same d*, k*, ∇d* as an unsplit pass), runs the chunk epilogue,
+// and the block adds its split waves' sums (fixed wave order) to the block's
+// partial column.
+template <typename T>
+__global__ __launch_bounds__(kPassBlock) void merge_kernel(const T* __restrict__ pts, int64_t n, int nblocks,
+                                                          PassModel<T> m, PassOutputs out) {
+  constexpr int kWaves = kPassBlock / 64;
+  constexpr int kRedStride = 64 * 6 + 2;
+  __shared__ double red[kWaves][kRedStride];
+  __shared__ double sgs[kWaves][192];  // per-wave gradient transpose (resident-order outputs)
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const SpillBufs& sp = out.spill;
+  const int count = sp.ctr[1];
+  for (int j = blockIdx.x; j < count; j += gridDim.x) {
+    const int lb = sp.blocks[j];
+    const int mask = sp.blk_mask[lb];
+    double* acc_row = &red[wave][lane * 6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) acc_row[q] = 0.0;
+    double cost_acc = 0.0;
+    if ((mask >> wave) & 1) {
+      const int64_t base = (int64_t)lb * kPassBlock + wave * 64, i = base + lane;
+      const bool valid = i < n;
+      const int64_t ii = valid ? i : n - 1;
+      const T px = pts[3 * ii + 0], py = pts[3 * ii + 1], pz = pts[3 * ii + 2];
+      T best = (T)0, gx = (T)0, gy = (T)0, gz = (T)0;
+      int bk = 0;
+      const int64_t chunk = base >> 6;
+      const int b0 = sp.chunk_items[2 * chunk], c = sp.chunk_items[2 * chunk + 1];
+      for (int q = 0; q < c; ++q) {  // each valid lane is in exactly one seed group
+        const int32_t* item = sp.items + 4 * (b0 + q);
+        const uint32_t w = (uint32_t)(lane < 32 ? item[2] : item[3]);
+        if ((w >> (lane & 31)) & 1) {
+          const int64_t e = (int64_t)(b0 + q) * 64 + lane;
+          const T* r = (const T*)sp.res + 4 * e;
+          best = r[0]; gx = r[1]; gy = r[2]; gz = r[3];
+          bk = sp.res_k[e];
+        }
+      }
+      if (!valid) bk = 0;
+      emit_chunk<T, 1, false>(px, py, pz, valid, best, bk, gx, gy, gz, i, base, n, m, out, acc_row, cost_acc, nullptr,
+                              (T*)sgs[wave], 0, 0);
+    }
+    cost_acc = wave_sum(cost_acc);
+    if (lane == 0) red[wave][64 * 6] = cost_acc;
+    __syncthreads();
+    const int len = 1 + 6 * m.S;
+    for (int t = threadIdx.x; t < len; t += kPassBlock) {
+      const int src = t == 0 ? 64 * 6 : t - 1;
+      double s = red[0][src];
+#pragma unroll
+      for (int w = 1; w < kWaves; ++w) s += red[w][src];
+      out.partials[(int64_t)t * nblocks + lb] += s;
+    }
+    __syncthreads();  // the rows are reused by the next block
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1563,8 +1758,9 @@ __device__ void build_order(const uint32_t* __restrict__ cost, int nb, int32_t* 
 
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict__ partials, int nblocks,
                                                         double* __restrict__ accum, const uint32_t* __restrict__ cost,
-                                                        int32_t* __restrict__ order) {
+                                                        int32_t* __restrict__ order, int32_t* __restrict__ spill_ctr) {
   const int j = blockIdx.x;
+  if (spill_ctr && j == 0 && threadIdx.x < 2) spill_ctr[threadIdx.x] = 0;  // the split pass is done with them
   if (cost && j == (int)gridDim.x - 1) {  // the extra workgroup
     build_order(cost, nblocks, order);
     return;
@@ -1675,6 +1871,12 @@ static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void
   const PassModel<T> m = pass_model<T>(lm, pm);
   const T* pts = (const T*)d_pts;
   const size_t lds = pass_lds_bytes(lm, false);
+  if constexpr (CULL && !RBF) {
+    if (lm.S <= 64 && out.spill.budget > 0) {
+      launch_lds(pass_kernel<T, 1, true, false, true>, nblocks, kPassBlock, lds, s, pts, n, m, out);
+      return;
+    }
+  }
   if (lm.S <= 64) launch_lds(pass_kernel<T, 1, CULL, RBF>, nblocks, kPassBlock, lds, s, pts, n, m, out);
   else if (lm.S <= 128) launch_lds(pass_kernel<T, 2, CULL, RBF>, nblocks, kPassBlock, lds, s, pts, n, m, out);
   else launch_lds(pass_kernel<T, 4, CULL, RBF>, nblocks, kPassBlock, lds, s, pts, n, m, out);
@@ -1691,7 +1893,12 @@ static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm,
                           int nblocks, const PassOutputs& out, hipStream_t s) {
 #if FSDF_BENCH_ONLY
   const PassModel<T> m = pass_model<T>(lm, pm);
-  launch_lds(pass_kernel<T, 1, true, false>, nblocks, kPassBlock, pass_lds_bytes(lm, false), s, (const T*)d_pts, n, m, out);
+  if (out.spill.budget > 0)
+    launch_lds(pass_kernel<T, 1, true, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false), s,
+               (const T*)d_pts, n, m, out);
+  else
+    launch_lds(pass_kernel<T, 1, true, false>, nblocks, kPassBlock, pass_lds_bytes(lm, false), s, (const T*)d_pts,
+               n, m, out);
 #else
   if (lm.R > 0) {
     if (cull) launch_pass_t<T, true, true>(lm, pm, d_pts, n, nblocks, out, s);
@@ -1712,6 +1919,36 @@ hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const Pos
   if (precision == 64) launch_pass_p<double>(cull, lm, pm, d_pts, n, nblocks, out, s);
   else launch_pass_p<float>(cull, lm, pm, d_pts, n, nblocks, out, s);
 #endif
+  return hipGetLastError();
+}
+
+bool pass_can_split(int precision, bool cull, const LocalModel& lm, int64_t n, int nblocks) {
+  (void)precision;
+  return kPassBlock == 256 && cull && lm.R == 0 && lm.K > 0 && lm.S <= 64 && n > 0 &&
+         (int64_t)nblocks * kPassBlock >= n;  // one wave-iteration per wave
+}
+
+#ifndef FSDF_OVERFLOW_BLOCKS
+#define FSDF_OVERFLOW_BLOCKS 1024
+#endif
+#ifndef FSDF_MERGE_BLOCKS
+#define FSDF_MERGE_BLOCKS 256
+#endif
+
+template <typename T>
+static void launch_split_t(const LocalModel& lm, const PosedModel& pm, const void* d_pts, int64_t n, int nblocks,
+                           const PassOutputs& out, hipStream_t s) {
+  const PassModel<T> m = pass_model<T>(lm, pm);
+  launch_lds(overflow_kernel<T>, FSDF_OVERFLOW_BLOCKS, kBlock, pass_lds_bytes(lm, true), s, (const T*)d_pts, n, m,
+             out.spill, out.stats);
+  hipLaunchKernelGGL(merge_kernel<T>, dim3(FSDF_MERGE_BLOCKS), dim3(kPassBlock), 0, s, (const T*)d_pts, n, nblocks, m,
+                     out);
+}
+
+hipError_t launch_split(int precision, const LocalModel& lm, const PosedModel& pm, const void* d_pts, int64_t n,
+                        int nblocks, const PassOutputs& out, hipStream_t s) {
+  if (precision == 64) launch_split_t<double>(lm, pm, d_pts, n, nblocks, out, s);
+  else launch_split_t<float>(lm, pm, d_pts, n, nblocks, out, s);
   return hipGetLastError();
 }
 
@@ -1752,9 +1989,9 @@ hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const 
 }
 
 hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum, hipStream_t s,
-                         const uint32_t* cost, int32_t* order) {
+                         const uint32_t* cost, int32_t* order, int32_t* spill_ctr) {
   hipLaunchKernelGGL(reduce_kernel, dim3(len + (cost ? 1 : 0)), dim3(kBlock), 0, s, partials, nblocks, d_accum,
-                     cost, order);
+                     cost, order, spill_ctr);
   return hipGetLastError();
 }
 

@@ -71,6 +71,8 @@ _PROTOS = {
     "fsdf_raycast": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "fsdf_profile_pass": (c_int32, [c_void_p, c_int32]),
     "fsdf_pass_time": (c_int32, [c_void_p, POINTER(c_double), POINTER(c_int64)]),
+    "fsdf_pass_times": (c_int32, [c_void_p, POINTER(c_double), POINTER(c_double), POINTER(c_int64)]),
+    "fsdf_set_split_budget": (c_int32, [c_void_p, c_int32]),
     "fsdf_kernel_stats": (c_int32, [c_void_p, c_int32, c_void_p]),
     "fsdf_tree_transforms": (c_int32, [c_int32] + [c_void_p] * 13),
 }
@@ -276,15 +278,27 @@ class Context:
         check(self._lib.fsdf_profile_pass(self._ctx, int(enable)), self._ctx, "profile_pass")
 
     def pass_time(self):
-        """(summed pass-kernel milliseconds, launches) since the last query."""
+        """(summed whole-pass milliseconds, launches) since the last query."""
         ms, n = c_double(0.0), c_int64(0)
         check(self._lib.fsdf_pass_time(self._ctx, ctypes.byref(ms), ctypes.byref(n)), self._ctx, "pass_time")
         return ms.value, n.value
 
+    def pass_times(self):
+        """(summed pass-kernel ms, summed whole-pass ms incl. the split kernels,
+        launches) since the last query."""
+        k, p, n = c_double(0.0), c_double(0.0), c_int64(0)
+        check(self._lib.fsdf_pass_times(self._ctx, ctypes.byref(k), ctypes.byref(p), ctypes.byref(n)), self._ctx,
+              "pass_times")
+        return k.value, p.value, n.value
+
+    def set_split_budget(self, evals: int):
+        """Hull evaluations per wave before the pass splits it (0 = never)."""
+        check(self._lib.fsdf_set_split_budget(self._ctx, int(evals)), self._ctx, "set_split_budget")
+
     STAT_NAMES = ("wave_iters", "hull_evals", "slow_waves", "lane_needs", "slow_lanes", "seed_evals",
                   "scan_waves", "full_scan_lanes", "wave_candidates", "faces_evaluated", "cyc_cull", "cyc_stage",
                   "cyc_plane", "cyc_fast", "cyc_slow", "cyc_iter", "cyc_reduce", "cyc_store", "cyc_scene",
-                  "screen_fallbacks", "screen_rejects", "walk_steps")
+                  "screen_fallbacks", "screen_rejects", "walk_steps", "split_items", "split_lanes")
 
     def kernel_stats(self, enable: bool):
         """enable=True: start counting; enable=False: stop, return the counters."""

@@ -26,6 +26,9 @@
 namespace {
 
 constexpr int kPoseRing = 8;
+#ifndef FSDF_CHUNK_WS
+#define FSDF_CHUNK_WS 1  // passes over the resident cloud read the chunk spheres of set_points
+#endif
 #ifndef FSDF_SPLIT_BUDGET
 #define FSDF_SPLIT_BUDGET 0
 #endif
@@ -91,6 +94,8 @@ struct fsdf_ctx {
   int64_t pts_cap = 0;
   int32_t* d_perm = nullptr;        // resident i -> caller index (sorted clouds)
   int64_t perm_cap = 0;
+  float* d_chunk_ws = nullptr;       // [ceil(n/64)][4] bounding sphere per 64-point chunk
+  int64_t chunk_ws_cap = 0;          // chunks
   fsdf::SortScratch sort;            // per-frame sort scratch (grown only)
   double* d_staging = nullptr;       // host-source clouds land here first
   int64_t staging_cap = 0;
@@ -223,6 +228,7 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   free_model(c);
   dfree(c->d_pts);
   dfree(c->d_perm);
+  dfree(c->d_chunk_ws);
   dfree(c->d_staging);
   fsdf::free_sort_scratch(c->sort);
   dfree(c->d_partials);
@@ -630,6 +636,17 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
     int rc = adopt_points_device(c, d_src, n, &c->d_pts, &c->pts_cap);
     if (rc) return rc;
   }
+  if (n > 0) {  // per-chunk bounding spheres of the resident order (pose-independent)
+    const int64_t nc = (n + 63) / 64;
+    if (c->chunk_ws_cap < nc) {
+      HIPCHECK(c, hipStreamSynchronize(c->stream));
+      dfree(c->d_chunk_ws);
+      c->chunk_ws_cap = 0;
+      HIPCHECK(c, hipMalloc(&c->d_chunk_ws, (size_t)nc * 4 * sizeof(float)));
+      c->chunk_ws_cap = nc;
+    }
+    HIPCHECK(c, fsdf::launch_chunk_spheres(c->precision, c->d_pts, n, c->d_chunk_ws, c->stream));
+  }
   // the caller may reuse its buffer once this returns
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   c->n = n;
@@ -732,6 +749,7 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
   out.grad = d_grad;
   out.perm = d_perm;
   out.stats = c->stats_on ? c->d_stats : nullptr;
+  out.chunk_ws = FSDF_CHUNK_WS && d_pts == c->d_pts && n == c->n ? c->d_chunk_ws : nullptr;  // resident cloud only
   if (schedule && n > 0) {
     if (!c->d_block_cost) {
       HIPCHECK(c, hipMalloc(&c->d_block_cost, fsdf::kMaxBlocks * sizeof(uint32_t)));

@@ -129,6 +129,9 @@ struct PassOutputs {
   // only on its split path (its pointers would not fit in the SGPR budget)
   SpillBufs spill;
   const SpillBufs* spill_dev = nullptr;
+  // optional [n64/64][4] f32 bounding sphere of each 64-point chunk of the
+  // resident cloud (launch_chunk_spheres at set_points; pose-independent)
+  const float* chunk_ws = nullptr;
 };
 
 // Surfaces whose poses ride in the pose kernel's arguments (12·64 doubles =
@@ -163,6 +166,10 @@ hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d
                          int32_t* spill_ctr = nullptr);
 
 hipError_t launch_to_f32(const double* src, float* dst, int64_t count, hipStream_t s);
+
+// per-chunk (64 points) bounding spheres of a resident cloud of the context
+// precision -> d_out [ceil(n/64)][4] f32 (the pass kernel's wave culling input)
+hipError_t launch_chunk_spheres(int precision, const void* d_pts, int64_t n, float* d_out, hipStream_t s);
 
 int pass_blocks(int64_t n);
 

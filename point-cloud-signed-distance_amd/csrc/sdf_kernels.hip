@@ -418,6 +418,13 @@ __device__ __forceinline__ bool count_events(const unsigned long long* stats) {
 #ifndef FSDF_ABLATE
 #define FSDF_ABLATE 0
 #endif
+// Per-hull wrench sums by LDS f64 atomics (1) or by the segmented ballot loop
+// with DPP wave sums (0). The atomics free ~150 VALU instructions per wave but
+// serialize a wave's 64 same-row adds in the LDS: measured 12 % slower (M64,
+// 2^20 points), so the loop stays.
+#ifndef FSDF_LDS_ATOMIC_SUMS
+#define FSDF_LDS_ATOMIC_SUMS 0
+#endif
 #ifndef FSDF_PASS_WAVES_PER_SIMD
 #define FSDF_PASS_WAVES_PER_SIMD 4
 #endif
@@ -998,6 +1005,36 @@ __device__ __forceinline__ float wave_minmax(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// Bounding sphere (bbox centre, half diagonal) of the wave's valid lanes'
+// points (invalid lanes stand in for the first valid one). Whole wave active.
+__device__ __forceinline__ WaveSphere wave_sphere(float pxf, float pyf, float pzf, bool valid) {
+  const uint64_t vm = __ballot(valid);
+  const int src = vm ? __builtin_ctzll(vm) : 0;
+  float qx = pxf, qy = pyf, qz = pzf;
+  if (!valid) { qx = __shfl(pxf, src, 64); qy = __shfl(pyf, src, 64); qz = __shfl(pzf, src, 64); }
+  const float lx = wave_minmax<false>(qx), ly = wave_minmax<false>(qy), lz = wave_minmax<false>(qz);
+  const float hx = wave_minmax<true>(qx), hy = wave_minmax<true>(qy), hz = wave_minmax<true>(qz);
+  const float ex = hx - lx, ey = hy - ly, ez = hz - lz;
+  WaveSphere ws;
+  ws.x = 0.5f * (lx + hx); ws.y = 0.5f * (ly + hy); ws.z = 0.5f * (lz + hz);
+  ws.r = 0.5f * __builtin_sqrtf(__builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez)));
+  return ws;
+}
+
+// Per-chunk bounding spheres of a resident cloud (one wave per 64 points),
+// read by the pass kernel instead of recomputing them every pass.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void chunk_sphere_kernel(const T* __restrict__ pts, int64_t n,
+                                                              F4* __restrict__ out) {
+  const int64_t base = ((int64_t)blockIdx.x * kBlock + threadIdx.x) & ~(int64_t)63;
+  if (base >= n) return;  // wave-uniform
+  const int64_t i = base + (threadIdx.x & 63);
+  const bool valid = i < n;
+  const int64_t ii = valid ? i : n - 1;
+  const WaveSphere ws = wave_sphere((float)pts[3 * ii], (float)pts[3 * ii + 1], (float)pts[3 * ii + 2], valid);
+  if ((threadIdx.x & 63) == 0) out[base >> 6] = F4{ws.x, ws.y, ws.z, ws.r};
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
   if (!FSDF_DPP_SUM) {
 #pragma unroll
@@ -1111,7 +1148,8 @@ template <typename T, int SLOTS, bool CULL, bool RBF, bool SPILL = false>
 __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const PassModel<T>& m,
                                            const HullRow* __restrict__ ht, float smax, T* __restrict__ lw,
                                            unsigned long long* __restrict__ stats, T& best, int& bk, T& gx, T& gy,
-                                           T& gz, const SpillBufs* sp = nullptr, int64_t base = 0,
+                                           T& gz, const F4* __restrict__ cws = nullptr,
+                                           const SpillBufs* sp = nullptr, int64_t base = 0,
                                            bool* spilled = nullptr) {
   static_assert(!SPILL || (SLOTS == 1 && CULL && !RBF), "split waves: culled hull-only <= 64 surfaces");
   const int K = m.K;
@@ -1133,20 +1171,16 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   }
   const uint64_t tc = phase_clock();
   // the wave's bounding sphere (bbox centre, half diagonal) over the valid
-  // lanes (invalid lanes stand in for the first valid one)
+  // lanes: precomputed per resident chunk at set_points (pose-independent,
+  // the same arithmetic) or computed here
   pxf = (float)px; pyf = (float)py; pzf = (float)pz;
   WaveSphere ws;
   for (int rep = (FSDF_ABLATE & 262144) ? 2 : 1; rep > 0; --rep) {  // (2x: marginal-cost ablation)
-  {
-    const uint64_t vm = __ballot(valid);
-    const int src = vm ? __builtin_ctzll(vm) : 0;
-    float qx = pxf, qy = pyf, qz = pzf;
-    if (!valid) { qx = __shfl(pxf, src, 64); qy = __shfl(pyf, src, 64); qz = __shfl(pzf, src, 64); }
-    const float lx = wave_minmax<false>(qx), ly = wave_minmax<false>(qy), lz = wave_minmax<false>(qz);
-    const float hx = wave_minmax<true>(qx), hy = wave_minmax<true>(qy), hz = wave_minmax<true>(qz);
-    const float ex = hx - lx, ey = hy - ly, ez = hz - lz;
-    ws.x = 0.5f * (lx + hx); ws.y = 0.5f * (ly + hy); ws.z = 0.5f * (lz + hz);
-    ws.r = 0.5f * __builtin_sqrtf(__builtin_fmaf(ex, ex, __builtin_fmaf(ey, ey, ez * ez)));
+  if (cws) {
+    const F4 v = *cws;
+    ws = WaveSphere{v[0], v[1], v[2], v[3]};
+  } else {
+    ws = wave_sphere(pxf, pyf, pzf, valid);
   }
   if (CULL) {
     // Wave-level culling, one hull per lane: with the wave's points inside the
@@ -1328,7 +1362,24 @@ __device__ __forceinline__ void emit_chunk(T px, T py, T pz, bool valid, T best,
   }
   phase_add(out.stats, 18, t_iter);
   const uint64_t t_red = phase_clock();
+#if FSDF_LDS_ATOMIC_SUMS
+  // Hull surfaces: every valid lane adds its wrench into the LDS row of its
+  // k* (ds_add_f64; lanes of one k* are applied in lane order by the LDS, so
+  // the sums are deterministic); only RBF skins take the segmented loop.
+  bool hull_lane = valid && !(FSDF_ABLATE & 16);
+  if (RBF) hull_lane = hull_lane && m.surface_kind[bk] == 0;
+  if (hull_lane) {
+    double* r = acc_row - lane * 6 + (bk >> 6) * 64 * 6 + (bk & 63) * 6;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      __hip_atomic_fetch_add(r + j, cF[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(r + 3 + j, cM[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  uint64_t pending = RBF ? __ballot(valid && !hull_lane && !(FSDF_ABLATE & 16)) : 0ull;
+#else
   uint64_t pending = (FSDF_ABLATE & 16) ? 0 : __ballot(valid);
+#endif
   while (pending) {
     const int leader = __builtin_ctzll(pending);
     const int kk = __builtin_amdgcn_readfirstlane(__shfl(bk, leader, 64));
@@ -1459,8 +1510,9 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
     T best, gx, gy, gz;
     int bk;
     bool spilled = false;
+    const F4* cws = out.chunk_ws ? (const F4*)out.chunk_ws + (base >> 6) : nullptr;
     scene_eval<T, SLOTS, CULL, RBF, SPILL>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz,
-                                           out.spill_dev, base, &spilled);
+                                           cws, out.spill_dev, base, &spilled);
     if (!valid) bk = 0;
 
     if (SPILL && spilled) {
@@ -1992,6 +2044,18 @@ hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d
                          const uint32_t* cost, int32_t* order, int32_t* spill_ctr) {
   hipLaunchKernelGGL(reduce_kernel, dim3(len + (cost ? 1 : 0)), dim3(kBlock), 0, s, partials, nblocks, d_accum,
                      cost, order, spill_ctr);
+  return hipGetLastError();
+}
+
+hipError_t launch_chunk_spheres(int precision, const void* d_pts, int64_t n, float* d_out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
+  if (precision == 64)
+    hipLaunchKernelGGL(chunk_sphere_kernel<double>, dim3(grid), dim3(kBlock), 0, s, (const double*)d_pts, n,
+                       (F4*)d_out);
+  else
+    hipLaunchKernelGGL(chunk_sphere_kernel<float>, dim3(grid), dim3(kBlock), 0, s, (const float*)d_pts, n,
+                       (F4*)d_out);
   return hipGetLastError();
 }
 

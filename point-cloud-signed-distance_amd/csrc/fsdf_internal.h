@@ -29,7 +29,7 @@
 //                               b = 2j+1 (= a when nf is odd and j is the last pair),
 //                               d' = d - n·c with c the hull's f32 sphere centre
 //
-//   per-block partial sums  partials [1+6K][nblocks] f64 (column = block)
+//   per-block partial sums  partials [len][nblocks] f64, len = 1+6S+Σ(4n+4) (column = block)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -112,7 +112,7 @@ struct SpillBufs {
 };
 
 struct PassOutputs {
-  double* partials = nullptr;  // [1+6K][nblocks]
+  double* partials = nullptr;  // [len][nblocks] (sdf_kernels.hip pidx)
   int32_t* kstar = nullptr;    // optional, caller order
   double* d = nullptr;         // optional
   double* grad = nullptr;      // optional [n][3]

@@ -1451,6 +1451,19 @@ __device__ __forceinline__ void emit_chunk(T px, T py, T pz, bool valid, T best,
   phase_add(out.stats, 17, t_st);
 }
 
+// Per-block partial sums: entry t of logical block b. Entry-major (each
+// entry's column of blocks contiguous: the reduce kernel's reads coalesce) or
+// block-major (each workgroup writes its len sums as one contiguous row).
+// Block-major writes whole 64-B lines — WRITE_SIZE 88.6 -> 50.6 MB per M64
+// pass, pass kernel -2.2 % — but the reduce then reads strided: +10 us per
+// step (measured, profiles/r02). Entry-major stays.
+#ifndef FSDF_PARTIALS_BLOCK_MAJOR
+#define FSDF_PARTIALS_BLOCK_MAJOR 0
+#endif
+__device__ __forceinline__ int64_t pidx(int t, int b, int len, int nblocks) {
+  return FSDF_PARTIALS_BLOCK_MAJOR ? (int64_t)b * len + t : (int64_t)t * nblocks + b;
+}
+
 // ---------------------------------------------------------------------------
 // Residual pass.
 // ---------------------------------------------------------------------------
@@ -1558,7 +1571,7 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
 #pragma unroll
       for (int w = 1; w < kPassBlock / 64; ++w) s += rbf_acc[w * kMaxRbfAcc + src];
     }
-    out.partials[(int64_t)t * gridDim.x + lb] = s;
+    out.partials[pidx(t, lb, len, gridDim.x)] = s;
   }
   if (SPILL && threadIdx.x == 0 && split_mask) {
     out.spill_dev->blk_mask[lb] = split_mask;
@@ -1676,7 +1689,7 @@ __global__ __launch_bounds__(kPassBlock) void merge_kernel(const T* __restrict__
       double s = red[0][src];
 #pragma unroll
       for (int w = 1; w < kWaves; ++w) s += red[w][src];
-      out.partials[(int64_t)t * nblocks + lb] += s;
+      out.partials[pidx(t, lb, len, nblocks)] += s;
     }
     __syncthreads();  // the rows are reused by the next block
   }
@@ -1808,7 +1821,7 @@ __device__ void build_order(const uint32_t* __restrict__ cost, int nb, int32_t* 
   }
 }
 
-__global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict__ partials, int nblocks,
+__global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict__ partials, int nblocks, int len,
                                                         double* __restrict__ accum, const uint32_t* __restrict__ cost,
                                                         int32_t* __restrict__ order, int32_t* __restrict__ spill_ctr) {
   const int j = blockIdx.x;
@@ -1817,16 +1830,16 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict
     build_order(cost, nblocks, order);
     return;
   }
-  const double* row = partials + (int64_t)j * nblocks;
+  auto at = [&](int b) { return partials[pidx(j, b, len, nblocks)]; };
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   int b = threadIdx.x;
   for (; b + 3 * kBlock < nblocks; b += 4 * kBlock) {
-    s0 += row[b];
-    s1 += row[b + kBlock];
-    s2 += row[b + 2 * kBlock];
-    s3 += row[b + 3 * kBlock];
+    s0 += at(b);
+    s1 += at(b + kBlock);
+    s2 += at(b + 2 * kBlock);
+    s3 += at(b + 3 * kBlock);
   }
-  for (; b < nblocks; b += kBlock) s0 += row[b];
+  for (; b < nblocks; b += kBlock) s0 += at(b);
   double s = wave_sum((s0 + s1) + (s2 + s3));
   __shared__ double sh[kBlock / 64];
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
@@ -2042,7 +2055,7 @@ hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const 
 
 hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum, hipStream_t s,
                          const uint32_t* cost, int32_t* order, int32_t* spill_ctr) {
-  hipLaunchKernelGGL(reduce_kernel, dim3(len + (cost ? 1 : 0)), dim3(kBlock), 0, s, partials, nblocks, d_accum,
+  hipLaunchKernelGGL(reduce_kernel, dim3(len + (cost ? 1 : 0)), dim3(kBlock), 0, s, partials, nblocks, len, d_accum,
                      cost, order, spill_ctr);
   return hipGetLastError();
 }

@@ -426,7 +426,9 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
       // pairs, 32 B per two faces) and vertex rows of 4 T, one 16-byte face row
       // per face (M64 f64: 4864 B; 4 waves + the wrench rows + the hull table
       // stay under 40 KiB, i.e. 4 workgroups per CU)
-      const int plane_bytes = (tsz_ == 8 && FSDF_SCREEN32) ? 32 * ((h.n_faces + 1) / 2) : h.n_faces * 4 * tsz_;
+      const int plane_bytes = (tsz_ == 8 && FSDF_SCREEN32)
+                                  ? 32 * ((h.n_faces + 1) / 2) + (FSDF_STAGE_PLANES64 ? h.n_faces * 32 : 0)
+                                  : h.n_faces * 4 * tsz_;
       stage_bytes = std::max(stage_bytes, plane_bytes + h.n_vertices * 4 * tsz_ + 16 * h.n_faces);
     }
     face_off.push_back((int32_t)(face_hull.size()));

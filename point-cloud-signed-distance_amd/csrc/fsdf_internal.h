@@ -42,6 +42,11 @@ namespace fsdf {
 #ifndef FSDF_SCREEN32
 #define FSDF_SCREEN32 1
 #endif
+// f64 contexts stage the fp64 planes too (fix-up, max face, certificates read
+// LDS instead of L1/L2); sizes the stage in fsdf_set_surfaces
+#ifndef FSDF_STAGE_PLANES64
+#define FSDF_STAGE_PLANES64 0
+#endif
 
 constexpr int kBlock = 256;
 #ifndef FSDF_PASS_BLOCK

@@ -452,10 +452,12 @@ __device__ __forceinline__ void stage_rows(T* __restrict__ lds, const T* __restr
 constexpr int kPlaneBatch = FSDF_PLANE_BATCH;  // plane rows per LDS batch (power of 2, >= 2)
 constexpr int kWalkSteps = 24;  // descent-walk cap before the exhaustive stage C
 
-// Three consecutive regions of 16-byte chunks: n0 from s0, n1 from s1, n2 from s2.
+// Consecutive regions of 16-byte chunks: n0 from s0, n1 from s1, n2 from s2,
+// n3 from s3.
 __device__ __forceinline__ void stage_hull(void* __restrict__ lw, const I4* __restrict__ s0, int n0,
-                                           const I4* __restrict__ s1, int n1, const I4* __restrict__ s2, int n2) {
-  const int P = n0, Q = P + n1, N = Q + n2;
+                                           const I4* __restrict__ s1, int n1, const I4* __restrict__ s2, int n2,
+                                           const I4* __restrict__ s3 = nullptr, int n3 = 0) {
+  const int P = n0, Q = P + n1, N3 = Q + n2, N = N3 + n3;
   const int lane = threadIdx.x & 63;
   I4* dst = (I4*)lw;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -464,7 +466,7 @@ __device__ __forceinline__ void stage_hull(void* __restrict__ lw, const I4* __re
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = min(c0 + 64 * j + lane, N - 1);
-      const I4* src = c < P ? s0 + c : (c < Q ? s1 + (c - P) : s2 + (c - Q));
+      const I4* src = c < P ? s0 + c : (c < Q ? s1 + (c - P) : (c < N3 ? s2 + (c - Q) : s3 + (c - N3)));
       if (!(FSDF_ABLATE & 64)) v[j] = *src;
       else v[j] = I4{c, c, c, 0};
     }
@@ -592,6 +594,17 @@ __device__ __forceinline__ bool cert_step(T px, T py, T pz, int f, int reg,
 // ---------------------------------------------------------------------------
 template <typename T>
 constexpr bool kStagePairs = sizeof(T) == 8 && FSDF_SCREEN32;
+// Seed phase: skip seeds no lane needs any more (1); take the seed shared by
+// the most pending lanes first (1) instead of the first pending lane's (0).
+#ifndef FSDF_SEED_SKIP
+#define FSDF_SEED_SKIP 1
+#endif
+#ifndef FSDF_SEED_ORDER
+#define FSDF_SEED_ORDER 1
+#endif
+#ifndef FSDF_SCREEN_INTERLEAVE
+#define FSDF_SCREEN_INTERLEAVE 0
+#endif
 #ifndef FSDF_SCREEN_ILP
 #define FSDF_SCREEN_ILP 4
 #endif
@@ -622,6 +635,20 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
       c[2 * q] = ls[2 * j];
       c[2 * q + 1] = ls[2 * j + 1];
     }
+#if FSDF_SCREEN_INTERLEAVE
+    // the four pairs' fma chains advanced stage by stage (independent
+    // neighbours: no dependent back-to-back packed ops); same operations
+    F2v h[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) h[q] = __builtin_elementwise_fma(F2v{c[2 * q + 1][0], c[2 * q + 1][1]}, qz2,
+                                                                 F2v{c[2 * q + 1][2], c[2 * q + 1][3]});
+#pragma unroll
+    for (int q = 0; q < 4; ++q) h[q] = __builtin_elementwise_fma(F2v{c[2 * q][2], c[2 * q][3]}, qy2, h[q]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) h[q] = __builtin_elementwise_fma(F2v{c[2 * q][0], c[2 * q][1]}, qx2, h[q]);
+    return fmaxf(fmaxf(fmaxf(h[0][0], h[0][1]), fmaxf(h[1][0], h[1][1])),
+                 fmaxf(fmaxf(h[2][0], h[2][1]), fmaxf(h[3][0], h[3][1])));
+#else
     float hm[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -631,6 +658,7 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
       hm[q] = fmaxf(h[0], h[1]);
     }
     return fmaxf(fmaxf(hm[0], hm[1]), fmaxf(hm[2], hm[3]));
+#endif
   };
   auto update = [&](float mb, int i) {
     b2 = fmaxf(b2, fminf(b1, mb));
@@ -708,12 +736,16 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   constexpr int cpr = (int)sizeof(T) / 4;  // 16-byte chunks per row of 4 T
   const int np2 = kStagePairs<T> ? 2 * ((nf + 1) >> 1) : nf * cpr;  // chunks of region 0
   const I4* src0 = kStagePairs<T> ? (const I4*)(m.screen + 4 * (f0 + k)) : (const I4*)(m.planes + 4 * f0);
+  // FSDF_STAGE_PLANES64: f64 contexts also stage the fp64 planes (after the pairs)
+  constexpr bool kP64 = kStagePairs<T> && FSDF_STAGE_PLANES64;
+  const int npl = kP64 ? nf * cpr : 0;
   for (int rep = (FSDF_ABLATE & 65536) ? 2 : 1; rep > 0; --rep)  // (2x: marginal-cost ablation)
-    stage_hull(lw, src0, np2, (const I4*)(m.verts + 4 * v0), nv * cpr, m.face_rows + f0, nf);
+    stage_hull(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0), nv * cpr,
+               m.face_rows + f0, nf);
   phase_add(stats, 11, tp);
   tp = phase_clock();
-  const R* lp = kStagePairs<T> ? (const R*)(m.planes + 4 * f0) : (const R*)lw;
-  const R* lv = (const R*)((const I4*)lw + np2);
+  const R* lp = kP64 ? (const R*)((const I4*)lw + np2) : (kStagePairs<T> ? (const R*)(m.planes + 4 * f0) : (const R*)lw);
+  const R* lv = (const R*)((const I4*)lw + np2 + npl);
   const I4* lf = (const I4*)(lv + nv);
   const T scale = (T)ht[k].hscale;
   const CRow<T> gp = scalar_rows<T>(m.planes + 4 * f0);  // uniform plane rows (SGPR)
@@ -1308,16 +1340,35 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     int k;
     bool need;
     if (pend) {
-      k = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(pend), 64));
-      pend &= ~__ballot(valid && kseed == k);
+      uint64_t grp;
+      if (FSDF_SEED_ORDER) {
+        // the pending seed shared by the most lanes first (tightens the most bounds)
+        k = 0;
+        grp = 0;
+        int most = -1;
+        for (uint64_t r = pend; r;) {
+          const int sk = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(r), 64));
+          const uint64_t g = __ballot(valid && kseed == sk);
+          r &= ~g;
+          const int c = __builtin_popcountll(g);
+          if (c > most) { most = c; k = sk; grp = g; }
+        }
+      } else {
+        k = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(pend), 64));
+        grp = __ballot(valid && kseed == k);
+      }
+      pend &= ~grp;
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s)
         if ((k >> 6) == s) done[s] |= 1ull << (k & 63);
+      need = needs(k);
+      // a seed no lane needs any more (earlier evaluations tightened the
+      // bounds) is skipped; bounds only tighten, so it is done for good
+      if (FSDF_SEED_SKIP && !__any(need)) continue;
       if (count_events(stats) && lane == 0) atomicAdd(stats + 5, 1ull);
 #if FSDF_WAVE_TIMES
       if (lane == 0) ++fsdf_wave_ev[threadIdx.x >> 6][1];
 #endif
-      need = needs(k);
     } else {
       while (!cm && slot < SLOTS - 1) {
         ++slot;

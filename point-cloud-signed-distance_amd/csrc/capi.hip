@@ -81,8 +81,15 @@ struct fsdf_ctx {
   hipEvent_t rbf_ev[kPoseRing] = {};  // independent of the pose ring: poses of <= 64
   int rbf_slot = 0;                   // surfaces never touch theirs)
   bool rbf_ready = false;
-  // posed model
+  // posed model, double-buffered: pass i poses into buffer i % 2 on its own
+  // stream while the context stream still runs pass i-1 / its reduce
+  // (FSDF_POSE_OVERLAP); ev_pm_free[b] marks the last read of buffer b
   fsdf::PosedModel pm;
+  fsdf::PosedModel pm_alt;
+  int pm_next = 0;
+  hipStream_t pose_stream = nullptr;
+  hipEvent_t ev_pose = nullptr;
+  hipEvent_t ev_pm_free[2] = {};
   // poses: pinned ring + device copy
   double* h_poses[kPoseRing] = {};
   hipEvent_t pose_ev[kPoseRing] = {};
@@ -181,11 +188,16 @@ static void free_model(fsdf_ctx* c) {
   }
   c->rbf_slot = 0;
   c->rbf_ready = false;
-  dfree(c->pm.verts_w);
-  dfree(c->pm.hscale_w);
-  dfree(c->pm.planes_w);
-  dfree(c->pm.spheres_w);
-  dfree(c->pm.screen_w);
+  if (c->pose_stream) (void)hipStreamSynchronize(c->pose_stream);
+  for (fsdf::PosedModel* P : {&c->pm, &c->pm_alt}) {
+    dfree(P->verts_w);
+    dfree(P->hscale_w);
+    dfree(P->planes_w);
+    dfree(P->spheres_w);
+    dfree(P->screen_w);
+  }
+  c->pm_alt.rbf_rows = nullptr;
+  c->pm_next = 0;
   dfree(c->d_poses);
   dfree(c->d_accum);
   c->lm = fsdf::LocalModel();
@@ -217,6 +229,14 @@ extern "C" int fsdf_create(fsdf_ctx** out, const fsdf_opts* opts) {
   }
   c->stream = c->own_stream;
   for (int i = 0; i < kPoseRing; ++i) c->pose_ev[i] = nullptr;
+  if (hipStreamCreateWithFlags(&c->pose_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_pose, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_pm_free[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_pm_free[1], hipEventDisableTiming) != hipSuccess) {
+    (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return FSDF_ERR_HIP;
+  }
   *out = c;
   return FSDF_OK;
 }
@@ -225,6 +245,7 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   if (!c) return FSDF_ERR_ARG;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->pose_stream) (void)hipStreamSynchronize(c->pose_stream);
   free_model(c);
   dfree(c->d_pts);
   dfree(c->d_perm);
@@ -255,6 +276,10 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
     if (c->h_poses[i]) (void)hipHostFree(c->h_poses[i]);
   }
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  if (c->pose_stream) (void)hipStreamDestroy(c->pose_stream);
+  if (c->ev_pose) (void)hipEventDestroy(c->ev_pose);
+  for (hipEvent_t e : c->ev_pm_free)
+    if (e) (void)hipEventDestroy(e);
   delete c;
   return FSDF_OK;
 }
@@ -464,11 +489,13 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   HIPCHECK(c, dalloc(&c->d_vert_hull, vert_hull.size() * sizeof(int32_t)));
   HIPCHECK(c, dalloc(&c->d_vert_off, vert_off.size() * sizeof(int32_t)));
   HIPCHECK(c, dalloc(&c->d_face_rows, std::max<size_t>(4, face_rows.size()) * sizeof(int32_t)));
-  HIPCHECK(c, dalloc((char**)&c->pm.verts_w, (size_t)V * 4 * tsz));
-  HIPCHECK(c, dalloc((char**)&c->pm.hscale_w, (size_t)K * tsz));
-  HIPCHECK(c, dalloc((char**)&c->pm.planes_w, (size_t)std::max(F, 1) * 4 * tsz));
-  HIPCHECK(c, dalloc(&c->pm.spheres_w, (size_t)K * fsdf::kBoundFloats * sizeof(float)));
-  HIPCHECK(c, dalloc(&c->pm.screen_w, (size_t)std::max(F + K, 1) * 4 * sizeof(float)));
+  for (fsdf::PosedModel* P : {&c->pm, &c->pm_alt}) {
+    HIPCHECK(c, dalloc((char**)&P->verts_w, (size_t)V * 4 * tsz));
+    HIPCHECK(c, dalloc((char**)&P->hscale_w, (size_t)K * tsz));
+    HIPCHECK(c, dalloc((char**)&P->planes_w, (size_t)std::max(F, 1) * 4 * tsz));
+    HIPCHECK(c, dalloc(&P->spheres_w, (size_t)K * fsdf::kBoundFloats * sizeof(float)));
+    HIPCHECK(c, dalloc(&P->screen_w, (size_t)std::max(F + K, 1) * 4 * sizeof(float)));
+  }
   HIPCHECK(c, dalloc(&c->d_poses, (size_t)S * 12 * sizeof(double)));
   const int R = (int)rbf_surface.size();
   HIPCHECK(c, dalloc(&c->d_accum, (size_t)(1 + 6 * S + rbf_acc_off.back()) * sizeof(double)));
@@ -672,7 +699,7 @@ static int ensure_partials(fsdf_ctx* c, int nblocks) {
   return FSDF_OK;
 }
 
-static int upload_poses(fsdf_ctx* c, const double* poses) {
+static int upload_poses(fsdf_ctx* c, const double* poses, hipStream_t st) {
   for (int i = 0; i < 12 * c->lm.S; ++i)
     if (!std::isfinite(poses[i])) return fail(c, FSDF_ERR_ARG, "poses: entry %d is not finite", i);
   if (c->lm.S <= fsdf::kPoseArgMax) return FSDF_OK;  // they ride in the pose kernel's arguments
@@ -681,8 +708,44 @@ static int upload_poses(fsdf_ctx* c, const double* poses) {
   HIPCHECK(c, hipEventSynchronize(c->pose_ev[s]));  // slot free once its last copy ran
   memcpy(c->h_poses[s], poses, (size_t)c->lm.S * 12 * sizeof(double));
   HIPCHECK(c, hipMemcpyAsync(c->d_poses, c->h_poses[s], (size_t)c->lm.S * 12 * sizeof(double),
-                             hipMemcpyHostToDevice, c->stream));
-  HIPCHECK(c, hipEventRecord(c->pose_ev[s], c->stream));
+                             hipMemcpyHostToDevice, st));
+  HIPCHECK(c, hipEventRecord(c->pose_ev[s], st));
+  return FSDF_OK;
+}
+
+#ifndef FSDF_POSE_OVERLAP
+#define FSDF_POSE_OVERLAP 0
+#endif
+// Pose the model for one pass into the next posed buffer. With
+// FSDF_POSE_OVERLAP the upload and pose kernel run on the context's pose
+// stream — behind the last reader of that buffer (two passes back), ahead of
+// the current pass's kernels on the context stream, which waits for them — so
+// the pose kernel overlaps the previous pass's tail and reduce. *buf: the
+// buffer index to release with release_posed() after its last reader.
+// Measured: the cross-stream event waits cost more than the overlap saves
+// (+10 us per step on M64), so it is off and the pose kernel runs in order.
+static int pose_model(fsdf_ctx* c, const double* poses, fsdf::PosedModel** out, int* buf) {
+  const int b = FSDF_POSE_OVERLAP ? c->pm_next : 0;
+  c->pm_next ^= FSDF_POSE_OVERLAP ? 1 : 0;
+  fsdf::PosedModel* P = b ? &c->pm_alt : &c->pm;
+  P->rbf_rows = c->pm.rbf_rows;  // per-pass RBF rows: one buffer, context-stream ordered
+  const hipStream_t ps = FSDF_POSE_OVERLAP ? c->pose_stream : c->stream;
+  if (FSDF_POSE_OVERLAP) HIPCHECK(c, hipStreamWaitEvent(ps, c->ev_pm_free[b], 0));
+  int rc = upload_poses(c, poses, ps);
+  if (rc) return rc;
+  HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, c->d_poses, *P, ps,
+                                c->lm.S <= fsdf::kPoseArgMax ? poses : nullptr));
+  if (FSDF_POSE_OVERLAP) {
+    HIPCHECK(c, hipEventRecord(c->ev_pose, ps));
+    HIPCHECK(c, hipStreamWaitEvent(c->stream, c->ev_pose, 0));
+  }
+  *out = P;
+  *buf = b;
+  return FSDF_OK;
+}
+
+static int release_posed(fsdf_ctx* c, int buf) {
+  if (FSDF_POSE_OVERLAP) HIPCHECK(c, hipEventRecord(c->ev_pm_free[buf], c->stream));
   return FSDF_OK;
 }
 
@@ -737,10 +800,10 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
                     int32_t* d_kstar, double* d_d, double* d_grad, const int32_t* d_perm, bool schedule) {
   if (c->lm.R > 0 && !c->rbf_ready)
     return fail(c, FSDF_ERR_STATE, "eval: the scene has RBF surfaces: call fsdf_set_rbf_params first");
-  int rc = upload_poses(c, poses);
+  fsdf::PosedModel* P = nullptr;
+  int pbuf = 0;
+  int rc = pose_model(c, poses, &P, &pbuf);
   if (rc) return rc;
-  HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, c->d_poses, c->pm, c->stream,
-                                c->lm.S <= fsdf::kPoseArgMax ? poses : nullptr));
   const int nblocks = fsdf::pass_blocks(n);
   rc = ensure_partials(c, nblocks);
   if (rc) return rc;
@@ -769,9 +832,11 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
   if (n > 0) {
     const bool prof = c->profiling && c->prof_used + 3 <= c->prof_ev.size();
     if (prof) HIPCHECK(c, hipEventRecord(c->prof_ev[c->prof_used], c->stream));
-    HIPCHECK(c, fsdf::launch_pass(c->precision, c->cull != 0, c->lm, c->pm, d_pts, n, nblocks, out, c->stream));
+    HIPCHECK(c, fsdf::launch_pass(c->precision, c->cull != 0, c->lm, *P, d_pts, n, nblocks, out, c->stream));
     if (prof) HIPCHECK(c, hipEventRecord(c->prof_ev[c->prof_used + 1], c->stream));
-    if (split) HIPCHECK(c, fsdf::launch_split(c->precision, c->lm, c->pm, d_pts, n, nblocks, out, c->stream));
+    if (split) HIPCHECK(c, fsdf::launch_split(c->precision, c->lm, *P, d_pts, n, nblocks, out, c->stream));
+    rc = release_posed(c, pbuf);
+    if (rc) return rc;
     if (prof) {
       HIPCHECK(c, hipEventRecord(c->prof_ev[c->prof_used + 2], c->stream));
       c->prof_used += 3;
@@ -788,6 +853,8 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
       c->order_age = 0;
     }
   } else {
+    rc = release_posed(c, pbuf);
+    if (rc) return rc;
     HIPCHECK(c, hipMemsetAsync(d_accum, 0, (size_t)accum_len(c) * sizeof(double), c->stream));
   }
   return FSDF_OK;
@@ -1011,12 +1078,14 @@ extern "C" int fsdf_raycast(fsdf_ctx* c, const double* poses, const double* orig
     HIPCHECK(c, hipMalloc(&c->d_q64, (size_t)n * 3 * sizeof(double)));
     c->q64_cap = n;
   }
-  rc = upload_poses(c, poses);
-  if (rc) return rc;
   HIPCHECK(c, hipMemcpyAsync(c->d_q64, rays, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, c->d_poses, c->pm, c->stream,
-                                c->lm.S <= fsdf::kPoseArgMax ? poses : nullptr));
-  HIPCHECK(c, fsdf::launch_raycast(c->precision, c->cull != 0, c->lm, c->pm, origin, c->d_q64, n, c->d_d, c->stream));
+  fsdf::PosedModel* P = nullptr;
+  int pbuf = 0;
+  rc = pose_model(c, poses, &P, &pbuf);
+  if (rc) return rc;
+  HIPCHECK(c, fsdf::launch_raycast(c->precision, c->cull != 0, c->lm, *P, origin, c->d_q64, n, c->d_d, c->stream));
+  rc = release_posed(c, pbuf);
+  if (rc) return rc;
   HIPCHECK(c, hipMemcpyAsync(depth_out, c->d_d, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   return FSDF_OK;

@@ -596,11 +596,13 @@ template <typename T>
 constexpr bool kStagePairs = sizeof(T) == 8 && FSDF_SCREEN32;
 // Seed phase: skip seeds no lane needs any more (1); take the seed shared by
 // the most pending lanes first (1) instead of the first pending lane's (0).
+// Measured on the bench cloud: no seed is ever skipped (hull evaluations
+// 26,835 either way) and the ordering is 1-2 % slower: both off.
 #ifndef FSDF_SEED_SKIP
-#define FSDF_SEED_SKIP 1
+#define FSDF_SEED_SKIP 0
 #endif
 #ifndef FSDF_SEED_ORDER
-#define FSDF_SEED_ORDER 1
+#define FSDF_SEED_ORDER 0
 #endif
 #ifndef FSDF_SCREEN_INTERLEAVE
 #define FSDF_SCREEN_INTERLEAVE 0

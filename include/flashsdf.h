@@ -128,6 +128,21 @@ int fsdf_tree_transforms(int32_t nb, const int32_t* parent, const int32_t* kind,
                          const double* axis, const double* AR, const double* At, const double* BR,
                          const double* Bt, const double* q, double* R, double* t, double* Rb, double* tb);
 
+/* Host chain rule (no device): ∂c/∂q of the mechanism from the accumulator's
+ * per-surface wrenches (surface_wrench[k] = accum[1+6k .. 7+6k]: F, M about the
+ * world origin) on surface_body[k] (-1: none), plus optional per-body wrenches
+ * body_wrench [nb][6] (the RBF chain's); tree arrays as fsdf_tree_transforms,
+ * Rb/tb = its joint frames before the motion; work = nb*6 doubles of scratch;
+ * gq [num_positions]. Replaces ForwardDiff's ⌈n/9⌉ Dual passes through
+ * RigidBodyDynamics (src/gradientdescent.jl:28-39, src/tracking.jl:16-21) for
+ * fixed, revolute and quaternion-floating joints (with normalize!'s projection,
+ * src/gradientdescent.jl:30); flash/mechanism.py config_gradient is the numpy
+ * twin the tests compare it with. */
+int fsdf_config_gradient(int32_t nb, const int32_t* parent, const int32_t* kind, const int32_t* qoff,
+                         const double* axis, const double* Rb, const double* tb, const double* q, int32_t nsurf,
+                         const int32_t* surface_body, const double* surface_wrench, const double* body_wrench,
+                         double* work, double* gq);
+
 /* ---- context ---------------------------------------------------------------- */
 int fsdf_create(fsdf_ctx** out, const fsdf_opts* opts);
 int fsdf_destroy(fsdf_ctx* ctx);

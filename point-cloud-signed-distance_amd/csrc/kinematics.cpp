@@ -81,3 +81,71 @@ extern "C" int fsdf_tree_transforms(int32_t nb, const int32_t* parent, const int
   }
   return FSDF_OK;
 }
+
+// ∂c/∂q from per-surface wrenches (the accumulator's hull rows) and optional
+// extra per-body wrenches (the RBF chain's), the chain rule of
+// flash/mechanism.py config_gradient: body wrenches summed over each subtree
+// (children before parents: reverse topological order), then per joint with
+// the world motion subspace of its frame before the motion (Rb, tb of
+// fsdf_tree_transforms): revolute ω = Rb·axis, v = tb × ω, ∂c/∂q = −(ω·M + v·F);
+// quaternion-floating (w, x, y, z, t): the four rotation columns through
+// E(q̂) and the normalization projection 1/|q| (src/gradientdescent.jl:30), the
+// translation columns −(Rb e_j)·F. F, M are about the world origin.
+extern "C" int fsdf_config_gradient(int32_t nb, const int32_t* parent, const int32_t* kind, const int32_t* qoff,
+                                    const double* axis, const double* Rb, const double* tb, const double* q,
+                                    int32_t nsurf, const int32_t* surface_body, const double* surface_wrench,
+                                    const double* body_wrench, double* work, double* gq) {
+  if (nb < 1 || !parent || !kind || !qoff || !axis || !Rb || !tb || !q || !work || !gq || nsurf < 0 ||
+      (nsurf > 0 && (!surface_body || !surface_wrench)))
+    return FSDF_ERR_ARG;
+  double* sub = work;  // [nb][6]
+  for (int i = 0; i < 6 * nb; ++i) sub[i] = body_wrench ? body_wrench[i] : 0.0;
+  for (int k = 0; k < nsurf; ++k) {
+    const int b = surface_body[k];
+    if (b < 0) continue;  // surface without a rigid body wrench (RBF skins: body_wrench)
+    if (b >= nb) return FSDF_ERR_ARG;
+    for (int j = 0; j < 6; ++j) sub[6 * b + j] += surface_wrench[6 * k + j];
+  }
+  for (int b = nb - 1; b >= 1; --b) {
+    const int p = parent[b];
+    if (p < 0 || p >= b) return FSDF_ERR_ARG;
+    for (int j = 0; j < 6; ++j) sub[6 * p + j] += sub[6 * b + j];
+  }
+  for (int b = 1; b < nb; ++b) {
+    const double* F = sub + 6 * b;
+    const double* M = F + 3;
+    const double* R = Rb + 9 * b;
+    const double* o = tb + 3 * b;
+    if (kind[b] == 1) {
+      const double* a = axis + 3 * b;
+      double w[3], v[3];
+      for (int i = 0; i < 3; ++i) w[i] = R[3 * i] * a[0] + R[3 * i + 1] * a[1] + R[3 * i + 2] * a[2];
+      v[0] = o[1] * w[2] - o[2] * w[1];
+      v[1] = o[2] * w[0] - o[0] * w[2];
+      v[2] = o[0] * w[1] - o[1] * w[0];
+      gq[qoff[b]] = -((w[0] * M[0] + w[1] * M[1] + w[2] * M[2]) + (v[0] * F[0] + v[1] * F[1] + v[2] * F[2]));
+    } else if (kind[b] == 2) {
+      const double* qq = q + qoff[b];
+      const double nrm = sqrt(qq[0] * qq[0] + qq[1] * qq[1] + qq[2] * qq[2] + qq[3] * qq[3]);
+      if (!(nrm > 0)) return FSDF_ERR_ARG;
+      const double W = qq[0] / nrm, X = qq[1] / nrm, Y = qq[2] / nrm, Z = qq[3] / nrm;
+      const double E[3][4] = {{-X, W, -Z, Y}, {-Y, Z, W, -X}, {-Z, -Y, X, W}};
+      double org[3];  // world origin of the frame after the joint
+      for (int i = 0; i < 3; ++i) org[i] = (R[3 * i] * qq[4] + R[3 * i + 1] * qq[5] + R[3 * i + 2] * qq[6]) + o[i];
+      for (int j = 0; j < 4; ++j) {
+        double w[3], v[3];
+        for (int i = 0; i < 3; ++i)
+          w[i] = R[3 * i] * (2.0 * E[0][j]) + R[3 * i + 1] * (2.0 * E[1][j]) + R[3 * i + 2] * (2.0 * E[2][j]);
+        v[0] = org[1] * w[2] - org[2] * w[1];
+        v[1] = org[2] * w[0] - org[0] * w[2];
+        v[2] = org[0] * w[1] - org[1] * w[0];
+        gq[qoff[b] + j] =
+            -((w[0] * M[0] + w[1] * M[1] + w[2] * M[2]) + (v[0] * F[0] + v[1] * F[1] + v[2] * F[2])) / nrm;
+      }
+      for (int j = 0; j < 3; ++j) gq[qoff[b] + 4 + j] = -(R[j] * F[0] + R[3 + j] * F[1] + R[6 + j] * F[2]);
+    } else if (kind[b] != 0) {
+      return FSDF_ERR_ARG;
+    }
+  }
+  return FSDF_OK;
+}

@@ -75,6 +75,7 @@ _PROTOS = {
     "fsdf_set_split_budget": (c_int32, [c_void_p, c_int32]),
     "fsdf_kernel_stats": (c_int32, [c_void_p, c_int32, c_void_p]),
     "fsdf_tree_transforms": (c_int32, [c_int32] + [c_void_p] * 13),
+    "fsdf_config_gradient": (c_int32, [c_int32] + [c_void_p] * 7 + [c_int32] + [c_void_p] * 5),
 }
 SYMBOLS = tuple(_PROTOS)
 

@@ -151,7 +151,9 @@ def _posed(manip: Manipulator, q: np.ndarray, surfaces) -> np.ndarray:
     if not surfaces:
         return np.zeros((0, 12))
     R, t, _, _ = manip.mechanism.body_transform_arrays(q)
-    key = tuple(id(s) for s in surfaces)
+    # surface lists only grow during model construction (Models.merge!): the
+    # list object and its length identify its contents
+    key = (id(surfaces), len(surfaces))
     cache = getattr(manip, "_frame_cache", None)
     if cache is None or cache[0] != key:
         cache = (key, np.array([s.body for s in surfaces]), np.stack([s.frame.R for s in surfaces]),
@@ -164,10 +166,22 @@ def _posed(manip: Manipulator, q: np.ndarray, surfaces) -> np.ndarray:
     return out
 
 
+def _surface_plan(manip: Manipulator):
+    """(key, convex surface indices, the convex surfaces (a list kept for the
+    pose cache), all surfaces convex) — rebuilt when the surface list changes."""
+    surf = manip.surfaces
+    plan = getattr(manip, "_surface_plan", None)
+    if plan is None or plan[0] != (id(surf), len(surf)):
+        idx = [i for i, s in enumerate(surf) if isinstance(s, ConvexGeometry)]
+        plan = ((id(surf), len(surf)), idx, [surf[i] for i in idx], len(idx) == len(surf))
+        manip._surface_plan = plan
+    return plan
+
+
 def hull_poses(manip: Manipulator, q: np.ndarray) -> np.ndarray:
     """[K,12] world poses of the convex surfaces: transform_to_root(state, frame)
     (src/Flash.jl:248) = T_world_body · T_body_geometry."""
-    return _posed(manip, q, manip.convex_surfaces())
+    return _posed(manip, q, _surface_plan(manip)[2])
 
 
 _IDENTITY12 = np.concatenate([np.eye(3).ravel(), np.zeros(3)])
@@ -176,9 +190,13 @@ _IDENTITY12 = np.concatenate([np.eye(3).ravel(), np.zeros(3)])
 def surface_poses(manip: Manipulator, q: np.ndarray) -> np.ndarray:
     """[S,12] one pose per surface in surface order (identity for RBF skins,
     whose centres travel separately)."""
-    out = np.tile(_IDENTITY12, (len(manip.surfaces), 1))
-    idx = [i for i, s in enumerate(manip.surfaces) if isinstance(s, ConvexGeometry)]
-    out[idx] = _posed(manip, q, [manip.surfaces[i] for i in idx])
+    surf = manip.surfaces
+    _, idx, convex, all_convex = _surface_plan(manip)
+    posed = _posed(manip, q, convex)
+    if all_convex:
+        return posed
+    out = np.tile(_IDENTITY12, (len(surf), 1))
+    out[idx] = posed
     return out
 
 

@@ -61,20 +61,21 @@ def gradient_from_accum(manip: Manipulator, x: np.ndarray, accum: np.ndarray, so
     ∂c/∂δ from the RBF block plus the regularizer 2wδ."""
     mech = manip.mechanism
     nq = mech.num_positions
-    body_w = np.zeros((mech.num_bodies, 6))
-    for k, s in enumerate(manip.surfaces):
-        if isinstance(s, ConvexGeometry):
-            body_w[s.body] += accum[1 + 6 * k: 7 + 6 * k]
+    S = len(manip.surfaces)
+    sb = getattr(manip, "_surface_body", None)
+    if sb is None or len(sb) != S:
+        sb = np.array([s.body if isinstance(s, ConvexGeometry) else -1 for s in manip.surfaces], np.int32)
+        manip._surface_body = sb
     gd = 2.0 * weight * np.asarray(x[nq:], np.float64)
+    body_w = None
     if solves:
         from . import rbf
-        S = len(manip.surfaces)
         w_rbf, g_rbf = rbf.chain(manip, mech.normalize(x[:nq]), solves, accum[1 + 6 * S:], manip.num_deformations())
-        body_w += w_rbf
+        body_w = w_rbf
         gd = gd + g_rbf
     # the gradient is taken at the caller's (un-normalized) x: the chain rule
     # includes the normalization projection (src/gradientdescent.jl:30)
-    gq = mech.config_gradient(np.asarray(x[:nq], np.float64), body_w)
+    gq = mech.config_gradient(np.asarray(x[:nq], np.float64), body_w, sb, np.asarray(accum[1:1 + 6 * S]))
     return np.concatenate([gq, gd])
 
 

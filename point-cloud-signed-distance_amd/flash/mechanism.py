@@ -137,10 +137,9 @@ class Mechanism:
     def normalize(self, q: np.ndarray) -> np.ndarray:
         """normalize! of every QuaternionFloating block (src/gradientdescent.jl:19-26)."""
         q = np.array(q, np.float64, copy=True)
-        for e in self.edges[1:]:
-            if e.joint.kind == "quaternion_floating":
-                s = slice(e.q_offset, e.q_offset + 4)
-                q[s] = q[s] / np.linalg.norm(q[s])
+        P = self._kinematic_plan()
+        for o in P["quat_qoff"]:
+            q[o:o + 4] = q[o:o + 4] / np.linalg.norm(q[o:o + 4])
         return q
 
     # -- kinematics -----------------------------------------------------------
@@ -173,8 +172,10 @@ class Mechanism:
         Kax[:, 0, 1], Kax[:, 0, 2] = -a[:, 2], a[:, 1]
         Kax[:, 1, 0], Kax[:, 1, 2] = a[:, 2], -a[:, 0]
         Kax[:, 2, 0], Kax[:, 2, 1] = -a[:, 1], a[:, 0]
+        quat = np.nonzero(kind == 2)[0]
         plan = dict(key=key, parent=parent, AR=AR, At=At, BR=BR, Bt=Bt, kind=kind, axis=axis, qoff=qoff,
-                    levels=levels, rev=rev, Kax=Kax, KK=Kax @ Kax, quat=np.nonzero(kind == 2)[0])
+                    levels=levels, rev=rev, Kax=Kax, KK=Kax @ Kax, quat=quat,
+                    quat_qoff=[int(qoff[i]) for i in quat])
         # contiguous copies for the native fsdf_tree_transforms (kept alive by the plan)
         c = lambda a, dt=np.float64: np.ascontiguousarray(a, dt)  # noqa: E731
         nat = (c(parent, np.int32), c(np.maximum(kind, 0), np.int32), c(qoff, np.int32), c(axis),
@@ -208,7 +209,7 @@ class Mechanism:
         out = (R, t, Rb, tb)
         for a in out:
             a.flags.writeable = False
-        self._fk_last = (P, q.copy(), out)
+        self._fk_last = (P, q.copy(), out, (Rb.ctypes.data, tb.ctypes.data))
         return out
 
     def body_transform_arrays_numpy(self, q: np.ndarray):
@@ -254,12 +255,40 @@ class Mechanism:
         R, t, _, _ = self.body_transform_arrays(q)
         return [Transform(R[b], t[b]) for b in range(self.num_bodies)]
 
-    def config_gradient(self, q: np.ndarray, body_wrench: np.ndarray) -> np.ndarray:
-        """∂c/∂q from per-body wrenches body_wrench[b] = (F, M about the world origin).
+    def config_gradient(self, q: np.ndarray, body_wrench: np.ndarray | None = None, surface_body=None,
+                        surface_wrench=None) -> np.ndarray:
+        """∂c/∂q from wrenches (F, M about the world origin): per body
+        (body_wrench [nb, 6]) and/or per surface (surface_wrench [S, 6] on body
+        surface_body[k], -1 = none) — natively (fsdf_config_gradient,
+        csrc/kinematics.cpp; config_gradient_numpy is the test reference).
 
         For a world twist (ω, v) of a body, δc = −(ω·M + v·F) (include/flashsdf.h).
         Quaternion blocks include the normalization projection (I − q̂q̂ᵀ)/|q| that
         ForwardDiff sees through normalize! (src/gradientdescent.jl:30)."""
+        from . import _lib
+        P = self._kinematic_plan()
+        q = np.ascontiguousarray(q, np.float64)
+        self.body_transform_arrays(q)
+        rb_ptr, tb_ptr = self._fk_last[3]
+        nb = self.num_bodies
+        bw = None if body_wrench is None else np.ascontiguousarray(body_wrench, np.float64).reshape(nb, 6)
+        ns = 0 if surface_body is None else len(surface_body)
+        sb = None if ns == 0 else np.ascontiguousarray(surface_body, np.int32)
+        sw = None if ns == 0 else np.ascontiguousarray(surface_wrench, np.float64).reshape(ns, 6)
+        if "cg_work" not in P:
+            P["cg_work"] = np.empty(6 * nb)
+            P["cg_work_ptr"] = P["cg_work"].ctypes.data
+        g = np.zeros(self._nq)
+        nat = P["native_ptrs"]
+        ptr = lambda a: None if a is None else a.ctypes.data  # noqa: E731
+        st = _lib.load().fsdf_config_gradient(nb, nat[0], nat[1], nat[2], nat[3], rb_ptr, tb_ptr, q.ctypes.data, ns,
+                                              ptr(sb), ptr(sw), ptr(bw), P["cg_work_ptr"], g.ctypes.data)
+        if st != _lib.FSDF_OK:
+            raise _lib.FlashNativeError(st, "fsdf_config_gradient: bad tree, configuration or surface bodies")
+        return g
+
+    def config_gradient_numpy(self, q: np.ndarray, body_wrench: np.ndarray) -> np.ndarray:
+        """The chain rule of config_gradient in numpy (test reference)."""
         nb = self.num_bodies
         P = self._kinematic_plan()
         sub = np.array(body_wrench, np.float64, copy=True).reshape(nb, 6)

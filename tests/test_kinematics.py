@@ -151,3 +151,41 @@ def test_native_forward_kinematics_matches_numpy():
     st = _lib.load().fsdf_tree_transforms(len(bad), bad.ctypes.data, *P["native_ptrs"][1:], q.ctypes.data,
                                           *[o.ctypes.data for o in out])
     assert st == 1  # FSDF_ERR_ARG
+
+
+def test_native_chain_rule_matches_numpy():
+    """fsdf_config_gradient (csrc/kinematics.cpp) == the numpy chain rule
+    (mechanism.config_gradient_numpy) on every model, revolute and
+    quaternion-floating joints, from per-body wrenches, per-surface wrenches
+    (with surfaces that carry none) and both together."""
+    from flash import Models
+    r = np.random.default_rng(41)
+    models = [Models.irb140(), Models.arm_grid(), Models.table(), Models.beanbag(), Models.two_link_arm(False),
+              Models.irb_and_squishable()[0]]
+    for m in models:
+        mech = m.mechanism
+        nb, S = mech.num_bodies, len(m.surfaces)
+        for _ in range(3):
+            q = mech.zero_configuration() + r.normal(scale=0.3, size=mech.num_positions)
+            bw = r.normal(size=(nb, 6))
+            sb = r.integers(-1, nb, size=S).astype(np.int32)
+            sw = r.normal(size=(S, 6))
+            ref_b = mech.config_gradient_numpy(q, bw)
+            assert np.allclose(mech.config_gradient(q, bw), ref_b, rtol=1e-12, atol=1e-12)
+            sb_w = np.zeros((nb, 6))
+            for k in range(S):
+                if sb[k] >= 0:
+                    sb_w[sb[k]] += sw[k]
+            ref_s = mech.config_gradient_numpy(q, sb_w)
+            assert np.allclose(mech.config_gradient(q, None, sb, sw), ref_s, rtol=1e-12, atol=1e-12)
+            assert np.allclose(mech.config_gradient(q, bw, sb, sw), mech.config_gradient_numpy(q, bw + sb_w),
+                               rtol=1e-12, atol=1e-12)
+
+
+def test_native_chain_rule_rejects_bad_input():
+    import pytest
+    from flash import Models, FlashNativeError
+    m = Models.irb140()
+    q = m.mechanism.zero_configuration()
+    with pytest.raises(FlashNativeError):
+        m.mechanism.config_gradient(q, None, np.array([99], np.int32), np.zeros((1, 6)))

@@ -137,19 +137,17 @@ def cpu_baseline(manip, pts, q_eval, target_s):
 
 def full_iteration_ms(manip, ctx, q, iters=20):
     """One CostFunctor.value_and_gradient iteration on the resident cloud, as
-    track! runs it: native FK + pose assembly, the pass, accumulator read-back,
-    chain rule to ∂c/∂q (the configuration moves every iteration, so the FK
-    cache never hits)."""
-    from flash.core import surface_poses
-    from flash.gradientdescent import gradient_from_accum
+    track! runs it for a rigid scene: fsdf_value_and_gradient = native FK +
+    surface poses, the pass, accumulator read-back, chain rule to ∂c/∂q (the
+    configuration moves every iteration)."""
+    surf = manip.surfaces
+    ctx.set_mechanism(manip.mechanism, [s.body for s in surf], [s.frame.R for s in surf], [s.frame.t for s in surf])
     x = np.array(q, np.float64)
     for i in range(iters + 3):
         if i == 3:
             t = time.perf_counter()
         x = x + 1e-6
-        poses = surface_poses(manip, manip.mechanism.normalize(x))
-        _, acc, _ = ctx.eval(poses)
-        gradient_from_accum(manip, x, acc, [], 10)
+        ctx.value_and_gradient(x)
     return (time.perf_counter() - t) / iters * 1e3
 
 
@@ -310,8 +308,9 @@ def main():
                 "frame_ms_at_30_iterations": frame_ms,
                 "frame_note": "set_points (H2D-resident copy + Hilbert sort) once + 30 residual passes",
                 "full_iteration_ms": iter_ms,
-                "full_iteration_note": "CostFunctor.value_and_gradient on the resident cloud: host FK + pose "
-                                       "assembly, pass, accumulator read-back, chain rule (rank 0, N=1 only)",
+                "full_iteration_note": "CostFunctor.value_and_gradient on the resident cloud (fsdf_value_and_gradient: "
+                                       "host FK + surface poses, pass, accumulator read-back, chain rule; rank 0, "
+                                       "N=1 only)",
             },
             "roofline": {
                 "bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

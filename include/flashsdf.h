@@ -143,6 +143,22 @@ int fsdf_config_gradient(int32_t nb, const int32_t* parent, const int32_t* kind,
                          const int32_t* surface_body, const double* surface_wrench, const double* body_wrench,
                          double* work, double* gq);
 
+/* The whole CostFunctor iteration of a rigid (hull-only) scene in one call:
+ * fsdf_set_mechanism registers the mechanism tree (the arrays of
+ * fsdf_tree_transforms, nq = num_positions) and, per surface of
+ * fsdf_set_surfaces, its body (-1: none) and body-to-geometry frame (R
+ * row-major [S][9], t [S][3]); fsdf_value_and_gradient(x) then runs host FK,
+ * the surface poses, one residual pass over the resident cloud, and the chain
+ * rule: cost_out = Σ_p d*(p)^2 and grad_out [nq] = ∂cost/∂x at the caller's x
+ * (quaternion blocks normalized for the evaluation, the projection in the
+ * gradient) — CostFunctor(x) with its ForwardDiff gradient
+ * (src/gradientdescent.jl:28-57) for scenes without deformations. RBF scenes
+ * keep fsdf_eval + the host's weight solve (FSDF_ERR_STATE here). */
+int fsdf_set_mechanism(fsdf_ctx* ctx, int32_t nb, const int32_t* parent, const int32_t* kind, const int32_t* qoff,
+                       const double* axis, const double* AR, const double* At, const double* BR, const double* Bt,
+                       int32_t nq, const int32_t* surface_body, const double* frame_R, const double* frame_t);
+int fsdf_value_and_gradient(fsdf_ctx* ctx, const double* x, double* cost_out, double* grad_out);
+
 /* ---- context ---------------------------------------------------------------- */
 int fsdf_create(fsdf_ctx** out, const fsdf_opts* opts);
 int fsdf_destroy(fsdf_ctx* ctx);

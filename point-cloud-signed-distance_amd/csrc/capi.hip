@@ -140,6 +140,13 @@ struct fsdf_ctx {
   int32_t* d_blk_mask = nullptr;     // [kMaxBlocks]
   int32_t* d_split_blocks = nullptr; // [kMaxBlocks]
   int64_t spill_n64 = 0;
+  // mechanism of fsdf_set_mechanism (host arrays; fsdf_value_and_gradient)
+  struct Mechanism {
+    int nb = 0, nq = 0;
+    std::vector<int32_t> parent, kind, qoff, surface_body;
+    std::vector<double> axis, AR, At, BR, Bt, frame_R, frame_t;
+    std::vector<double> R, t, Rb, tb, poses, accum, work;  // scratch
+  } mech;
   fsdf::SpillBufs* d_spill_dev = nullptr;  // device copy of the record (read by the pass kernel)
   fsdf::SpillBufs spill_dev_copy;          // what d_spill_dev holds (host, stable address)
 };
@@ -956,6 +963,90 @@ extern "C" int fsdf_eval(fsdf_ctx* c, const double* poses, double* cost_out, dou
                     want_pp ? c->d_d : nullptr, want_pp ? c->d_grad : nullptr, out_perm(c), true);
   if (rc) return rc;
   return fetch(c, c->n, cost_out, accum_out, kstar_out, d_out, grad_out, want_pp);
+}
+
+extern "C" int fsdf_set_mechanism(fsdf_ctx* c, int32_t nb, const int32_t* parent, const int32_t* kind,
+                                  const int32_t* qoff, const double* axis, const double* AR, const double* At,
+                                  const double* BR, const double* Bt, int32_t nq, const int32_t* surface_body,
+                                  const double* frame_R, const double* frame_t) {
+  if (!c) return FSDF_ERR_ARG;
+  if (c->lm.S == 0) return fail(c, FSDF_ERR_STATE, "set_mechanism: set the surfaces first");
+  if (nb < 1 || nq < 0 || !parent || !kind || !qoff || !axis || !AR || !At || !BR || !Bt || !surface_body ||
+      !frame_R || !frame_t)
+    return fail(c, FSDF_ERR_ARG, "set_mechanism: bad arguments");
+  const int S = c->lm.S;
+  for (int b = 1; b < nb; ++b) {
+    if (parent[b] < 0 || parent[b] >= b) return fail(c, FSDF_ERR_ARG, "set_mechanism: bodies not in topological order");
+    if (kind[b] < 0 || kind[b] > 2) return fail(c, FSDF_ERR_ARG, "set_mechanism: joint kind %d", kind[b]);
+    const int width = kind[b] == 1 ? 1 : (kind[b] == 2 ? 7 : 0);
+    if (width && (qoff[b] < 0 || qoff[b] + width > nq)) return fail(c, FSDF_ERR_ARG, "set_mechanism: q offset");
+  }
+  for (int k = 0; k < S; ++k)
+    if (surface_body[k] < -1 || surface_body[k] >= nb) return fail(c, FSDF_ERR_ARG, "set_mechanism: surface body");
+  auto& M = c->mech;
+  M.nb = nb;
+  M.nq = nq;
+  M.parent.assign(parent, parent + nb);
+  M.kind.assign(kind, kind + nb);
+  M.qoff.assign(qoff, qoff + nb);
+  M.surface_body.assign(surface_body, surface_body + S);
+  M.axis.assign(axis, axis + 3 * nb);
+  M.AR.assign(AR, AR + 9 * nb);
+  M.At.assign(At, At + 3 * nb);
+  M.BR.assign(BR, BR + 9 * nb);
+  M.Bt.assign(Bt, Bt + 3 * nb);
+  M.frame_R.assign(frame_R, frame_R + 9 * S);
+  M.frame_t.assign(frame_t, frame_t + 3 * S);
+  M.R.resize(9 * nb);
+  M.t.resize(3 * nb);
+  M.Rb.resize(9 * nb);
+  M.tb.resize(3 * nb);
+  M.poses.resize(12 * S);
+  M.work.resize(6 * nb);
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cost_out, double* grad_out) {
+  if (!c) return FSDF_ERR_ARG;
+  auto& M = c->mech;
+  if (M.nb == 0) return fail(c, FSDF_ERR_STATE, "value_and_gradient: no mechanism (call fsdf_set_mechanism)");
+  if (c->lm.R > 0)
+    return fail(c, FSDF_ERR_STATE, "value_and_gradient: RBF scenes need the host's weight solve (use fsdf_eval)");
+  if (!x || !cost_out || !grad_out) return fail(c, FSDF_ERR_ARG, "value_and_gradient: null argument");
+  HIPCHECK(c, hipSetDevice(c->device));
+  // forward kinematics (quaternion blocks normalized inside: normalize!, src/gradientdescent.jl:30)
+  int rc = fsdf_tree_transforms(M.nb, M.parent.data(), M.kind.data(), M.qoff.data(), M.axis.data(), M.AR.data(),
+                                M.At.data(), M.BR.data(), M.Bt.data(), x, M.R.data(), M.t.data(), M.Rb.data(),
+                                M.tb.data());
+  if (rc) return fail(c, rc, "value_and_gradient: forward kinematics (bad configuration)");
+  // surface poses T_world_body · T_body_geometry (identity for surfaces without a body)
+  const int S = c->lm.S;
+  for (int k = 0; k < S; ++k) {
+    double* P = M.poses.data() + 12 * k;
+    const int b = M.surface_body[k];
+    if (b < 0) {
+      for (int i = 0; i < 12; ++i) P[i] = (i % 4 == 0 && i < 9) ? 1.0 : 0.0;
+      continue;
+    }
+    const double* Rw = M.R.data() + 9 * b;
+    const double* FR = M.frame_R.data() + 9 * k;
+    const double* Ft = M.frame_t.data() + 3 * k;
+    for (int i = 0; i < 3; ++i) {
+      for (int j = 0; j < 3; ++j) P[3 * i + j] = Rw[3 * i] * FR[j] + Rw[3 * i + 1] * FR[3 + j] + Rw[3 * i + 2] * FR[6 + j];
+      P[9 + i] = (Rw[3 * i] * Ft[0] + Rw[3 * i + 1] * Ft[1] + Rw[3 * i + 2] * Ft[2]) + M.t[3 * b + i];
+    }
+  }
+  rc = run_pass(c, M.poses.data(), c->d_pts, c->n, c->d_accum, nullptr, nullptr, nullptr, nullptr, true);
+  if (rc) return rc;
+  M.accum.resize(accum_len(c));
+  rc = fetch(c, c->n, cost_out, M.accum.data(), nullptr, nullptr, nullptr, false);
+  if (rc) return rc;
+  for (int i = 0; i < M.nq; ++i) grad_out[i] = 0.0;
+  rc = fsdf_config_gradient(M.nb, M.parent.data(), M.kind.data(), M.qoff.data(), M.axis.data(), M.Rb.data(),
+                            M.tb.data(), x, S, M.surface_body.data(), M.accum.data() + 1, nullptr, M.work.data(),
+                            grad_out);
+  if (rc) return fail(c, rc, "value_and_gradient: chain rule");
+  return FSDF_OK;
 }
 
 extern "C" int fsdf_skin(fsdf_ctx* c, const double* poses, const double* xyz, int64_t n, double* d_out,

@@ -76,6 +76,8 @@ _PROTOS = {
     "fsdf_kernel_stats": (c_int32, [c_void_p, c_int32, c_void_p]),
     "fsdf_tree_transforms": (c_int32, [c_int32] + [c_void_p] * 13),
     "fsdf_config_gradient": (c_int32, [c_int32] + [c_void_p] * 7 + [c_int32] + [c_void_p] * 5),
+    "fsdf_set_mechanism": (c_int32, [c_void_p, c_int32] + [c_void_p] * 8 + [c_int32] + [c_void_p] * 3),
+    "fsdf_value_and_gradient": (c_int32, [c_void_p, c_void_p, POINTER(c_double), c_void_p]),
 }
 SYMBOLS = tuple(_PROTOS)
 
@@ -291,6 +293,27 @@ class Context:
         check(self._lib.fsdf_pass_times(self._ctx, ctypes.byref(k), ctypes.byref(p), ctypes.byref(n)), self._ctx,
               "pass_times")
         return k.value, p.value, n.value
+
+    def set_mechanism(self, mechanism, surface_body, frame_R, frame_t):
+        """Register the mechanism tree and each surface's body / frame for
+        value_and_gradient (hull-only scenes)."""
+        P = mechanism._kinematic_plan()
+        nb = mechanism.num_bodies
+        sb = np.ascontiguousarray(surface_body, np.int32)
+        fr = np.ascontiguousarray(frame_R, np.float64).reshape(-1, 9)
+        ft = np.ascontiguousarray(frame_t, np.float64).reshape(-1, 3)
+        check(self._lib.fsdf_set_mechanism(self._ctx, nb, *P["native_ptrs"][:8], mechanism.num_positions, ptr(sb),
+                                           ptr(fr), ptr(ft)), self._ctx, "set_mechanism")
+        self.nq = mechanism.num_positions
+
+    def value_and_gradient(self, x):
+        """(Σ d², ∂/∂x) of a rigid scene in one native call (FK, pass, chain rule)."""
+        x = np.ascontiguousarray(x, np.float64)
+        g = np.empty(self.nq)
+        c = c_double(0.0)
+        check(self._lib.fsdf_value_and_gradient(self._ctx, ptr(x), ctypes.byref(c), ptr(g)), self._ctx,
+              "value_and_gradient")
+        return c.value, g
 
     def set_split_budget(self, evals: int):
         """Hull evaluations per wave before the pass splits it (0 = never)."""

@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .core import ConvexGeometry, Manipulator, ManipulatorState, prepare_pass
+from .core import ConvexGeometry, Manipulator, ManipulatorState, num_states, prepare_pass
 
 default_deformation_cost_weight = 10
 
@@ -96,6 +96,14 @@ class CostFunctor:
         self.ctx.set_points(self.sensed_points)
         self._resident = id(self)
         manipulator._resident_cloud = self._resident
+        # rigid scenes: the whole iteration (FK, pass, chain rule) in one native
+        # call (fsdf_value_and_gradient); deformable ones keep the host weight solve
+        self._native = not manipulator.has_rbf() and num_states(manipulator) == manipulator.mechanism.num_positions
+        if self._native and getattr(self.ctx, "_mechanism_of", None) is not manipulator:
+            surf = manipulator.surfaces
+            self.ctx.set_mechanism(manipulator.mechanism, [s.body for s in surf], [s.frame.R for s in surf],
+                                   [s.frame.t for s in surf])
+            self.ctx._mechanism_of = manipulator
 
     def set_sensed_points(self, sensed_points):
         """Swap the resident cloud (a new frame): one upload + device sort; the
@@ -123,6 +131,9 @@ class CostFunctor:
     def value_and_gradient(self, x):
         """(c(x), ∂c/∂x) from one residual pass."""
         x = np.asarray(x, np.float64)
+        if self._native:
+            self._ensure_resident()
+            return self.ctx.value_and_gradient(x)
         c, accum, _ = self._pass(x)
         return c, gradient_from_accum(self.manipulator, x, accum, self._solves, self.weight)
 

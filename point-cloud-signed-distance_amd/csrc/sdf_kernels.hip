@@ -1528,6 +1528,7 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   __shared__ int split_mask;  // SPILL: waves of this block that split their chunk
+  __shared__ unsigned long long block_touched;  // sparse partials: surfaces with a nonzero sum
   // All LDS is one dynamic region (16-byte aligned carve, see pass_lds_bytes):
   //   red     [4 waves][kRedStride] f64  per-hull wrench sums + cost
   //   rbf_acc [4 waves][kMaxRbfAcc] f64  (RBF variants only)
@@ -1557,6 +1558,7 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
   const uint64_t t_block0 = __builtin_amdgcn_s_memrealtime();
 #endif
   if (SPILL && threadIdx.x == 0) split_mask = 0;  // ordered by load_hull_table's barrier
+  if (threadIdx.x == 0) block_touched = 0ull;
   const float smax = load_hull_table(m, ht);
 #if FSDF_PHASE_TIMING
   if (lane < 10) fsdf_phase_acc[wave][lane] = 0;
@@ -1611,6 +1613,10 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
   __syncthreads();
   const int len6 = 1 + 6 * m.S;
   const int len = len6 + (RBF ? m.rbf_acc_off[m.R] : 0);
+  // sparse partials (out.hull_mask, <= 64 surfaces): a block writes the six
+  // entries of the surfaces it touched (any nonzero sum) and their bit mask;
+  // the reduce skips the others (a skipped entry is an exact zero)
+  const bool sparse = out.hull_mask != nullptr;
   for (int t = threadIdx.x; t < len; t += kPassBlock) {
     double s;
     if (t < len6) {
@@ -1624,7 +1630,24 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
 #pragma unroll
       for (int w = 1; w < kPassBlock / 64; ++w) s += rbf_acc[w * kMaxRbfAcc + src];
     }
-    out.partials[pidx(t, lb, len, gridDim.x)] = s;
+    if (sparse) {
+      // the block sum goes back into wave 0's slot (only this thread reads it)
+      if (t >= 1 && t < len6 && s != 0.0) atomicOr(&block_touched, 1ull << ((t - 1) / 6));
+      if (t < len6) red[(t == 0) ? SLOTS * 64 * 6 : t - 1] = s;
+      else rbf_acc[RBF ? t - len6 : 0] = s;
+    } else {
+      out.partials[pidx(t, lb, len, gridDim.x)] = s;
+    }
+  }
+  if (sparse) {
+    __syncthreads();
+    const uint64_t touched = block_touched;
+    for (int t = threadIdx.x; t < len; t += kPassBlock) {
+      if (t >= 1 && t < len6 && !((touched >> ((t - 1) / 6)) & 1)) continue;
+      const double v = t < len6 ? red[(t == 0) ? SLOTS * 64 * 6 : t - 1] : rbf_acc[RBF ? t - len6 : 0];
+      out.partials[pidx(t, lb, len, gridDim.x)] = v;
+    }
+    if (threadIdx.x == 0) out.hull_mask[lb] = touched;
   }
   if (SPILL && threadIdx.x == 0 && split_mask) {
     out.spill_dev->blk_mask[lb] = split_mask;
@@ -1742,8 +1765,13 @@ __global__ __launch_bounds__(kPassBlock) void merge_kernel(const T* __restrict__
       double s = red[0][src];
 #pragma unroll
       for (int w = 1; w < kWaves; ++w) s += red[w][src];
-      out.partials[pidx(t, lb, len, nblocks)] += s;
+      double* pp = out.partials + pidx(t, lb, len, nblocks);
+      // sparse partials: an entry the pass kernel skipped holds stale data
+      const bool had = !out.hull_mask || t == 0 || ((out.hull_mask[lb] >> ((t - 1) / 6)) & 1);
+      *pp = had ? *pp + s : s;
     }
+    __syncthreads();
+    if (out.hull_mask && threadIdx.x == 0) out.hull_mask[lb] = m.S >= 64 ? ~0ull : (1ull << m.S) - 1;
     __syncthreads();  // the rows are reused by the next block
   }
 }
@@ -1876,14 +1904,19 @@ __device__ void build_order(const uint32_t* __restrict__ cost, int nb, int32_t* 
 
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict__ partials, int nblocks, int len,
                                                         double* __restrict__ accum, const uint32_t* __restrict__ cost,
-                                                        int32_t* __restrict__ order, int32_t* __restrict__ spill_ctr) {
+                                                        int32_t* __restrict__ order, int32_t* __restrict__ spill_ctr,
+                                                        const uint64_t* __restrict__ hull_mask, int len6) {
   const int j = blockIdx.x;
   if (spill_ctr && j == 0 && threadIdx.x < 2) spill_ctr[threadIdx.x] = 0;  // the split pass is done with them
   if (cost && j == (int)gridDim.x - 1) {  // the extra workgroup
     build_order(cost, nblocks, order);
     return;
   }
-  auto at = [&](int b) { return partials[pidx(j, b, len, nblocks)]; };
+  // sparse partials: hull entries of blocks that did not touch the hull are
+  // exact zeros, not stored (skipping them leaves the sums unchanged)
+  const bool masked = hull_mask && j >= 1 && j < len6;
+  const uint64_t bit = masked ? 1ull << ((j - 1) / 6) : 0ull;
+  auto at = [&](int b) { return (!masked || (hull_mask[b] & bit)) ? partials[pidx(j, b, len, nblocks)] : 0.0; };
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   int b = threadIdx.x;
   for (; b + 3 * kBlock < nblocks; b += 4 * kBlock) {
@@ -1898,6 +1931,70 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x == 0) accum[j] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
+// Reduce over sparse partials (PassOutputs::hull_mask): workgroup 0 sums the
+// cost entry, workgroup 1 + k the six entries of surface k over the blocks
+// whose mask has bit k (one mask load per block, not per entry), the rest one
+// dense RBF entry each; the last (when cost/order are given) rebuilds the
+// schedule. Fixed order: per thread its blocks b = tid + 256 i in order, then
+// the DPP wave sum and the fixed 4-wave combine (deterministic).
+__global__ __launch_bounds__(kBlock) void reduce_sparse_kernel(const double* __restrict__ partials, int nblocks,
+                                                               int len, int S, double* __restrict__ accum,
+                                                               const uint64_t* __restrict__ hull_mask,
+                                                               const uint32_t* __restrict__ cost,
+                                                               int32_t* __restrict__ order,
+                                                               int32_t* __restrict__ spill_ctr) {
+  const int j = blockIdx.x;
+  if (cost && j == (int)gridDim.x - 1) {
+    build_order(cost, nblocks, order);
+    return;
+  }
+  if (spill_ctr && j == 0 && threadIdx.x < 2) spill_ctr[threadIdx.x] = 0;
+  const int len6 = 1 + 6 * S;
+  __shared__ double sh[6][kBlock / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (j >= 1 && j <= S) {
+    const int k = j - 1;
+    const uint64_t bit = 1ull << k;
+    double sv[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    // masks for 16 blocks in flight at once, then the (few) selected entries
+    for (int b0 = threadIdx.x; b0 < nblocks; b0 += 16 * kBlock) {
+      uint64_t m[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) m[i] = b0 + i * kBlock < nblocks ? hull_mask[b0 + i * kBlock] & bit : 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        if (m[i]) {
+#pragma unroll
+          for (int q = 0; q < 6; ++q) sv[q] += partials[pidx(1 + 6 * k + q, b0 + i * kBlock, len, nblocks)];
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const double w = wave_sum(sv[q]);
+      if (lane == 0) sh[q][wave] = w;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) accum[1 + 6 * k + threadIdx.x] = (sh[threadIdx.x][0] + sh[threadIdx.x][1]) +
+                                                          (sh[threadIdx.x][2] + sh[threadIdx.x][3]);
+    return;
+  }
+  const int t = j == 0 ? 0 : len6 + (j - 1 - S);  // cost, or a dense RBF entry
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int b = threadIdx.x;
+  for (; b + 3 * kBlock < nblocks; b += 4 * kBlock) {
+    s0 += partials[pidx(t, b, len, nblocks)];
+    s1 += partials[pidx(t, b + kBlock, len, nblocks)];
+    s2 += partials[pidx(t, b + 2 * kBlock, len, nblocks)];
+    s3 += partials[pidx(t, b + 3 * kBlock, len, nblocks)];
+  }
+  for (; b < nblocks; b += kBlock) s0 += partials[pidx(t, b, len, nblocks)];
+  const double w = wave_sum((s0 + s1) + (s2 + s3));
+  if (lane == 0) sh[0][wave] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) accum[t] = (sh[0][0] + sh[0][1]) + (sh[0][2] + sh[0][3]);
 }
 
 __global__ void to_f32_kernel(const double* __restrict__ src, float* __restrict__ dst, int64_t count) {
@@ -2107,9 +2204,16 @@ hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const 
 }
 
 hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum, hipStream_t s,
-                         const uint32_t* cost, int32_t* order, int32_t* spill_ctr) {
+                         const uint32_t* cost, int32_t* order, int32_t* spill_ctr, const uint64_t* hull_mask,
+                         int len6) {
+  if (hull_mask) {
+    const int S = (len6 - 1) / 6;
+    hipLaunchKernelGGL(reduce_sparse_kernel, dim3(1 + S + (len - len6) + (cost ? 1 : 0)), dim3(kBlock), 0, s,
+                       partials, nblocks, len, S, d_accum, hull_mask, cost, order, spill_ctr);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(reduce_kernel, dim3(len + (cost ? 1 : 0)), dim3(kBlock), 0, s, partials, nblocks, len, d_accum,
-                     cost, order, spill_ctr);
+                     cost, order, spill_ctr, hull_mask, len6);
   return hipGetLastError();
 }
 

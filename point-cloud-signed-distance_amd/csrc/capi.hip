@@ -701,7 +701,8 @@ extern "C" int fsdf_set_points_device(fsdf_ctx* c, const double* d_xyz, int64_t 
 }
 
 static int ensure_partials(fsdf_ctx* c, int nblocks) {
-  const size_t need = (size_t)accum_len(c) * nblocks;
+  // (rounded up to whole 8-entry tiles: FSDF_PARTIALS_LAYOUT 2)
+  const size_t need = (size_t)((accum_len(c) + 7) & ~7) * nblocks;
   if (c->partials_cap < need) {
     dfree(c->d_partials);
     c->partials_cap = 0;

@@ -397,8 +397,37 @@ __device__ __forceinline__ uint64_t phase_clock() {
 __shared__ unsigned long long fsdf_phase_acc[kBlock / 64][10];  // per wave, flushed at kernel end
 #endif
 #if FSDF_WAVE_TIMES
-__shared__ unsigned fsdf_wave_ev[kBlock / 64][2];  // per wave-iteration: hull evaluations, seed evaluations
+// per wave-iteration, packed 16-bit fields:
+//   ev[0]: hull evaluations | screen rejections << 16 | slow evaluations << 32 | walk steps << 48
+//   ev[1]: seed evaluations | needing lanes << 16 | wave candidates << 32 | full fp64 scans << 48
+//   ph[0]: 10-ns units in hull staging | screen | fast path | closest-feature search
+//   ph[1]: culling | RBF | segmented reduction + stores | -
+__shared__ unsigned long long fsdf_wave_ev[kBlock / 64][2];
+__shared__ unsigned long long fsdf_wave_ph[kBlock / 64][2];
 #endif
+__device__ __forceinline__ uint64_t wt_now() {
+#if FSDF_WAVE_TIMES
+  return __builtin_amdgcn_s_memrealtime();
+#else
+  return 0;
+#endif
+}
+// adds the time since t0 to phase field f (0..7); returns now
+__device__ __forceinline__ uint64_t wt_add(int f, uint64_t t0) {
+#if FSDF_WAVE_TIMES
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0) fsdf_wave_ph[threadIdx.x >> 6][f >> 2] += (t1 - t0) << (16 * (f & 3));
+  return t1;
+#else
+  return t0;
+#endif
+}
+// adds v to event field f (0..7) of this wave-iteration
+__device__ __forceinline__ void wt_count(int f, uint64_t v) {
+#if FSDF_WAVE_TIMES
+  if ((threadIdx.x & 63) == 0) fsdf_wave_ev[threadIdx.x >> 6][f >> 2] += v << (16 * (f & 3));
+#endif
+}
 __device__ __forceinline__ void phase_add(unsigned long long* stats, int slot, uint64_t t0) {
 #if FSDF_PHASE_TIMING
   const uint64_t t1 = phase_clock();
@@ -610,10 +639,28 @@ constexpr bool kStagePairs = sizeof(T) == 8 && FSDF_SCREEN32;
 #ifndef FSDF_SCREEN_ILP
 #define FSDF_SCREEN_ILP 4
 #endif
+// lane-divergent evaluation of waves with at least this many distinct seed
+// hulls (scene_eval; 0 = off)
+#ifndef FSDF_LANE_SEEDS
+#define FSDF_LANE_SEEDS 0
+#endif
+constexpr int kLaneSeeds = FSDF_LANE_SEEDS;
 constexpr int kScreenIlp = FSDF_SCREEN_ILP;  // independent 8-face batches per loop iteration  // see hull_sdf / fsdf_internal.h
 typedef float F2v __attribute__((ext_vector_type(2)));
 
-template <typename T>
+// wave-wide int max (butterfly; every lane gets the result). Whole wave active.
+__device__ __forceinline__ int wave_max_int(int v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// LANE (lane-divergent evaluation, scene_eval's many-seed waves): k, f0 and nf
+// differ per lane and the pairs are read from global memory (L1/L2) instead of
+// the wave's LDS stage; every lane runs the same sequence of batches as the
+// wave path over its own hull (masked batches past its end), so its b1, b2,
+// ib — and the result — are bit-identical.
+template <typename T, bool LANE = false>
 __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0, int nf, const PassModel<T>& m,
                                                  const HullRow* __restrict__ ht, const void* __restrict__ lw,
                                                  const typename Row4<T>::type* __restrict__ lp, bool active,
@@ -624,7 +671,7 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
   const float E2 = 32.0f * 5.9604645e-8f * (((fabsf(qx) + fabsf(qy)) + fabsf(qz)) + sp[3]) * 1.0001f +
                    1e-12f * (1.0f + fabsf((float)px) + fabsf((float)py) + fabsf((float)pz) + sp[3]);
   const F2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
-  const F4* ls = (const F4*)lw;  // staged pairs: two 16-byte chunks each
+  const F4* ls = LANE ? (const F4*)(m.screen + 4 * (f0 + k)) : (const F4*)lw;  // pairs: two 16-byte chunks each
   const int np = (nf + 1) >> 1;
   float b1 = -__builtin_huge_valf(), b2 = -__builtin_huge_valf();
   int ib = 0;
@@ -673,6 +720,20 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
   const float thr = bf + E2 + 2.5e-7f * fabsf(bf);
   rejected = false;
   int i0 = 0;
+  if constexpr (LANE) {
+    const int npm = wave_max_int(np);
+    for (; i0 < npm; i0 += 4 * kScreenIlp) {
+      float mx[kScreenIlp];
+#pragma unroll
+      for (int u = 0; u < kScreenIlp; ++u) {
+        const int j = i0 + 4 * u;
+        mx[u] = j < np ? batch_max(j, true) : -__builtin_huge_valf();  // (a no-op update)
+      }
+#pragma unroll
+      for (int u = 0; u < kScreenIlp; ++u) update(mx[u], i0 + 4 * u);
+      if (!__any(active && !(b1 > thr))) { rejected = true; return true; }
+    }
+  } else {
   // the first 16 faces get a rejection test of their own: a hull that cannot
   // win is usually exposed by its first planes (3 % faster than waiting for
   // the first 32-face round)
@@ -694,6 +755,7 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
   }
   for (; i0 < np; i0 += 4) update(batch_max(i0, i0 + 4 > np), i0);
   if (!__any(active && !(b1 > thr))) { rejected = true; return true; }
+  }
   // exact fp64 first-index argmax over the best batch's faces
   const int fb = 2 * ib;
   hA = -tinf<T>();
@@ -720,17 +782,31 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
 // `bound`: the lane's best distance so far (only a result below it matters).
 // `lw`: this wave's LDS stage (m.stage_bytes). Whole wave active.
 // ---------------------------------------------------------------------------
-template <typename T>
+// LANE: k differs per lane (scene_eval's many-seed waves); nothing is staged,
+// every row is read from global memory (L1/L2) through per-lane pointers, and
+// the loops over faces run to the wave's largest count with the other lanes
+// masked — the same arithmetic per lane as the wave path, the same result.
+template <typename T, bool LANE = false>
 __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassModel<T>& m,
                                          const HullRow* __restrict__ ht, bool active, T bound,
                                          T& d, T& gx, T& gy, T& gz, T* __restrict__ lw,
                                          unsigned long long* __restrict__ stats) {
   typedef typename Row4<T>::type R;
-  const int f0 = __builtin_amdgcn_readfirstlane(ht[k].f0);
-  const int nf = __builtin_amdgcn_readfirstlane(ht[k + 1].f0) - f0;
-  const int v0 = __builtin_amdgcn_readfirstlane(ht[k].v0);
-  const int nv = __builtin_amdgcn_readfirstlane(ht[k + 1].v0) - v0;
+  int f0, nf, v0, nv;
+  if constexpr (LANE) {
+    f0 = ht[k].f0;
+    nf = ht[k + 1].f0 - f0;
+    v0 = ht[k].v0;
+    nv = ht[k + 1].v0 - v0;
+  } else {
+    f0 = __builtin_amdgcn_readfirstlane(ht[k].f0);
+    nf = __builtin_amdgcn_readfirstlane(ht[k + 1].f0) - f0;
+    v0 = __builtin_amdgcn_readfirstlane(ht[k].v0);
+    nv = __builtin_amdgcn_readfirstlane(ht[k + 1].v0) - v0;
+  }
+  const int nfm = LANE ? wave_max_int(nf) : nf;  // loop bound of the face loops
   uint64_t tp = phase_clock();
+  uint64_t tw = wt_now();
   // Stage layout: f64 contexts stage the fp32 screening pairs (16 B per face)
   // and read the fp64 planes — needed per lane only for the batch fix-up, the
   // max face and the certificates — from global memory (L1/L2); f32 contexts
@@ -741,17 +817,21 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   // FSDF_STAGE_PLANES64: f64 contexts also stage the fp64 planes (after the pairs)
   constexpr bool kP64 = kStagePairs<T> && FSDF_STAGE_PLANES64;
   const int npl = kP64 ? nf * cpr : 0;
-  for (int rep = (FSDF_ABLATE & 65536) ? 2 : 1; rep > 0; --rep)  // (2x: marginal-cost ablation)
-    stage_hull(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0), nv * cpr,
-               m.face_rows + f0, nf);
+  if constexpr (!LANE)
+    for (int rep = (FSDF_ABLATE & 65536) ? 2 : 1; rep > 0; --rep)  // (2x: marginal-cost ablation)
+      stage_hull(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0), nv * cpr,
+                 m.face_rows + f0, nf);
   phase_add(stats, 11, tp);
   tp = phase_clock();
-  const R* lp = kP64 ? (const R*)((const I4*)lw + np2) : (kStagePairs<T> ? (const R*)(m.planes + 4 * f0) : (const R*)lw);
-  const R* lv = (const R*)((const I4*)lw + np2 + npl);
-  const I4* lf = (const I4*)(lv + nv);
+  tw = wt_add(0, tw);
+  const R* lp = LANE ? (const R*)(m.planes + 4 * f0)
+                     : (kP64 ? (const R*)((const I4*)lw + np2)
+                             : (kStagePairs<T> ? (const R*)(m.planes + 4 * f0) : (const R*)lw));
+  const R* lv = LANE ? (const R*)(m.verts + 4 * v0) : (const R*)((const I4*)lw + np2 + npl);
+  const I4* lf = LANE ? (const I4*)(m.face_rows + f0) : (const I4*)((const R*)((const I4*)lw + np2 + npl) + nv);
   const T scale = (T)ht[k].hscale;
-  const CRow<T> gp = scalar_rows<T>(m.planes + 4 * f0);  // uniform plane rows (SGPR)
-  auto uplane = [&](int f) -> R { return FSDF_SCALAR_PLANES ? (R)gp[f] : lp[f]; };
+  const CRow<T> gp = scalar_rows<T>(m.planes + 4 * (LANE ? 0 : f0));  // uniform plane rows (SGPR)
+  auto uplane = [&](int f) -> R { return (FSDF_SCALAR_PLANES && !LANE) ? (R)gp[f] : lp[f]; };
   // two independent running maxima (even / odd faces) shorten the serial
   // compare chain; merged with the first-index rule, identical to one chain
   // Batches of kPlaneBatch rows, all of a batch's LDS reads issued before the
@@ -767,20 +847,23 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   if constexpr (sizeof(T) == 8) {
     bool rejected = false;
     if (FSDF_SCREEN32 && !screened)
-      screened = screen_plane_max(px, py, pz, k, f0, nf, m, ht, lw, lp, active, bound, hA, iA, rejected);
+      screened = screen_plane_max<T, LANE>(px, py, pz, k, f0, nf, m, ht, lw, lp, active, bound, hA, iA, rejected);
     if (FSDF_ABLATE & 131072) {  // 2x screen (marginal cost; identical result)
       T h2; int i2; bool r2;
-      const bool s2 = screen_plane_max(px + (T)0 * hA, py, pz, k, f0, nf, m, ht, lw, lp, active, bound, h2, i2, r2);
+      const bool s2 = screen_plane_max<T, LANE>(px + (T)0 * hA, py, pz, k, f0, nf, m, ht, lw, lp, active, bound, h2, i2, r2);
       screened = screened && s2; rejected = rejected && r2;
     }
     if (count_events(stats) && lane_id() == 0) {
       if (rejected) atomicAdd(stats + 20, 1ull);
       else if (!screened) atomicAdd(stats + 19, 1ull);
     }
+    if (rejected) wt_count(1, 1);
+    else if (!screened) wt_count(7, 1);
     if (rejected) {  // cannot win nor tie for any lane that needs it
       d = tinf<T>();
       gx = gy = gz = (T)0;
       phase_add(stats, 12, tp);
+      wt_add(1, tw);
       return;
     }
   }
@@ -801,8 +884,13 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
     if (h[0] > hA) { hA = h[0]; ib = i; }
   };
   int i0 = 0;
-  for (; i0 + kPlaneBatch <= nf; i0 += kPlaneBatch) batch(i0, false);  // one base address, immediate offsets
-  if (i0 < nf) batch(i0, true);
+  if constexpr (LANE) {
+    for (; i0 < nfm; i0 += kPlaneBatch)
+      if (i0 < nf) batch(i0, true);  // (the clamp is a no-op before the lane's last batch)
+  } else {
+    for (; i0 + kPlaneBatch <= nf; i0 += kPlaneBatch) batch(i0, false);  // one base address, immediate offsets
+    if (i0 < nf) batch(i0, true);
+  }
   // faces before batch ib are all < hA, so the window may start earlier
   const int fb = nf >= kPlaneBatch ? min(ib, nf - kPlaneBatch) : ib;
   iA = min(fb + kPlaneBatch - 1, nf - 1);
@@ -814,6 +902,7 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   }
   phase_add(stats, 12, tp);
   tp = phase_clock();
+  tw = wt_add(1, tw);
   if (count_events(stats) && lane_id() == 0) {
     atomicAdd(stats + 9, (unsigned long long)nf);
   }
@@ -841,7 +930,9 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   slow = slow && active && !(hmax - lb_margin > bound) && !(FSDF_ABLATE & 4);
   const uint64_t slow_mask = __ballot(slow);
   phase_add(stats, 13, tp);
+  tw = wt_add(2, tw);
   if (!slow_mask) return;
+  wt_count(2, 1);
   tp = phase_clock();
   if (count_events(stats) && (threadIdx.x & 63) == 0) {
     atomicAdd(stats + 2, 1ull);
@@ -864,6 +955,7 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   bool walking = todo;
   for (int step = 0; step < kWalkSteps && __any(walking); ++step) {
     if (count_events(stats) && lane_id() == 0) atomicAdd(stats + 21, 1ull);
+    wt_count(3, 1);
     if (walking) {
       int n1, n2;
       if (cert_step<T>(px, py, pz, cf, cr, lp, lv, lf, scale, n1, n2)) {
@@ -907,8 +999,8 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
       // no branches); then each lane walks its own marks in index order,
       // re-testing against its current b2 — the oracle's sequential scan,
       // without running closest_on_triangle for faces no lane needs.
-      for (int c0 = 0; c0 < nf; c0 += 64) {
-        const int cn = min(64, nf - c0);
+      for (int c0 = 0; c0 < nfm; c0 += 64) {
+        const int cn = max(0, min(64, nf - c0));
         uint64_t mark = 0;
         for (int j = 0; j < cn; ++j) {
           const T h = plane_h<T>(uplane(c0 + j), px, py, pz);
@@ -935,6 +1027,7 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
     }
   }
   phase_add(stats, 14, tp);
+  wt_add(3, tw);
   if (slow) {
     if (best2 > (T)0) {
       d = tsqrt(best2);
@@ -1204,6 +1297,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     cand[s] = left >= 64 ? ~0ull : (left > 0 ? (1ull << left) - 1 : 0ull);
   }
   const uint64_t tc = phase_clock();
+  uint64_t tw = wt_now();
   // the wave's bounding sphere (bbox centre, half diagonal) over the valid
   // lanes: precomputed per resident chunk at set_points (pose-independent,
   // the same arithmetic) or computed here
@@ -1271,6 +1365,9 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   }
   const float ub = __builtin_sqrtf(ub2);
   phase_add(stats, 10, tc);
+  tw = wt_add(4, tw);
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) wt_count(6, __builtin_popcountll(cand[s]));
   if (SPILL) {
     // distinct seed hulls of the valid lanes (one wave-evaluation each)
     uint64_t seeds = 0;
@@ -1302,6 +1399,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
       rbf_skin_from_field(F, sv, hx, hy, hz, c_, iG);
       if (valid && (sv < best || (sv == best && ks < bk))) { best = sv; bk = ks; gx = hx; gy = hy; gz = hz; }
     }
+    wt_add(5, tw);
   }
   // hull k is needed by a lane unless its lower bound exceeds min(ub, best)
   // by more than the fp32 rounding margin
@@ -1313,9 +1411,8 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   };
   // evaluations may run out of index order: ties keep the smaller k
   auto evaluate = [&](int k, bool need) {
-#if FSDF_WAVE_TIMES
-    if (lane == 0) ++fsdf_wave_ev[threadIdx.x >> 6][0];
-#endif
+    wt_count(0, 1);
+    wt_count(5, __builtin_popcountll(__ballot(need)));
     T dk, hx, hy, hz;
     hull_sdf<T>(px, py, pz, k, m, ht, need, best, dk, hx, hy, hz, lw, stats);
     if (count_events(stats)) {
@@ -1328,6 +1425,58 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     const int ks = RBF ? m.hull_surface[k] : k;
     if (need && (dk < best || (dk == best && ks < bk))) { best = dk; bk = ks; gx = hx; gy = hy; gz = hz; }
   };
+  // Many-seed waves (points among several hulls: each lane needs a few of
+  // them, the wave the union — evaluated one hull at a time, the wave's
+  // latency is the union's length): lane-divergent rounds instead — in every
+  // round each lane evaluates its own next hull (its seed, then the
+  // candidates it still needs in index order) through hull_sdf<LANE>; the
+  // wave needs max over lanes rounds instead of the union.
+  bool lane_mode = false;
+  if (kLaneSeeds > 0 && CULL && !RBF && !SPILL) {
+    int ns = 0;
+    for (uint64_t rem = __ballot(valid); rem && ns < kLaneSeeds; ++ns) {
+      const int sd = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(rem), 64));
+      rem &= ~__ballot(valid && kseed == sd);
+    }
+    lane_mode = ns >= kLaneSeeds;
+  }
+  if (lane_mode) {
+    uint64_t lc[SLOTS];
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) lc[s] = valid ? cand[s] & ~((kseed >> 6) == s ? 1ull << (kseed & 63) : 0ull) : 0ull;
+    bool seedp = valid;
+    for (;;) {
+      int k = -1;
+      if (seedp) {
+        k = kseed;
+        seedp = false;
+      } else {
+#pragma unroll
+        for (int s = 0; s < SLOTS; ++s) {
+          while (k < 0 && lc[s]) {
+            const int kk = 64 * s + __builtin_ctzll(lc[s]);
+            lc[s] &= lc[s] - 1;
+            if (needs(kk)) k = kk;
+          }
+        }
+      }
+      const uint64_t am = __ballot(k >= 0);
+      if (!am) break;
+      const bool act = k >= 0;
+      const int kf = __builtin_amdgcn_readfirstlane(__shfl(k, __builtin_ctzll(am), 64));
+      wt_count(0, 1);
+      wt_count(5, __builtin_popcountll(am));
+      T dk, hx, hy, hz;
+      hull_sdf<T, true>(px, py, pz, act ? k : kf, m, ht, act, best, dk, hx, hy, hz, lw, stats);
+      if (count_events(stats) && lane == 0) {
+        atomicAdd(stats + 1, 1ull);
+        atomicAdd(stats + 3, (unsigned long long)__builtin_popcountll(am));
+      }
+      if (act && (dk < best || (dk == best && k < bk))) { best = dk; bk = k; gx = hx; gy = hy; gz = hz; }
+    }
+    if (count_events(stats) && lane == 0) atomicAdd(stats + 0, 1ull);
+    return;
+  }
   uint64_t done[SLOTS];
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) done[s] = 0;
@@ -1368,9 +1517,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
       // bounds) is skipped; bounds only tighten, so it is done for good
       if (FSDF_SEED_SKIP && !__any(need)) continue;
       if (count_events(stats) && lane == 0) atomicAdd(stats + 5, 1ull);
-#if FSDF_WAVE_TIMES
-      if (lane == 0) ++fsdf_wave_ev[threadIdx.x >> 6][1];
-#endif
+      wt_count(4, 1);
     } else {
       while (!cm && slot < SLOTS - 1) {
         ++slot;
@@ -1415,6 +1562,7 @@ __device__ __forceinline__ void emit_chunk(T px, T py, T pz, bool valid, T best,
   }
   phase_add(out.stats, 18, t_iter);
   const uint64_t t_red = phase_clock();
+  const uint64_t tw = wt_now();
 #if FSDF_LDS_ATOMIC_SUMS
   // Hull surfaces: every valid lane adds its wrench into the LDS row of its
   // k* (ds_add_f64; lanes of one k* are applied in lane order by the LDS, so
@@ -1502,19 +1650,22 @@ __device__ __forceinline__ void emit_chunk(T px, T py, T pz, bool valid, T best,
     }
   }
   phase_add(out.stats, 17, t_st);
+  wt_add(6, tw);
 }
 
-// Per-block partial sums: entry t of logical block b. Entry-major (each
-// entry's column of blocks contiguous: the reduce kernel's reads coalesce) or
-// block-major (each workgroup writes its len sums as one contiguous row).
-// Block-major writes whole 64-B lines — WRITE_SIZE 88.6 -> 50.6 MB per M64
-// pass, pass kernel -2.2 % — but the reduce then reads strided: +10 us per
-// step (measured, profiles/r02). Entry-major stays.
-#ifndef FSDF_PARTIALS_BLOCK_MAJOR
-#define FSDF_PARTIALS_BLOCK_MAJOR 0
+// Per-block partial sums: entry t of logical block b, FSDF_PARTIALS_LAYOUT
+//   0 entry-major  partials[t][b]: each entry's column contiguous (the reduce
+//     coalesces), but a block writes one 8-B entry per 64-B line;
+//   1 block-major  partials[b][t]: whole-line writes (WRITE_SIZE 88.6 -> 50.6 MB
+//     per M64 pass, pass kernel -2.2 %), the reduce reads strided (+10 us);
+//   2 line tiles   partials[t / 8][b][t % 8]: a block writes whole 64-B lines
+//     and reduce_tiles_kernel reads whole lines.
+#ifndef FSDF_PARTIALS_LAYOUT
+#define FSDF_PARTIALS_LAYOUT 2
 #endif
 __device__ __forceinline__ int64_t pidx(int t, int b, int len, int nblocks) {
-  return FSDF_PARTIALS_BLOCK_MAJOR ? (int64_t)b * len + t : (int64_t)t * nblocks + b;
+  if (FSDF_PARTIALS_LAYOUT == 2) return ((int64_t)(t >> 3) * nblocks + b) * 8 + (t & 7);
+  return FSDF_PARTIALS_LAYOUT == 1 ? (int64_t)b * len + t : (int64_t)t * nblocks + b;
 }
 
 // ---------------------------------------------------------------------------
@@ -1572,7 +1723,7 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
     const uint64_t t_iter = phase_clock();
 #if FSDF_WAVE_TIMES
     const uint64_t w_t0 = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0) fsdf_wave_ev[wave][0] = fsdf_wave_ev[wave][1] = 0;
+    if (lane == 0) fsdf_wave_ev[wave][0] = fsdf_wave_ev[wave][1] = fsdf_wave_ph[wave][0] = fsdf_wave_ph[wave][1] = 0;
 #endif
 
     T best, gx, gy, gz;
@@ -1600,6 +1751,8 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
       out.stats[33 + 2 * wv] = __builtin_amdgcn_s_memrealtime();
       out.stats[32 + 8 * kMaxBlocks + 2 * wv] = fsdf_wave_ev[wave][0];
       out.stats[33 + 8 * kMaxBlocks + 2 * wv] = fsdf_wave_ev[wave][1];
+      out.stats[32 + 18 * kMaxBlocks + 2 * wv] = fsdf_wave_ph[wave][0];
+      out.stats[33 + 18 * kMaxBlocks + 2 * wv] = fsdf_wave_ph[wave][1];
     }
 #endif
   }
@@ -1933,6 +2086,61 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict
   if (threadIdx.x == 0) accum[j] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
 }
 
+// Line-tiled partials (FSDF_PARTIALS_LAYOUT 2): workgroup x (16 waves) sums
+// entries 8x .. 8x+7 over all blocks. The tile is read as a flat array of
+// 16-B pairs, fully coalesced: thread i reads pairs i + 1024 j (pair e holds
+// entries 2 (e & 3), +1 of block e >> 2), 16 loads in flight, so it always
+// sums the same two entries over blocks (i >> 2) + 256 j, in order; then per
+// entry pair a masked DPP wave sum and a fixed-order 16-wave combine
+// (deterministic). The schedule rebuild is a launch of its own (order_kernel).
+constexpr int kTileBlock = 1024;
+__global__ __launch_bounds__(kTileBlock) void reduce_tiles_kernel(const double* __restrict__ partials, int nblocks,
+                                                                  int len, double* __restrict__ accum,
+                                                                  int32_t* __restrict__ spill_ctr) {
+  const int x = blockIdx.x;
+  if (spill_ctr && x == 0 && threadIdx.x < 2) spill_ctr[threadIdx.x] = 0;
+  typedef double D2 __attribute__((ext_vector_type(2)));
+  const D2* tile = (const D2*)(partials + (int64_t)x * nblocks * 8);
+  const int np = 4 * nblocks;  // pairs in the tile
+  double s0 = 0.0, s1 = 0.0;
+  int e = threadIdx.x;
+  constexpr int U = 16;
+  for (; e + (U - 1) * kTileBlock < np; e += U * kTileBlock) {
+    D2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = tile[e + u * kTileBlock];
+#pragma unroll
+    for (int u = 0; u < U; ++u) { s0 += v[u][0]; s1 += v[u][1]; }
+  }
+  for (; e < np; e += kTileBlock) {
+    const D2 v = tile[e];
+    s0 += v[0];
+    s1 += v[1];
+  }
+  constexpr int W = kTileBlock / 64;
+  __shared__ double sh[8][W];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, q = lane & 3;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const double w0 = wave_sum(q == r ? s0 : 0.0), w1 = wave_sum(q == r ? s1 : 0.0);
+    if (lane == 0) { sh[2 * r][wave] = w0; sh[2 * r + 1][wave] = w1; }
+  }
+  __syncthreads();
+  const int t = 8 * x + (int)threadIdx.x;
+  if (threadIdx.x < 8 && t < len) {
+    double a[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      a[g] = (sh[threadIdx.x][4 * g] + sh[threadIdx.x][4 * g + 1]) + (sh[threadIdx.x][4 * g + 2] + sh[threadIdx.x][4 * g + 3]);
+    accum[t] = (a[0] + a[1]) + (a[2] + a[3]);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void order_kernel(const uint32_t* __restrict__ cost, int nblocks,
+                                                       int32_t* __restrict__ order) {
+  build_order(cost, nblocks, order);
+}
+
 // Reduce over sparse partials (PassOutputs::hull_mask): workgroup 0 sums the
 // cost entry, workgroup 1 + k the six entries of surface k over the blocks
 // whose mask has bit k (one mask load per block, not per entry), the rest one
@@ -2206,6 +2414,12 @@ hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const 
 hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum, hipStream_t s,
                          const uint32_t* cost, int32_t* order, int32_t* spill_ctr, const uint64_t* hull_mask,
                          int len6) {
+  if (FSDF_PARTIALS_LAYOUT == 2 && !hull_mask) {
+    hipLaunchKernelGGL(reduce_tiles_kernel, dim3((len + 7) / 8), dim3(kTileBlock), 0, s, partials, nblocks, len,
+                       d_accum, spill_ctr);
+    if (cost) hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kBlock), 0, s, cost, nblocks, order);
+    return hipGetLastError();
+  }
   if (hull_mask) {
     const int S = (len6 - 1) / 6;
     hipLaunchKernelGGL(reduce_sparse_kernel, dim3(1 + S + (len - len6) + (cost ? 1 : 0)), dim3(kBlock), 0, s,

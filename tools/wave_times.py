@@ -40,13 +40,22 @@ def main():
         c.eval(poses)
     lib = _lib.load()
     nw = -(-args.points // 64)
-    buf = np.zeros(32 + 4 * 4 * 16384 + 2 * 16384, np.uint64)
+    buf = np.zeros(32 + 26 * 16384, np.uint64)
     assert lib.fsdf_kernel_stats(c._ctx, 1, None) == 0
     c.eval(poses)
     assert lib.fsdf_kernel_stats(c._ctx, 0, buf.ctypes.data_as(ctypes.c_void_p)) == 0
     c.close()
     t = buf[32:32 + 2 * min(nw, 4 * 16384)].reshape(-1, 2).astype(np.int64)
     ev = buf[32 + 8 * 16384:32 + 8 * 16384 + 2 * min(nw, 4 * 16384)].reshape(-1, 2).astype(np.int64)
+    ph = buf[32 + 18 * 16384:32 + 18 * 16384 + 2 * min(nw, 4 * 16384)].reshape(-1, 2).astype(np.uint64)
+    ev_raw = buf[32 + 8 * 16384:32 + 8 * 16384 + 2 * min(nw, 4 * 16384)].reshape(-1, 2).astype(np.uint64)
+
+    def fields(a):  # (n, 2) packed 16-bit fields -> (n, 8)
+        return np.stack([(a[:, j // 4] >> np.uint64(16 * (j % 4))) & np.uint64(0xffff) for j in range(8)],
+                        1).astype(np.int64)
+    evf = fields(ev_raw)  # evals, rejects, slow, walk steps, seeds, need lanes, candidates, full scans
+    phf = fields(ph) * 0.01  # us: stage, screen, fast, search, cull, rbf, emit, -
+    ev = np.stack([evf[:, 0], evf[:, 4]], 1)
     nb = -(-args.points // 256)
     bt = buf[32 + 16 * 16384:32 + 16 * 16384 + 2 * min(nb, 16384)].reshape(-1, 2).astype(np.int64)
     if not t[:, 0].any():
@@ -78,6 +87,21 @@ def main():
            "block_minus_slowest_wave_us_mean": float(((bt[:, 1] - bt[:, 0]) * 0.01 - dur[:len(bt) * 4].reshape(-1, 4).max(1)).mean()),
            "block_start_to_first_wave_us_mean": float(((t[:len(bt) * 4, 0].reshape(-1, 4).min(1) - bt[:, 0]) * 0.01).mean()),
            "heaviest_waves": [[float(dur[i]), int(ev[i, 0]), int(ev[i, 1])] for i in np.argsort(-dur)[:12]]}
+    ev_names = ["evals", "rejects", "slow", "walk_steps", "seeds", "need_lanes", "candidates", "full_scans"]
+    ph_names = ["stage", "screen", "fast", "search", "cull", "rbf", "emit"]
+    heavy = np.argsort(-dur)[:16]
+    res["heaviest_detail"] = [{"us": round(float(dur[i]), 2), **{n: int(evf[i, j]) for j, n in enumerate(ev_names)},
+                               **{"t_" + n: round(float(phf[i, j]), 2) for j, n in enumerate(ph_names)}}
+                              for i in heavy]
+    tot = phf[:, :7].sum(0)
+    res["phase_us_total_frac"] = {n: round(float(tot[j] / dur.sum()), 4) for j, n in enumerate(ph_names)}
+    ne = max(int(evf[:, 0].sum()), 1)
+    res["per_eval_us"] = {n: round(float(phf[:, j].sum() / ne), 3) for j, n in enumerate(ph_names[:4])}
+    res["event_totals"] = {n: int(evf[:, j].sum()) for j, n in enumerate(ev_names)}
+    top = dur >= np.percentile(dur, 99)
+    res["top1pct"] = {"waves": int(top.sum()), "us_mean": float(dur[top].mean()),
+                      **{n: round(float(evf[top, j].mean()), 2) for j, n in enumerate(ev_names)},
+                      **{"t_" + n: round(float(phf[top, j].mean()), 2) for j, n in enumerate(ph_names)}}
     print(json.dumps(res))
     if args.json:
         np.savez_compressed(args.json.replace(".json", ".npz"), start=start, end=end, evals=ev)

@@ -1142,7 +1142,7 @@ extern "C" int fsdf_set_split_budget(fsdf_ctx* c, int32_t evals) {
 #define FSDF_WAVE_TIMES 0
 #endif
 // 24 counters; diagnostic builds with -DFSDF_WAVE_TIMES=1 append per-wave clocks
-static constexpr int kStatCount = FSDF_WAVE_TIMES ? 32 + 4 * 4 * fsdf::kMaxBlocks + 2 * fsdf::kMaxBlocks : 24;
+static constexpr int kStatCount = FSDF_WAVE_TIMES ? 32 + 32 * fsdf::kMaxBlocks : 24;
 
 extern "C" int fsdf_kernel_stats(fsdf_ctx* c, int32_t enable, uint64_t* counters) {
   if (!c) return FSDF_ERR_ARG;

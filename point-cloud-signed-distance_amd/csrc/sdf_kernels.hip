@@ -402,7 +402,10 @@ __shared__ unsigned long long fsdf_phase_acc[kBlock / 64][10];  // per wave, flu
 //   ev[1]: seed evaluations | needing lanes << 16 | wave candidates << 32 | full fp64 scans << 48
 //   ph[0]: 10-ns units in hull staging | screen | fast path | closest-feature search
 //   ph[1]: culling | RBF | segmented reduction + stores | -
-__shared__ unsigned long long fsdf_wave_ev[kBlock / 64][2];
+//   ev[2]: lane-evaluations through the closest-feature search | those whose
+//          hull won the lane | lanes spared the search by the h_max bound | -
+__shared__ unsigned long long fsdf_wave_ev[kBlock / 64][3];
+__shared__ bool fsdf_wt_slow[kBlock];  // per lane: the last hull_sdf ran its search
 __shared__ unsigned long long fsdf_wave_ph[kBlock / 64][2];
 #endif
 __device__ __forceinline__ uint64_t wt_now() {
@@ -807,6 +810,9 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   const int nfm = LANE ? wave_max_int(nf) : nf;  // loop bound of the face loops
   uint64_t tp = phase_clock();
   uint64_t tw = wt_now();
+#if FSDF_WAVE_TIMES
+  fsdf_wt_slow[threadIdx.x] = false;
+#endif
   // Stage layout: f64 contexts stage the fp32 screening pairs (16 B per face)
   // and read the fp64 planes — needed per lane only for the batch fix-up, the
   // max face and the certificates — from global memory (L1/L2); f32 contexts
@@ -927,8 +933,15 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   // far by more than the rounding of either value, hull k cannot win (nor tie)
   // and its exact distance is not needed — d stays hmax (> bound).
   const T lb_margin = (T)16 * cert_eps<T>() * (scale + ((fabs(px) + fabs(py)) + fabs(pz)));
+#if FSDF_WAVE_TIMES
+  wt_count(10, __builtin_popcountll(__ballot(slow && active && (hmax - lb_margin > bound))));
+#endif
   slow = slow && active && !(hmax - lb_margin > bound) && !(FSDF_ABLATE & 4);
   const uint64_t slow_mask = __ballot(slow);
+#if FSDF_WAVE_TIMES
+  wt_count(8, __builtin_popcountll(slow_mask));
+  fsdf_wt_slow[threadIdx.x] = slow;
+#endif
   phase_add(stats, 13, tp);
   tw = wt_add(2, tw);
   if (!slow_mask) return;
@@ -1410,11 +1423,17 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     return valid && needs_at(ht[k], pxf, pyf, pzf, fminf(ub, (float)best) + mrg);
   };
   // evaluations may run out of index order: ties keep the smaller k
+#if FSDF_WAVE_TIMES
+  uint64_t wt_slowk = 0;  // hulls whose evaluation ran this lane's search
+#endif
   auto evaluate = [&](int k, bool need) {
     wt_count(0, 1);
     wt_count(5, __builtin_popcountll(__ballot(need)));
     T dk, hx, hy, hz;
     hull_sdf<T>(px, py, pz, k, m, ht, need, best, dk, hx, hy, hz, lw, stats);
+#if FSDF_WAVE_TIMES
+    if (fsdf_wt_slow[threadIdx.x]) wt_slowk |= 1ull << (k & 63);
+#endif
     if (count_events(stats)) {
       const uint64_t nm = __ballot(need);
       if (lane == 0) {
@@ -1480,6 +1499,9 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   uint64_t done[SLOTS];
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) done[s] = 0;
+#if FSDF_WAVE_TIMES
+  auto wt_won = [&]() { wt_count(9, __builtin_popcountll(__ballot(valid && ((wt_slowk >> (bk & 63)) & 1)))); };
+#endif
   // ONE evaluation site (hull_sdf is large: two inlined copies doubled the
   // kernel's code to ~40 KB): first each lane's seed hull (Phase B, one
   // evaluation per distinct seed in the wave, so that `best` is tight), then
@@ -1533,6 +1555,9 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     }
     evaluate(k, need);
   }
+#if FSDF_WAVE_TIMES
+  wt_won();
+#endif
   if (count_events(stats) && lane == 0) atomicAdd(stats + 0, 1ull);
 }
 
@@ -1723,7 +1748,9 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
     const uint64_t t_iter = phase_clock();
 #if FSDF_WAVE_TIMES
     const uint64_t w_t0 = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0) fsdf_wave_ev[wave][0] = fsdf_wave_ev[wave][1] = fsdf_wave_ph[wave][0] = fsdf_wave_ph[wave][1] = 0;
+    if (lane == 0)
+      fsdf_wave_ev[wave][0] = fsdf_wave_ev[wave][1] = fsdf_wave_ev[wave][2] = fsdf_wave_ph[wave][0] =
+          fsdf_wave_ph[wave][1] = 0;
 #endif
 
     T best, gx, gy, gz;
@@ -1753,6 +1780,7 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
       out.stats[33 + 8 * kMaxBlocks + 2 * wv] = fsdf_wave_ev[wave][1];
       out.stats[32 + 18 * kMaxBlocks + 2 * wv] = fsdf_wave_ph[wave][0];
       out.stats[33 + 18 * kMaxBlocks + 2 * wv] = fsdf_wave_ph[wave][1];
+      out.stats[32 + 26 * kMaxBlocks + wv] = fsdf_wave_ev[wave][2];
     }
 #endif
   }

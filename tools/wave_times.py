@@ -40,7 +40,7 @@ def main():
         c.eval(poses)
     lib = _lib.load()
     nw = -(-args.points // 64)
-    buf = np.zeros(32 + 26 * 16384, np.uint64)
+    buf = np.zeros(32 + 32 * 16384, np.uint64)
     assert lib.fsdf_kernel_stats(c._ctx, 1, None) == 0
     c.eval(poses)
     assert lib.fsdf_kernel_stats(c._ctx, 0, buf.ctypes.data_as(ctypes.c_void_p)) == 0
@@ -55,6 +55,9 @@ def main():
                         1).astype(np.int64)
     evf = fields(ev_raw)  # evals, rejects, slow, walk steps, seeds, need lanes, candidates, full scans
     phf = fields(ph) * 0.01  # us: stage, screen, fast, search, cull, rbf, emit, -
+    e2 = buf[32 + 26 * 16384:32 + 26 * 16384 + min(nw, 4 * 16384)].astype(np.uint64)
+    ev2 = np.stack([(e2 >> np.uint64(16 * j)) & np.uint64(0xffff) for j in range(3)], 1).astype(np.int64)
+    # slow lane-evaluations | of which the hull won the lane | lanes spared the search by h_max
     ev = np.stack([evf[:, 0], evf[:, 4]], 1)
     nb = -(-args.points // 256)
     bt = buf[32 + 16 * 16384:32 + 16 * 16384 + 2 * min(nb, 16384)].reshape(-1, 2).astype(np.int64)
@@ -98,10 +101,15 @@ def main():
     ne = max(int(evf[:, 0].sum()), 1)
     res["per_eval_us"] = {n: round(float(phf[:, j].sum() / ne), 3) for j, n in enumerate(ph_names[:4])}
     res["event_totals"] = {n: int(evf[:, j].sum()) for j, n in enumerate(ev_names)}
+    e2n = ["slow_lane_evals", "slow_lane_evals_won", "lanes_spared_by_hmax"]
+    res["search_lanes"] = {n: int(ev2[:, j].sum()) for j, n in enumerate(e2n)}
+    for i, r in zip(heavy, res["heaviest_detail"]):
+        r.update({n: int(ev2[i, j]) for j, n in enumerate(e2n)})
     top = dur >= np.percentile(dur, 99)
     res["top1pct"] = {"waves": int(top.sum()), "us_mean": float(dur[top].mean()),
                       **{n: round(float(evf[top, j].mean()), 2) for j, n in enumerate(ev_names)},
-                      **{"t_" + n: round(float(phf[top, j].mean()), 2) for j, n in enumerate(ph_names)}}
+                      **{"t_" + n: round(float(phf[top, j].mean()), 2) for j, n in enumerate(ph_names)},
+                      **{n: round(float(ev2[top, j].mean()), 2) for j, n in enumerate(e2n)}}
     print(json.dumps(res))
     if args.json:
         np.savez_compressed(args.json.replace(".json", ".npz"), start=start, end=end, evals=ev)

@@ -143,6 +143,19 @@ int fsdf_config_gradient(int32_t nb, const int32_t* parent, const int32_t* kind,
                          const int32_t* surface_body, const double* surface_wrench, const double* body_wrench,
                          double* work, double* gq);
 
+/* RBF weight solve and its adjoint (host only, no device; the host side of
+ * the interpolating skins, src/Flash.jl:143-213, around fsdf_set_rbf_params and
+ * the pass). fsdf_rbf_solve: centres [n][3] (world), values [n] (0 surface
+ * points, -1 skeleton points) -> u [n+4] = (w, a, b) of
+ * [A P; Pᵀ 0] u = [v; 0], A_ij = |c_i - c_j|^3, P_i = (1, c_iᵀ); lu
+ * [(n+4)^2] and piv [n+4] receive the factorization for the adjoint.
+ * fsdf_rbf_adjoint: this surface's accumulator block [4n+4] (λ [n+4], then E
+ * [n][3]) -> G [n][3] = ∂cost/∂c_j (world); work [n+4]. flash/rbf.py solve /
+ * chain are the numpy twins. FSDF_ERR_DEGENERATE: singular system. */
+int fsdf_rbf_solve(int32_t n, const double* centres, const double* values, double* u, double* lu, int32_t* piv);
+int fsdf_rbf_adjoint(int32_t n, const double* centres, const double* u, const double* lu, const int32_t* piv,
+                     const double* block, double* G, double* work);
+
 /* The whole CostFunctor iteration of a rigid (hull-only) scene in one call:
  * fsdf_set_mechanism registers the mechanism tree (the arrays of
  * fsdf_tree_transforms, nq = num_positions) and, per surface of
@@ -152,12 +165,28 @@ int fsdf_config_gradient(int32_t nb, const int32_t* parent, const int32_t* kind,
  * rule: cost_out = Σ_p d*(p)^2 and grad_out [nq] = ∂cost/∂x at the caller's x
  * (quaternion blocks normalized for the evaluation, the projection in the
  * gradient) — CostFunctor(x) with its ForwardDiff gradient
- * (src/gradientdescent.jl:28-57) for scenes without deformations. RBF scenes
- * keep fsdf_eval + the host's weight solve (FSDF_ERR_STATE here). */
+ * (src/gradientdescent.jl:28-57). Scenes with RBF skins also declare their
+ * centres (fsdf_set_rbf_centres, below; FSDF_ERR_STATE until every RBF
+ * surface has them). */
 int fsdf_set_mechanism(fsdf_ctx* ctx, int32_t nb, const int32_t* parent, const int32_t* kind, const int32_t* qoff,
                        const double* axis, const double* AR, const double* At, const double* BR, const double* Bt,
                        int32_t nq, const int32_t* surface_body, const double* frame_R, const double* frame_t);
 int fsdf_value_and_gradient(fsdf_ctx* ctx, const double* x, double* cost_out, double* grad_out);
+/* RBF scenes in fsdf_value_and_gradient (after fsdf_set_mechanism): every RBF
+ * surface's centres are declared once — n_sp surface points (body, body-frame
+ * xyz, deformation row or -1; value 0) then n_sk skeleton points (value -1),
+ * n_sp + n_sk = its n_centers (src/Flash.jl:143-213) — and
+ * fsdf_set_deformations gives the deformation count (x = [q; δ], 3 per
+ * deformable point, src/gradientdescent.jl:9-17) and the regularizer weight
+ * (default_deformation_cost_weight = 10, :7). value_and_gradient then also
+ * places the centres (c = R_b (p + δ) + t_b), solves the weights, uploads the
+ * rows, and chains the pass's RBF block through the solve: cost_out = Σ d*^2 +
+ * weight Σ|δ|^2, grad_out [nq + 3 n_deform] (CostFunctor(x) with its gradient,
+ * src/gradientdescent.jl:28-57). */
+int fsdf_set_rbf_centres(fsdf_ctx* ctx, int32_t surface, int32_t n_sp, const int32_t* body_sp,
+                         const double* local_sp, const int32_t* deform_row_sp, int32_t n_sk, const int32_t* body_sk,
+                         const double* local_sk);
+int fsdf_set_deformations(fsdf_ctx* ctx, int32_t n_deform, double weight);
 
 /* ---- context ---------------------------------------------------------------- */
 int fsdf_create(fsdf_ctx** out, const fsdf_opts* opts);

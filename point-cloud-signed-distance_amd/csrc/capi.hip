@@ -82,6 +82,7 @@ struct fsdf_ctx {
   double* d_rbf64 = nullptr;     // per-pass RBF rows (f64)
   double* h_rbf[kPoseRing] = {}; // pinned staging ring for RBF rows (own slots and events,
   hipEvent_t rbf_ev[kPoseRing] = {};  // independent of the pose ring: poses of <= 64
+  std::vector<int32_t> h_surface_kind, h_n_centers;  // host copy of the surface list (set_surfaces)
   int rbf_slot = 0;                   // surfaces never touch theirs)
   bool rbf_ready = false;
   // posed model, double-buffered: pass i poses into buffer i % 2 on its own
@@ -150,6 +151,16 @@ struct fsdf_ctx {
     std::vector<int32_t> parent, kind, qoff, surface_body;
     std::vector<double> axis, AR, At, BR, Bt, frame_R, frame_t;
     std::vector<double> R, t, Rb, tb, poses, accum, work;  // scratch
+    // RBF surfaces (fsdf_set_rbf_centres), in surface order; n == 0: undeclared
+    struct Rbf {
+      int n_sp = 0, n = 0;
+      std::vector<int32_t> body, drow, piv;
+      std::vector<double> local, values, centres, u, lu, G, work;
+    };
+    std::vector<Rbf> rbf;
+    int n_deform = 0;
+    double weight = 10.0;  // default_deformation_cost_weight (src/gradientdescent.jl:7)
+    std::vector<double> rows, body_wrench;
   } mech;
   fsdf::SpillBufs* d_spill_dev = nullptr;  // device copy of the record (read by the pass kernel)
   fsdf::SpillBufs spill_dev_copy;          // what d_spill_dev holds (host, stable address)
@@ -572,6 +583,10 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   c->lm.stage_bytes = stage_bytes;
   c->lm.S = S;
   c->lm.R = R;
+  c->h_surface_kind = surface_kind;
+  c->h_n_centers.assign(S, 0);
+  for (int k = 0; k < S; ++k) c->h_n_centers[k] = surfs[k].kind == FSDF_SURFACE_RBF ? surfs[k].n_centers : 0;
+  c->mech.rbf.clear();  // centre declarations refer to the previous surface list
   c->lm.rbf_rows = nrows;
   c->lm.rbf_acc = rbf_acc_off.back();
   c->lm.hull_surface = c->d_hull_surface;
@@ -1016,12 +1031,73 @@ extern "C" int fsdf_set_mechanism(fsdf_ctx* c, int32_t nb, const int32_t* parent
   return FSDF_OK;
 }
 
+extern "C" int fsdf_set_rbf_centres(fsdf_ctx* c, int32_t surface, int32_t n_sp, const int32_t* body_sp,
+                                    const double* local_sp, const int32_t* deform_row_sp, int32_t n_sk,
+                                    const int32_t* body_sk, const double* local_sk) {
+  if (!c) return FSDF_ERR_ARG;
+  auto& M = c->mech;
+  if (M.nb == 0) return fail(c, FSDF_ERR_STATE, "set_rbf_centres: call fsdf_set_mechanism first");
+  const int S = c->lm.S;
+  if (surface < 0 || surface >= S || c->h_surface_kind[surface] != FSDF_SURFACE_RBF)
+    return fail(c, FSDF_ERR_ARG, "set_rbf_centres: surface %d is not an RBF surface", surface);
+  if (n_sp < 0 || n_sk < 0 || n_sp + n_sk != c->h_n_centers[surface] || (n_sp && (!body_sp || !local_sp)) ||
+      (n_sk && (!body_sk || !local_sk)))
+    return fail(c, FSDF_ERR_ARG, "set_rbf_centres: surface %d has %d centres, got %d + %d", surface,
+                c->h_n_centers[surface], n_sp, n_sk);
+  int r = 0;
+  for (int k = 0; k < surface; ++k) r += c->h_surface_kind[k] == FSDF_SURFACE_RBF;
+  M.rbf.resize(c->lm.R);
+  auto& D = M.rbf[r];
+  const int n = n_sp + n_sk;
+  D.n_sp = n_sp;
+  D.n = n;
+  D.body.resize(n);
+  D.drow.assign(n, -1);
+  D.local.resize(3 * n);
+  D.values.resize(n);
+  for (int j = 0; j < n; ++j) {
+    const bool sp = j < n_sp;
+    const int b = sp ? body_sp[j] : body_sk[j - n_sp];
+    if (b < -1 || b >= M.nb) return fail(c, FSDF_ERR_ARG, "set_rbf_centres: centre %d body %d", j, b);
+    D.body[j] = b;
+    if (sp && deform_row_sp) D.drow[j] = deform_row_sp[j];
+    if (D.drow[j] < -1) return fail(c, FSDF_ERR_ARG, "set_rbf_centres: centre %d deformation row", j);
+    const double* p = sp ? local_sp + 3 * j : local_sk + 3 * (j - n_sp);
+    for (int i = 0; i < 3; ++i) D.local[3 * j + i] = p[i];
+    D.values[j] = sp ? 0.0 : -1.0;  // src/Flash.jl:208-211
+  }
+  D.centres.resize(3 * n);
+  D.u.resize(n + 4);
+  D.lu.resize((size_t)(n + 4) * (n + 4));
+  D.piv.resize(n + 4);
+  D.G.resize(3 * n);
+  D.work.resize(n + 4);
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_set_deformations(fsdf_ctx* c, int32_t n_deform, double weight) {
+  if (!c) return FSDF_ERR_ARG;
+  if (n_deform < 0 || !std::isfinite(weight)) return fail(c, FSDF_ERR_ARG, "set_deformations: bad arguments");
+  c->mech.n_deform = n_deform;
+  c->mech.weight = weight;
+  return FSDF_OK;
+}
+
 extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cost_out, double* grad_out) {
   if (!c) return FSDF_ERR_ARG;
   auto& M = c->mech;
   if (M.nb == 0) return fail(c, FSDF_ERR_STATE, "value_and_gradient: no mechanism (call fsdf_set_mechanism)");
-  if (c->lm.R > 0)
-    return fail(c, FSDF_ERR_STATE, "value_and_gradient: RBF scenes need the host's weight solve (use fsdf_eval)");
+  const int R = c->lm.R;
+  if (R > 0) {
+    bool all = (int)M.rbf.size() == R;
+    for (int r = 0; all && r < R; ++r) all = M.rbf[r].n > 0;
+    if (!all) return fail(c, FSDF_ERR_STATE, "value_and_gradient: declare every RBF surface's centres (fsdf_set_rbf_centres)");
+    for (const auto& D : M.rbf)
+      for (int j = 0; j < D.n; ++j)
+        if (D.drow[j] >= M.n_deform)
+          return fail(c, FSDF_ERR_STATE, "value_and_gradient: deformation row %d >= %d (fsdf_set_deformations)",
+                      D.drow[j], M.n_deform);
+  }
   if (!x || !cost_out || !grad_out) return fail(c, FSDF_ERR_ARG, "value_and_gradient: null argument");
   HIPCHECK(c, hipSetDevice(c->device));
   // forward kinematics (quaternion blocks normalized inside: normalize!, src/gradientdescent.jl:30)
@@ -1029,6 +1105,33 @@ extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cos
                                 M.At.data(), M.BR.data(), M.Bt.data(), x, M.R.data(), M.t.data(), M.Rb.data(),
                                 M.tb.data());
   if (rc) return fail(c, rc, "value_and_gradient: forward kinematics (bad configuration)");
+  const double* delta = x + M.nq;
+  // RBF skins: centres c = R_b (p + δ) + t_b, the weight solve, the rows
+  // (flash/rbf.py solve / rows)
+  if (R > 0) {
+    M.rows.clear();
+    for (auto& D : M.rbf) {
+      for (int j = 0; j < D.n; ++j) {
+        double p[3] = {D.local[3 * j], D.local[3 * j + 1], D.local[3 * j + 2]};
+        if (D.drow[j] >= 0)
+          for (int i = 0; i < 3; ++i) p[i] += delta[3 * D.drow[j] + i];
+        const int b = D.body[j];
+        for (int i = 0; i < 3; ++i)
+          D.centres[3 * j + i] = b < 0 ? p[i]
+                                       : (M.R[9 * b + 3 * i] * p[0] + M.R[9 * b + 3 * i + 1] * p[1] +
+                                          M.R[9 * b + 3 * i + 2] * p[2]) + M.t[3 * b + i];
+      }
+      rc = fsdf_rbf_solve(D.n, D.centres.data(), D.values.data(), D.u.data(), D.lu.data(), D.piv.data());
+      if (rc) return fail(c, rc, "value_and_gradient: singular RBF system");
+      for (int j = 0; j < D.n; ++j) {
+        M.rows.insert(M.rows.end(), D.centres.begin() + 3 * j, D.centres.begin() + 3 * j + 3);
+        M.rows.push_back(D.u[j]);
+      }
+      M.rows.insert(M.rows.end(), D.u.begin() + D.n, D.u.end());
+    }
+    rc = fsdf_set_rbf_params(c, M.rows.data(), (int64_t)M.rows.size());
+    if (rc) return rc;
+  }
   // surface poses T_world_body · T_body_geometry (identity for surfaces without a body)
   const int S = c->lm.S;
   for (int k = 0; k < S; ++k) {
@@ -1051,11 +1154,49 @@ extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cos
   M.accum.resize(accum_len(c));
   rc = fetch(c, c->n, cost_out, M.accum.data(), nullptr, nullptr, nullptr, false);
   if (rc) return rc;
-  for (int i = 0; i < M.nq; ++i) grad_out[i] = 0.0;
+  for (int i = 0; i < M.nq + 3 * M.n_deform; ++i) grad_out[i] = 0.0;
+  // RBF chain (flash/rbf.py chain): G_j = ∂c/∂c_j through the solve -> body
+  // wrenches (F, M about the world origin; δc = -(ω·M + v·F)) and ∂c/∂δ
+  if (R > 0) {
+    M.body_wrench.assign(6 * M.nb, 0.0);
+    const double* block = M.accum.data() + 1 + 6 * S;
+    for (auto& D : M.rbf) {
+      rc = fsdf_rbf_adjoint(D.n, D.centres.data(), D.u.data(), D.lu.data(), D.piv.data(), block, D.G.data(),
+                            D.work.data());
+      if (rc) return fail(c, rc, "value_and_gradient: RBF adjoint");
+      block += 4 * D.n + 4;
+      for (int j = 0; j < D.n; ++j) {
+        const double* G = D.G.data() + 3 * j;
+        const double* cj = D.centres.data() + 3 * j;
+        const int b = D.body[j];
+        if (b >= 0) {
+          double* w = M.body_wrench.data() + 6 * b;
+          w[0] -= G[0];
+          w[1] -= G[1];
+          w[2] -= G[2];
+          w[3] -= cj[1] * G[2] - cj[2] * G[1];
+          w[4] -= cj[2] * G[0] - cj[0] * G[2];
+          w[5] -= cj[0] * G[1] - cj[1] * G[0];
+        }
+        if (D.drow[j] >= 0) {  // c_j = R_b (p_j + δ_j) + t_b
+          double* gd = grad_out + M.nq + 3 * D.drow[j];
+          for (int i = 0; i < 3; ++i)
+            gd[i] += b < 0 ? G[i] : (M.R[9 * b + i] * G[0] + M.R[9 * b + 3 + i] * G[1] + M.R[9 * b + 6 + i] * G[2]);
+        }
+      }
+    }
+  }
   rc = fsdf_config_gradient(M.nb, M.parent.data(), M.kind.data(), M.qoff.data(), M.axis.data(), M.Rb.data(),
-                            M.tb.data(), x, S, M.surface_body.data(), M.accum.data() + 1, nullptr, M.work.data(),
-                            grad_out);
+                            M.tb.data(), x, S, M.surface_body.data(), M.accum.data() + 1,
+                            R > 0 ? M.body_wrench.data() : nullptr, M.work.data(), grad_out);
   if (rc) return fail(c, rc, "value_and_gradient: chain rule");
+  // the deformation regularizer weight Σ|δ|^2 (src/gradientdescent.jl:33-37)
+  double reg = 0.0;
+  for (int i = 0; i < 3 * M.n_deform; ++i) {
+    reg += delta[i] * delta[i];
+    grad_out[M.nq + i] += 2.0 * M.weight * delta[i];
+  }
+  *cost_out += M.weight * reg;
   return FSDF_OK;
 }
 

@@ -78,6 +78,10 @@ _PROTOS = {
     "fsdf_config_gradient": (c_int32, [c_int32] + [c_void_p] * 7 + [c_int32] + [c_void_p] * 5),
     "fsdf_set_mechanism": (c_int32, [c_void_p, c_int32] + [c_void_p] * 8 + [c_int32] + [c_void_p] * 3),
     "fsdf_value_and_gradient": (c_int32, [c_void_p, c_void_p, POINTER(c_double), c_void_p]),
+    "fsdf_rbf_solve": (c_int32, [c_int32] + [c_void_p] * 5),
+    "fsdf_rbf_adjoint": (c_int32, [c_int32] + [c_void_p] * 7),
+    "fsdf_set_rbf_centres": (c_int32, [c_void_p, c_int32, c_int32] + [c_void_p] * 3 + [c_int32] + [c_void_p] * 2),
+    "fsdf_set_deformations": (c_int32, [c_void_p, c_int32, c_double]),
 }
 SYMBOLS = tuple(_PROTOS)
 
@@ -306,10 +310,29 @@ class Context:
                                            ptr(fr), ptr(ft)), self._ctx, "set_mechanism")
         self.nq = mechanism.num_positions
 
+    def set_rbf_centres(self, surface: int, surface_points, skeleton_points, deform_rows=None):
+        """Declare RBF surface `surface`'s centres for value_and_gradient:
+        lists of (body, body-frame xyz); deform_rows[j] = the deformation row of
+        surface point j (-1: rigid)."""
+        nsp, nsk = len(surface_points), len(skeleton_points)
+        bsp = np.ascontiguousarray([b for b, _ in surface_points], np.int32)
+        lsp = np.ascontiguousarray(np.reshape([p for _, p in surface_points], (nsp, 3)), np.float64)
+        dr = None if deform_rows is None else np.ascontiguousarray(deform_rows, np.int32)
+        bsk = np.ascontiguousarray([b for b, _ in skeleton_points], np.int32)
+        lsk = np.ascontiguousarray(np.reshape([p for _, p in skeleton_points], (nsk, 3)), np.float64)
+        check(self._lib.fsdf_set_rbf_centres(self._ctx, int(surface), nsp, ptr(bsp), ptr(lsp), ptr(dr), nsk, ptr(bsk),
+                                             ptr(lsk)), self._ctx, "set_rbf_centres")
+
+    def set_deformations(self, n_deform: int, weight: float):
+        """x = [q; δ] with 3·n_deform deformation entries, regularizer weight."""
+        check(self._lib.fsdf_set_deformations(self._ctx, int(n_deform), float(weight)), self._ctx, "set_deformations")
+        self.n_deform = int(n_deform)
+
     def value_and_gradient(self, x):
-        """(Σ d², ∂/∂x) of a rigid scene in one native call (FK, pass, chain rule)."""
+        """(cost, ∂cost/∂x) in one native call (FK, RBF solve, pass, chain rule,
+        regularizer)."""
         x = np.ascontiguousarray(x, np.float64)
-        g = np.empty(self.nq)
+        g = np.empty(self.nq + 3 * getattr(self, "n_deform", 0))
         c = c_double(0.0)
         check(self._lib.fsdf_value_and_gradient(self._ctx, ptr(x), ctypes.byref(c), ptr(g)), self._ctx,
               "value_and_gradient")

@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .core import ConvexGeometry, Manipulator, ManipulatorState, num_states, prepare_pass
+from .core import ConvexGeometry, InterpolatingGeometry, Manipulator, ManipulatorState, prepare_pass
 
 default_deformation_cost_weight = 10
 
@@ -96,14 +96,29 @@ class CostFunctor:
         self.ctx.set_points(self.sensed_points)
         self._resident = id(self)
         manipulator._resident_cloud = self._resident
-        # rigid scenes: the whole iteration (FK, pass, chain rule) in one native
-        # call (fsdf_value_and_gradient); deformable ones keep the host weight solve
-        self._native = not manipulator.has_rbf() and num_states(manipulator) == manipulator.mechanism.num_positions
-        if self._native and getattr(self.ctx, "_mechanism_of", None) is not manipulator:
-            surf = manipulator.surfaces
-            self.ctx.set_mechanism(manipulator.mechanism, [s.body for s in surf], [s.frame.R for s in surf],
-                                   [s.frame.t for s in surf])
-            self.ctx._mechanism_of = manipulator
+        # the whole iteration (FK, RBF weight solve, pass, chain rule,
+        # regularizer) in one native call (fsdf_value_and_gradient)
+        self._native = all(isinstance(s, (ConvexGeometry, InterpolatingGeometry)) for s in manipulator.surfaces)
+        if self._native and getattr(self.ctx, "_mechanism_of", None) != (manipulator, self.weight):
+            self._register_native()
+
+    def _register_native(self):
+        m, ctx = self.manipulator, self.ctx
+        surf = m.surfaces
+        hull = [isinstance(s, ConvexGeometry) for s in surf]
+        eye, zero = np.eye(3), np.zeros(3)
+        ctx.set_mechanism(m.mechanism, [s.body if h else -1 for s, h in zip(surf, hull)],
+                          [s.frame.R if h else eye for s, h in zip(surf, hull)],
+                          [s.frame.t if h else zero for s, h in zip(surf, hull)])
+        row0 = 0  # deformation rows in surface order (flash/rbf.py solve)
+        for k, s in enumerate(surf):
+            nd = s.num_deformations()
+            if isinstance(s, InterpolatingGeometry):
+                rows = np.arange(row0, row0 + nd, dtype=np.int32) if nd else None
+                ctx.set_rbf_centres(k, s.surface_points, s.skeleton_points, rows)
+            row0 += nd
+        ctx.set_deformations(m.num_deformations(), self.weight)
+        ctx._mechanism_of = (m, self.weight)
 
     def set_sensed_points(self, sensed_points):
         """Swap the resident cloud (a new frame): one upload + device sort; the
@@ -133,6 +148,8 @@ class CostFunctor:
         x = np.asarray(x, np.float64)
         if self._native:
             self._ensure_resident()
+            if getattr(self.ctx, "_mechanism_of", None) != (self.manipulator, self.weight):
+                self._register_native()  # another functor of this engine registered its own
             return self.ctx.value_and_gradient(x)
         c, accum, _ = self._pass(x)
         return c, gradient_from_accum(self.manipulator, x, accum, self._solves, self.weight)

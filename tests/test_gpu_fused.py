@@ -1,5 +1,5 @@
-"""GPU: fsdf_value_and_gradient — the whole CostFunctor iteration of a rigid
-scene in one native call (host FK, surface poses, one pass, chain rule) —
+"""GPU: fsdf_value_and_gradient — the whole CostFunctor iteration in one
+native call (host FK, surface poses, RBF weight solve, one pass, chain rule) —
 against the composed host path (Python poses, fsdf_eval, the numpy chain
 rule), on revolute (IRB140, M64) and quaternion-floating (the table, an
 un-normalized quaternion) mechanisms. The native poses are summed in another
@@ -48,18 +48,54 @@ def test_fused_matches_composed(name):
     assert c3 != c1
 
 
-def test_fused_refuses_rbf_scene():
-    """RBF scenes keep the host weight solve: the context refuses the fused call."""
-    import flash
-    from flash import Models, FlashNativeError
+def _rbf_scene(name):
+    from flash import Models
+    return Models.beanbag() if name == "c3_beanbag" else Models.irb_and_squishable()[0]
+
+
+@pytest.mark.parametrize("name", ["c3_beanbag", "c5_scene"])
+def test_fused_rbf_matches_golden_and_composed(name):
+    """RBF scenes (BASELINE configs 3, 5): the native iteration (centres from FK
+    + δ, LU weight solve, rows, pass, RBF adjoint, chain rule, regularizer)
+    against the oracle's golden dc/dx and against the composed host path
+    (numpy solve/chain on the same context). The two weight solves (LAPACK vs
+    the native LU) agree to ~1e-13, so the passes see rows equal to a few ulp."""
+    import os
+    from conftest import GOLDEN
     from flash.gradientdescent import CostFunctor
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    m = _rbf_scene(name)
+    nq = m.mechanism.num_positions
+    cf = CostFunctor(m, z["points"])
+    assert cf._native
+    x = np.asarray(z["x"], np.float64)
+    c1, g1 = cf.value_and_gradient(x)
+    reg = 10.0 * float(np.dot(x[nq:], x[nq:]))
+    assert c1 == pytest.approx(float(z["accum"][0]) + reg, rel=1e-9)
+    assert np.allclose(g1, z["dcdx"], rtol=1e-7, atol=1e-7 * np.abs(z["dcdx"]).max())
+    # deformations away from the golden state, vs the composed host path
+    x2 = x.copy()
+    x2[nq:] += 0.01 * np.random.default_rng(5).normal(size=len(x) - nq)
+    for xx in (x, x2):
+        c1, g1 = cf.value_and_gradient(xx)
+        cf._native = False
+        c0, g0 = cf.value_and_gradient(xx)
+        cf._native = True
+        assert c1 == pytest.approx(c0, rel=1e-10)
+        assert np.allclose(g1, g0, rtol=1e-8, atol=1e-8 * np.abs(g0).max())
+    c2, g2 = cf.value_and_gradient(x2)
+    assert c2 == c1 and np.array_equal(g2, g1)
+
+
+def test_fused_rbf_needs_declared_centres():
+    """An RBF scene without fsdf_set_rbf_centres is refused (FSDF_ERR_STATE)."""
+    from flash import Models, FlashNativeError, _lib
     m = Models.beanbag()
-    cf = CostFunctor(m, np.random.default_rng(1).normal(size=(100, 3)))
-    assert not cf._native
-    c, g = cf.value_and_gradient(np.zeros(flash.num_states(m)) + np.r_[1.0, np.zeros(flash.num_states(m) - 1)])
-    assert np.isfinite(c) and np.isfinite(g).all()
-    ctx = cf.ctx
+    c = _lib.Context(device=0)
+    c.set_surfaces([("rbf", len(s.surface_points) + len(s.skeleton_points)) for s in m.surfaces])
+    c.set_points(np.random.default_rng(1).normal(size=(100, 3)))
     mech = m.mechanism
-    ctx.set_mechanism(mech, [0] * len(m.surfaces), [np.eye(3)] * len(m.surfaces), [np.zeros(3)] * len(m.surfaces))
+    c.set_mechanism(mech, [-1] * len(m.surfaces), [np.eye(3)] * len(m.surfaces), [np.zeros(3)] * len(m.surfaces))
     with pytest.raises(FlashNativeError):
-        ctx.value_and_gradient(mech.zero_configuration())
+        c.value_and_gradient(mech.zero_configuration())
+    c.close()

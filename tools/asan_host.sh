@@ -1,6 +1,6 @@
 #!/bin/bash
 # AddressSanitizer on the host code (CPU; no GPU): instrumented builds of
-# csrc/hull.cpp + csrc/kinematics.cpp and oracle/flash_oracle.c, driven from
+# csrc/hull.cpp + csrc/kinematics.cpp + csrc/rbf_host.cpp and oracle/flash_oracle.c, driven from
 # Python with libasan preloaded. Exits non-zero on the first ASan report.
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -8,6 +8,7 @@ B=$R/build_asan
 mkdir -p $B
 g++ -O1 -g -fsanitize=address -fno-omit-frame-pointer -fPIC -shared -std=c++17 -I$R/include \
     $R/point-cloud-signed-distance_amd/csrc/hull.cpp $R/point-cloud-signed-distance_amd/csrc/kinematics.cpp \
+    $R/point-cloud-signed-distance_amd/csrc/rbf_host.cpp \
     -o $B/libfsdf_host_asan.so
 gcc -O1 -g -fsanitize=address -fno-omit-frame-pointer -fPIC -mfma -mavx2 -ffp-contract=off -fno-fast-math \
     -fopenmp -shared $R/oracle/flash_oracle.c -o $B/liboracle_asan.so -lm

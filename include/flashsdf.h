@@ -187,6 +187,14 @@ int fsdf_set_rbf_centres(fsdf_ctx* ctx, int32_t surface, int32_t n_sp, const int
                          const double* local_sp, const int32_t* deform_row_sp, int32_t n_sk, const int32_t* body_sk,
                          const double* local_sk);
 int fsdf_set_deformations(fsdf_ctx* ctx, int32_t n_deform, double weight);
+/* The same iteration split around a multi-GPU all-reduce (one context per
+ * rank, each over its shard): fsdf_eval_state_device(x) runs FK, the RBF solve,
+ * the poses and the pass into the DEVICE accumulator d_accum (asynchronous on
+ * the context's stream); after the caller's all-reduce (RCCL) and read-back,
+ * fsdf_state_gradient(x, accum) returns cost and gradient as
+ * fsdf_value_and_gradient does (reusing the FK / solve of the same x). */
+int fsdf_eval_state_device(fsdf_ctx* ctx, const double* x, double* d_accum);
+int fsdf_state_gradient(fsdf_ctx* ctx, const double* x, const double* accum, double* cost_out, double* grad_out);
 
 /* ---- context ---------------------------------------------------------------- */
 int fsdf_create(fsdf_ctx** out, const fsdf_opts* opts);

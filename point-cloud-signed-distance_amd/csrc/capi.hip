@@ -160,7 +160,7 @@ struct fsdf_ctx {
     std::vector<Rbf> rbf;
     int n_deform = 0;
     double weight = 10.0;  // default_deformation_cost_weight (src/gradientdescent.jl:7)
-    std::vector<double> rows, body_wrench;
+    std::vector<double> rows, body_wrench, x_prepared;
   } mech;
   fsdf::SpillBufs* d_spill_dev = nullptr;  // device copy of the record (read by the pass kernel)
   fsdf::SpillBufs spill_dev_copy;          // what d_spill_dev holds (host, stable address)
@@ -1083,28 +1083,30 @@ extern "C" int fsdf_set_deformations(fsdf_ctx* c, int32_t n_deform, double weigh
   return FSDF_OK;
 }
 
-extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cost_out, double* grad_out) {
-  if (!c) return FSDF_ERR_ARG;
+// The host halves of one CostFunctor iteration at x (fsdf_value_and_gradient
+// and its device-split form fsdf_eval_state_device + fsdf_state_gradient):
+// prepare = FK, RBF centres + weight solve + rows upload, surface poses;
+// finish = RBF adjoint, chain rule, regularizer from an accumulator.
+static int iteration_prepare(fsdf_ctx* c, const double* x, const char* who) {
   auto& M = c->mech;
-  if (M.nb == 0) return fail(c, FSDF_ERR_STATE, "value_and_gradient: no mechanism (call fsdf_set_mechanism)");
+  if (M.nb == 0) return fail(c, FSDF_ERR_STATE, "%s: no mechanism (call fsdf_set_mechanism)", who);
   const int R = c->lm.R;
   if (R > 0) {
     bool all = (int)M.rbf.size() == R;
     for (int r = 0; all && r < R; ++r) all = M.rbf[r].n > 0;
-    if (!all) return fail(c, FSDF_ERR_STATE, "value_and_gradient: declare every RBF surface's centres (fsdf_set_rbf_centres)");
+    if (!all) return fail(c, FSDF_ERR_STATE, "%s: declare every RBF surface's centres (fsdf_set_rbf_centres)", who);
     for (const auto& D : M.rbf)
       for (int j = 0; j < D.n; ++j)
         if (D.drow[j] >= M.n_deform)
-          return fail(c, FSDF_ERR_STATE, "value_and_gradient: deformation row %d >= %d (fsdf_set_deformations)",
-                      D.drow[j], M.n_deform);
+          return fail(c, FSDF_ERR_STATE, "%s: deformation row %d >= %d (fsdf_set_deformations)", who, D.drow[j],
+                      M.n_deform);
   }
-  if (!x || !cost_out || !grad_out) return fail(c, FSDF_ERR_ARG, "value_and_gradient: null argument");
   HIPCHECK(c, hipSetDevice(c->device));
   // forward kinematics (quaternion blocks normalized inside: normalize!, src/gradientdescent.jl:30)
   int rc = fsdf_tree_transforms(M.nb, M.parent.data(), M.kind.data(), M.qoff.data(), M.axis.data(), M.AR.data(),
                                 M.At.data(), M.BR.data(), M.Bt.data(), x, M.R.data(), M.t.data(), M.Rb.data(),
                                 M.tb.data());
-  if (rc) return fail(c, rc, "value_and_gradient: forward kinematics (bad configuration)");
+  if (rc) return fail(c, rc, "%s: forward kinematics (bad configuration)", who);
   const double* delta = x + M.nq;
   // RBF skins: centres c = R_b (p + δ) + t_b, the weight solve, the rows
   // (flash/rbf.py solve / rows)
@@ -1122,7 +1124,7 @@ extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cos
                                           M.R[9 * b + 3 * i + 2] * p[2]) + M.t[3 * b + i];
       }
       rc = fsdf_rbf_solve(D.n, D.centres.data(), D.values.data(), D.u.data(), D.lu.data(), D.piv.data());
-      if (rc) return fail(c, rc, "value_and_gradient: singular RBF system");
+      if (rc) return fail(c, rc, "%s: singular RBF system", who);
       for (int j = 0; j < D.n; ++j) {
         M.rows.insert(M.rows.end(), D.centres.begin() + 3 * j, D.centres.begin() + 3 * j + 3);
         M.rows.push_back(D.u[j]);
@@ -1149,21 +1151,25 @@ extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cos
       P[9 + i] = (Rw[3 * i] * Ft[0] + Rw[3 * i + 1] * Ft[1] + Rw[3 * i + 2] * Ft[2]) + M.t[3 * b + i];
     }
   }
-  rc = run_pass(c, M.poses.data(), c->d_pts, c->n, c->d_accum, nullptr, nullptr, nullptr, nullptr, true);
-  if (rc) return rc;
-  M.accum.resize(accum_len(c));
-  rc = fetch(c, c->n, cost_out, M.accum.data(), nullptr, nullptr, nullptr, false);
-  if (rc) return rc;
+  M.x_prepared.assign(x, x + M.nq + 3 * M.n_deform);
+  return FSDF_OK;
+}
+
+static int iteration_finish(fsdf_ctx* c, const double* x, const double* accum, double* cost_out, double* grad_out,
+                            const char* who) {
+  auto& M = c->mech;
+  const int R = c->lm.R, S = c->lm.S;
+  const double* delta = x + M.nq;
   for (int i = 0; i < M.nq + 3 * M.n_deform; ++i) grad_out[i] = 0.0;
   // RBF chain (flash/rbf.py chain): G_j = ∂c/∂c_j through the solve -> body
   // wrenches (F, M about the world origin; δc = -(ω·M + v·F)) and ∂c/∂δ
   if (R > 0) {
     M.body_wrench.assign(6 * M.nb, 0.0);
-    const double* block = M.accum.data() + 1 + 6 * S;
+    const double* block = accum + 1 + 6 * S;
     for (auto& D : M.rbf) {
-      rc = fsdf_rbf_adjoint(D.n, D.centres.data(), D.u.data(), D.lu.data(), D.piv.data(), block, D.G.data(),
-                            D.work.data());
-      if (rc) return fail(c, rc, "value_and_gradient: RBF adjoint");
+      const int rc = fsdf_rbf_adjoint(D.n, D.centres.data(), D.u.data(), D.lu.data(), D.piv.data(), block,
+                                      D.G.data(), D.work.data());
+      if (rc) return fail(c, rc, "%s: RBF adjoint", who);
       block += 4 * D.n + 4;
       for (int j = 0; j < D.n; ++j) {
         const double* G = D.G.data() + 3 * j;
@@ -1186,18 +1192,54 @@ extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cos
       }
     }
   }
-  rc = fsdf_config_gradient(M.nb, M.parent.data(), M.kind.data(), M.qoff.data(), M.axis.data(), M.Rb.data(),
-                            M.tb.data(), x, S, M.surface_body.data(), M.accum.data() + 1,
-                            R > 0 ? M.body_wrench.data() : nullptr, M.work.data(), grad_out);
-  if (rc) return fail(c, rc, "value_and_gradient: chain rule");
+  const int rc = fsdf_config_gradient(M.nb, M.parent.data(), M.kind.data(), M.qoff.data(), M.axis.data(),
+                                      M.Rb.data(), M.tb.data(), x, S, M.surface_body.data(), accum + 1,
+                                      R > 0 ? M.body_wrench.data() : nullptr, M.work.data(), grad_out);
+  if (rc) return fail(c, rc, "%s: chain rule", who);
   // the deformation regularizer weight Σ|δ|^2 (src/gradientdescent.jl:33-37)
   double reg = 0.0;
   for (int i = 0; i < 3 * M.n_deform; ++i) {
     reg += delta[i] * delta[i];
     grad_out[M.nq + i] += 2.0 * M.weight * delta[i];
   }
-  *cost_out += M.weight * reg;
+  *cost_out = accum[0] + M.weight * reg;
   return FSDF_OK;
+}
+
+extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cost_out, double* grad_out) {
+  if (!c) return FSDF_ERR_ARG;
+  if (!x || !cost_out || !grad_out) return fail(c, FSDF_ERR_ARG, "value_and_gradient: null argument");
+  int rc = iteration_prepare(c, x, "value_and_gradient");
+  if (rc) return rc;
+  auto& M = c->mech;
+  rc = run_pass(c, M.poses.data(), c->d_pts, c->n, c->d_accum, nullptr, nullptr, nullptr, nullptr, true);
+  if (rc) return rc;
+  M.accum.resize(accum_len(c));
+  rc = fetch(c, c->n, nullptr, M.accum.data(), nullptr, nullptr, nullptr, false);
+  if (rc) return rc;
+  return iteration_finish(c, x, M.accum.data(), cost_out, grad_out, "value_and_gradient");
+}
+
+extern "C" int fsdf_eval_state_device(fsdf_ctx* c, const double* x, double* d_accum) {
+  if (!c) return FSDF_ERR_ARG;
+  if (!x || !d_accum) return fail(c, FSDF_ERR_ARG, "eval_state_device: null argument");
+  int rc = iteration_prepare(c, x, "eval_state_device");
+  if (rc) return rc;
+  return run_pass(c, c->mech.poses.data(), c->d_pts, c->n, d_accum, nullptr, nullptr, nullptr, nullptr, true);
+}
+
+extern "C" int fsdf_state_gradient(fsdf_ctx* c, const double* x, const double* accum, double* cost_out,
+                                   double* grad_out) {
+  if (!c) return FSDF_ERR_ARG;
+  if (!x || !accum || !cost_out || !grad_out) return fail(c, FSDF_ERR_ARG, "state_gradient: null argument");
+  auto& M = c->mech;
+  const size_t nx = (size_t)M.nq + 3 * (size_t)M.n_deform;
+  // the FK / weight solve of the pass that produced accum (same x): reuse it
+  if (M.nb == 0 || M.x_prepared.size() != nx || memcmp(M.x_prepared.data(), x, nx * sizeof(double)) != 0) {
+    const int rc = iteration_prepare(c, x, "state_gradient");
+    if (rc) return rc;
+  }
+  return iteration_finish(c, x, accum, cost_out, grad_out, "state_gradient");
 }
 
 extern "C" int fsdf_skin(fsdf_ctx* c, const double* poses, const double* xyz, int64_t n, double* d_out,

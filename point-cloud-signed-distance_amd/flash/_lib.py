@@ -82,6 +82,8 @@ _PROTOS = {
     "fsdf_rbf_adjoint": (c_int32, [c_int32] + [c_void_p] * 7),
     "fsdf_set_rbf_centres": (c_int32, [c_void_p, c_int32, c_int32] + [c_void_p] * 3 + [c_int32] + [c_void_p] * 2),
     "fsdf_set_deformations": (c_int32, [c_void_p, c_int32, c_double]),
+    "fsdf_eval_state_device": (c_int32, [c_void_p, c_void_p, c_void_p]),
+    "fsdf_state_gradient": (c_int32, [c_void_p] + [c_void_p] * 2 + [POINTER(c_double), c_void_p]),
 }
 SYMBOLS = tuple(_PROTOS)
 
@@ -336,6 +338,22 @@ class Context:
         c = c_double(0.0)
         check(self._lib.fsdf_value_and_gradient(self._ctx, ptr(x), ctypes.byref(c), ptr(g)), self._ctx,
               "value_and_gradient")
+        return c.value, g
+
+    def eval_state_device(self, x, d_accum: int):
+        """FK, RBF solve, poses and the pass at x into the device accumulator
+        (asynchronous; value_and_gradient's first half)."""
+        x = np.ascontiguousarray(x, np.float64)
+        check(self._lib.fsdf_eval_state_device(self._ctx, ptr(x), c_void_p(d_accum)), self._ctx, "eval_state_device")
+
+    def state_gradient(self, x, accum):
+        """(cost, ∂cost/∂x) from an (all-reduced) host accumulator of the pass at x."""
+        x = np.ascontiguousarray(x, np.float64)
+        a = np.ascontiguousarray(accum, np.float64)
+        g = np.empty(self.nq + 3 * getattr(self, "n_deform", 0))
+        c = c_double(0.0)
+        check(self._lib.fsdf_state_gradient(self._ctx, ptr(x), ptr(a), ctypes.byref(c), ptr(g)), self._ctx,
+              "state_gradient")
         return c.value, g
 
     def set_split_budget(self, evals: int):

@@ -16,8 +16,8 @@ from __future__ import annotations
 import numpy as np
 
 from .core import ConvexGeometry, Manipulator, ManipulatorState, prepare_pass
-from .gradientdescent import (_regularizer, default_deformation_cost_weight, gradient_from_accum, normalize,
-                              unflatten)
+from .gradientdescent import (_regularizer, default_deformation_cost_weight, gradient_from_accum, native_capable,
+                              normalize, register_native, unflatten)
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
@@ -58,13 +58,24 @@ class ShardedCostFunctor:
         self.accum = torch.zeros(self.ctx.accum_len, dtype=torch.float64, device=self.dev)
         self.stream = torch.cuda.current_stream(self.dev)
         self.ctx.set_stream(self.stream.cuda_stream)
+        # native iterations (fsdf_eval_state_device + fsdf_state_gradient: FK,
+        # RBF solve, poses, pass; chain rule after the all-reduce)
+        self._native = native_capable(manipulator)
+
+    def _ensure_native(self):
+        if getattr(self.ctx, "_mechanism_of", None) != (self.manipulator, self.weight):
+            register_native(self.manipulator, self.ctx, self.weight)
 
     def launch(self, x):
         """Enqueue one residual pass + all-reduce (asynchronous)."""
-        unflatten(self.state, x)
-        normalize(self.state)
-        poses, self._solves = prepare_pass(self.ctx, self.manipulator, self.state.q, self.state.deformation_data)
-        self.ctx.eval_device(poses, self.accum.data_ptr())
+        if self._native:
+            self._ensure_native()
+            self.ctx.eval_state_device(np.asarray(x, np.float64), self.accum.data_ptr())
+        else:
+            unflatten(self.state, x)
+            normalize(self.state)
+            poses, self._solves = prepare_pass(self.ctx, self.manipulator, self.state.q, self.state.deformation_data)
+            self.ctx.eval_device(poses, self.accum.data_ptr())
         allreduce_accum(self.accum, self.group)
         return self.accum
 
@@ -86,5 +97,7 @@ class ShardedCostFunctor:
     def value_and_gradient(self, x):
         x = np.asarray(x, np.float64)
         acc = self.launch(x).cpu().numpy()
+        if self._native:
+            return self.ctx.state_gradient(x, acc)
         c = float(acc[0]) + _regularizer(self.state, self.weight)
         return c, chain_gradient(self.manipulator, x, acc, self.weight, self._solves)

@@ -79,6 +79,33 @@ def gradient_from_accum(manip: Manipulator, x: np.ndarray, accum: np.ndarray, so
     return np.concatenate([gq, gd])
 
 
+def native_capable(manipulator: Manipulator) -> bool:
+    """Scenes fsdf_value_and_gradient handles: convex hulls and RBF skins."""
+    return all(isinstance(s, (ConvexGeometry, InterpolatingGeometry)) for s in manipulator.surfaces)
+
+
+def register_native(manipulator: Manipulator, ctx, weight) -> None:
+    """Declare the mechanism, surface bodies/frames, RBF centres and
+    deformations to the context (fsdf_set_mechanism, fsdf_set_rbf_centres,
+    fsdf_set_deformations) for its native iterations."""
+    m = manipulator
+    surf = m.surfaces
+    hull = [isinstance(s, ConvexGeometry) for s in surf]
+    eye, zero = np.eye(3), np.zeros(3)
+    ctx.set_mechanism(m.mechanism, [s.body if h else -1 for s, h in zip(surf, hull)],
+                      [s.frame.R if h else eye for s, h in zip(surf, hull)],
+                      [s.frame.t if h else zero for s, h in zip(surf, hull)])
+    row0 = 0  # deformation rows in surface order (flash/rbf.py solve)
+    for k, s in enumerate(surf):
+        nd = s.num_deformations()
+        if isinstance(s, InterpolatingGeometry):
+            rows = np.arange(row0, row0 + nd, dtype=np.int32) if nd else None
+            ctx.set_rbf_centres(k, s.surface_points, s.skeleton_points, rows)
+        row0 += nd
+    ctx.set_deformations(m.num_deformations(), weight)
+    ctx._mechanism_of = (m, weight)
+
+
 class CostFunctor:
     """CostFunctor(manipulator, sensed_points) (src/gradientdescent.jl:41-57).
 
@@ -98,27 +125,12 @@ class CostFunctor:
         manipulator._resident_cloud = self._resident
         # the whole iteration (FK, RBF weight solve, pass, chain rule,
         # regularizer) in one native call (fsdf_value_and_gradient)
-        self._native = all(isinstance(s, (ConvexGeometry, InterpolatingGeometry)) for s in manipulator.surfaces)
+        self._native = native_capable(manipulator)
         if self._native and getattr(self.ctx, "_mechanism_of", None) != (manipulator, self.weight):
             self._register_native()
 
     def _register_native(self):
-        m, ctx = self.manipulator, self.ctx
-        surf = m.surfaces
-        hull = [isinstance(s, ConvexGeometry) for s in surf]
-        eye, zero = np.eye(3), np.zeros(3)
-        ctx.set_mechanism(m.mechanism, [s.body if h else -1 for s, h in zip(surf, hull)],
-                          [s.frame.R if h else eye for s, h in zip(surf, hull)],
-                          [s.frame.t if h else zero for s, h in zip(surf, hull)])
-        row0 = 0  # deformation rows in surface order (flash/rbf.py solve)
-        for k, s in enumerate(surf):
-            nd = s.num_deformations()
-            if isinstance(s, InterpolatingGeometry):
-                rows = np.arange(row0, row0 + nd, dtype=np.int32) if nd else None
-                ctx.set_rbf_centres(k, s.surface_points, s.skeleton_points, rows)
-            row0 += nd
-        ctx.set_deformations(m.num_deformations(), self.weight)
-        ctx._mechanism_of = (m, self.weight)
+        register_native(self.manipulator, self.ctx, self.weight)
 
     def set_sensed_points(self, sensed_points):
         """Swap the resident cloud (a new frame): one upload + device sort; the

@@ -52,7 +52,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP64_VALU_PEAK_TFLOPS = 78.6
 FP32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md
 SIMDS, CLOCK_HZ, CYCLES_PER_WAVE_OP = 1024, 2.4e9, 2   # MI355X_MICROARCH.md §Wave scheduling
-ITERS_PER_FRAME = 30           # examples/irb_and_squishable.ipynb: NaiveSolver iteration_limit
+ITERS_PER_FRAME = 30           # src/tracking.jl:10-13 default NaiveSolver iteration_limit (manipulator.ipynb: 30)
 
 CONFIGS = {
     # name: (model, default points, scaling, description)

@@ -401,7 +401,7 @@ __shared__ unsigned long long fsdf_phase_acc[kBlock / 64][10];  // per wave, flu
 //   ev[0]: hull evaluations | screen rejections << 16 | slow evaluations << 32 | walk steps << 48
 //   ev[1]: seed evaluations | needing lanes << 16 | wave candidates << 32 | full fp64 scans << 48
 //   ph[0]: 10-ns units in hull staging | screen | fast path | closest-feature search
-//   ph[1]: culling | RBF | segmented reduction + stores | -
+//   ph[1]: culling | RBF | segmented reduction + stores | descent walk (within the search)
 //   ev[2]: lane-evaluations through the closest-feature search | those whose
 //          hull won the lane | lanes spared the search by the h_max bound | -
 __shared__ unsigned long long fsdf_wave_ev[kBlock / 64][3];
@@ -591,9 +591,9 @@ __device__ __forceinline__ bool cert_step(T px, T py, T pz, int f, int reg,
   int g = f, j = reg;
   I4 r = fr;
   for (int it = 0; it < 32; ++it) {
+    const int g2 = fr_nbr(r, j);  // across edge v -> u
     const R Un = lv[fr_vert(r, j == 2 ? 0 : j + 1)];
     const T dot = mfma_(wx, Un[0] - V[0], mfma_(wy, Un[1] - V[1], wz * (Un[2] - V[2])));
-    const int g2 = fr_nbr(r, j);  // across edge v -> u
     if (dot > tol) {
       n1 = g != f ? g : g2;
       n2 = g != f && g2 != f ? g2 : -1;
@@ -966,6 +966,7 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   bool todo = !(FSDF_ABLATE & 256) && slow;
   int cf = fs, cr = rA;
   bool walking = todo;
+  const uint64_t tw_walk = wt_now();
   for (int step = 0; step < kWalkSteps && __any(walking); ++step) {
     if (count_events(stats) && lane_id() == 0) atomicAdd(stats + 21, 1ull);
     wt_count(3, 1);
@@ -994,6 +995,7 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
       }
     }
   }
+  wt_add(7, tw_walk);  // (the descent walk: certificates and steps)
   if (__any(todo) && !(FSDF_ABLATE & 512)) {
     if (count_events(stats) && (threadIdx.x & 63) == 0) atomicAdd(stats + 6, 1ull);
     const uint64_t scan_mask = __ballot(todo);

@@ -91,12 +91,12 @@ def main():
            "block_start_to_first_wave_us_mean": float(((t[:len(bt) * 4, 0].reshape(-1, 4).min(1) - bt[:, 0]) * 0.01).mean()),
            "heaviest_waves": [[float(dur[i]), int(ev[i, 0]), int(ev[i, 1])] for i in np.argsort(-dur)[:12]]}
     ev_names = ["evals", "rejects", "slow", "walk_steps", "seeds", "need_lanes", "candidates", "full_scans"]
-    ph_names = ["stage", "screen", "fast", "search", "cull", "rbf", "emit"]
+    ph_names = ["stage", "screen", "fast", "search", "cull", "rbf", "emit", "walk"]
     heavy = np.argsort(-dur)[:16]
     res["heaviest_detail"] = [{"us": round(float(dur[i]), 2), **{n: int(evf[i, j]) for j, n in enumerate(ev_names)},
                                **{"t_" + n: round(float(phf[i, j]), 2) for j, n in enumerate(ph_names)}}
                               for i in heavy]
-    tot = phf[:, :7].sum(0)
+    tot = phf[:, :8].sum(0)
     res["phase_us_total_frac"] = {n: round(float(tot[j] / dur.sum()), 4) for j, n in enumerate(ph_names)}
     ne = max(int(evf[:, 0].sum()), 1)
     res["per_eval_us"] = {n: round(float(phf[:, j].sum() / ne), 3) for j, n in enumerate(ph_names[:4])}

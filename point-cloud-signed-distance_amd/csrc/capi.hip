@@ -26,9 +26,6 @@
 namespace {
 
 constexpr int kPoseRing = 8;
-#ifndef FSDF_SPARSE_PARTIALS
-#define FSDF_SPARSE_PARTIALS 0  // 1: blocks store only the surfaces they touched (<= 64 surfaces); measured slower
-#endif
 #ifndef FSDF_CHUNK_WS
 #define FSDF_CHUNK_WS 1  // passes over the resident cloud read the chunk spheres of set_points
 #endif
@@ -114,7 +111,6 @@ struct fsdf_ctx {
   double* d_partials = nullptr;
   size_t partials_cap = 0;
   // cost-ordered schedule of resident-cloud passes (fsdf::PassOutputs::order)
-  uint64_t* d_hull_mask = nullptr;   // [kMaxBlocks] sparse partial sums (fsdf::PassOutputs::hull_mask)
   uint32_t* d_block_cost = nullptr;  // [kMaxBlocks]
   int32_t* d_block_order = nullptr;  // [kMaxBlocks]
   int order_nblocks = 0;             // grid the order was built for (0: none yet)
@@ -283,7 +279,6 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   dfree(c->d_stats);
   dfree(c->d_block_cost);
   dfree(c->d_block_order);
-  dfree(c->d_hull_mask);
   dfree(c->d_spill_ctr);
   dfree(c->d_spill_items);
   dfree(c->d_spill_res);
@@ -843,10 +838,6 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
   out.perm = d_perm;
   out.stats = c->stats_on ? c->d_stats : nullptr;
   out.chunk_ws = FSDF_CHUNK_WS && d_pts == c->d_pts && n == c->n ? c->d_chunk_ws : nullptr;  // resident cloud only
-  if (FSDF_SPARSE_PARTIALS && c->lm.S <= 64 && n > 0) {
-    if (!c->d_hull_mask) HIPCHECK(c, hipMalloc(&c->d_hull_mask, fsdf::kMaxBlocks * sizeof(uint64_t)));
-    out.hull_mask = c->d_hull_mask;
-  }
   if (schedule && n > 0) {
     if (!c->d_block_cost) {
       HIPCHECK(c, hipMalloc(&c->d_block_cost, fsdf::kMaxBlocks * sizeof(uint32_t)));
@@ -879,7 +870,7 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
     const bool rebuild = out.cost && (c->order_nblocks != nblocks || ++c->order_age >= kOrderEvery);
     HIPCHECK(c, fsdf::launch_reduce(c->d_partials, nblocks, accum_len(c), d_accum, c->stream,
                                     rebuild ? out.cost : nullptr, rebuild ? c->d_block_order : nullptr,
-                                    split ? c->d_spill_ctr : nullptr, out.hull_mask, 1 + 6 * c->lm.S));
+                                    split ? c->d_spill_ctr : nullptr));
     if (rebuild) {
       c->order_nblocks = nblocks;
       c->order_age = 0;

@@ -137,9 +137,6 @@ struct PassOutputs {
   // optional [n64/64][4] f32 bounding sphere of each 64-point chunk of the
   // resident cloud (launch_chunk_spheres at set_points; pose-independent)
   const float* chunk_ws = nullptr;
-  // optional sparse partial sums (<= 64 surfaces): [nblocks] bit k = the block
-  // wrote surface k's six entries (launch_reduce reads the others as zero)
-  uint64_t* hull_mask = nullptr;
 };
 
 // Surfaces whose poses ride in the pose kernel's arguments (12·64 doubles =
@@ -171,7 +168,7 @@ hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const 
 // blocks first) from this pass's costs, for the next pass of the same grid.
 hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum,
                          hipStream_t s, const uint32_t* cost = nullptr, int32_t* order = nullptr,
-                         int32_t* spill_ctr = nullptr, const uint64_t* hull_mask = nullptr, int len6 = 0);
+                         int32_t* spill_ctr = nullptr);
 
 hipError_t launch_to_f32(const double* src, float* dst, int64_t count, hipStream_t s);
 

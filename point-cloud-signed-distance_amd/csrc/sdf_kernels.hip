@@ -642,28 +642,10 @@ constexpr bool kStagePairs = sizeof(T) == 8 && FSDF_SCREEN32;
 #ifndef FSDF_SCREEN_ILP
 #define FSDF_SCREEN_ILP 4
 #endif
-// lane-divergent evaluation of waves with at least this many distinct seed
-// hulls (scene_eval; 0 = off)
-#ifndef FSDF_LANE_SEEDS
-#define FSDF_LANE_SEEDS 0
-#endif
-constexpr int kLaneSeeds = FSDF_LANE_SEEDS;
 constexpr int kScreenIlp = FSDF_SCREEN_ILP;  // independent 8-face batches per loop iteration  // see hull_sdf / fsdf_internal.h
 typedef float F2v __attribute__((ext_vector_type(2)));
 
-// wave-wide int max (butterfly; every lane gets the result). Whole wave active.
-__device__ __forceinline__ int wave_max_int(int v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
-  return v;
-}
-
-// LANE (lane-divergent evaluation, scene_eval's many-seed waves): k, f0 and nf
-// differ per lane and the pairs are read from global memory (L1/L2) instead of
-// the wave's LDS stage; every lane runs the same sequence of batches as the
-// wave path over its own hull (masked batches past its end), so its b1, b2,
-// ib — and the result — are bit-identical.
-template <typename T, bool LANE = false>
+template <typename T>
 __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0, int nf, const PassModel<T>& m,
                                                  const HullRow* __restrict__ ht, const void* __restrict__ lw,
                                                  const typename Row4<T>::type* __restrict__ lp, bool active,
@@ -674,7 +656,7 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
   const float E2 = 32.0f * 5.9604645e-8f * (((fabsf(qx) + fabsf(qy)) + fabsf(qz)) + sp[3]) * 1.0001f +
                    1e-12f * (1.0f + fabsf((float)px) + fabsf((float)py) + fabsf((float)pz) + sp[3]);
   const F2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
-  const F4* ls = LANE ? (const F4*)(m.screen + 4 * (f0 + k)) : (const F4*)lw;  // pairs: two 16-byte chunks each
+  const F4* ls = (const F4*)lw;  // staged pairs: two 16-byte chunks each
   const int np = (nf + 1) >> 1;
   float b1 = -__builtin_huge_valf(), b2 = -__builtin_huge_valf();
   int ib = 0;
@@ -723,20 +705,6 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
   const float thr = bf + E2 + 2.5e-7f * fabsf(bf);
   rejected = false;
   int i0 = 0;
-  if constexpr (LANE) {
-    const int npm = wave_max_int(np);
-    for (; i0 < npm; i0 += 4 * kScreenIlp) {
-      float mx[kScreenIlp];
-#pragma unroll
-      for (int u = 0; u < kScreenIlp; ++u) {
-        const int j = i0 + 4 * u;
-        mx[u] = j < np ? batch_max(j, true) : -__builtin_huge_valf();  // (a no-op update)
-      }
-#pragma unroll
-      for (int u = 0; u < kScreenIlp; ++u) update(mx[u], i0 + 4 * u);
-      if (!__any(active && !(b1 > thr))) { rejected = true; return true; }
-    }
-  } else {
   // the first 16 faces get a rejection test of their own: a hull that cannot
   // win is usually exposed by its first planes (3 % faster than waiting for
   // the first 32-face round)
@@ -758,7 +726,6 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
   }
   for (; i0 < np; i0 += 4) update(batch_max(i0, i0 + 4 > np), i0);
   if (!__any(active && !(b1 > thr))) { rejected = true; return true; }
-  }
   // exact fp64 first-index argmax over the best batch's faces
   const int fb = 2 * ib;
   hA = -tinf<T>();
@@ -785,29 +752,16 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
 // `bound`: the lane's best distance so far (only a result below it matters).
 // `lw`: this wave's LDS stage (m.stage_bytes). Whole wave active.
 // ---------------------------------------------------------------------------
-// LANE: k differs per lane (scene_eval's many-seed waves); nothing is staged,
-// every row is read from global memory (L1/L2) through per-lane pointers, and
-// the loops over faces run to the wave's largest count with the other lanes
-// masked — the same arithmetic per lane as the wave path, the same result.
-template <typename T, bool LANE = false>
+template <typename T>
 __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassModel<T>& m,
                                          const HullRow* __restrict__ ht, bool active, T bound,
                                          T& d, T& gx, T& gy, T& gz, T* __restrict__ lw,
                                          unsigned long long* __restrict__ stats) {
   typedef typename Row4<T>::type R;
-  int f0, nf, v0, nv;
-  if constexpr (LANE) {
-    f0 = ht[k].f0;
-    nf = ht[k + 1].f0 - f0;
-    v0 = ht[k].v0;
-    nv = ht[k + 1].v0 - v0;
-  } else {
-    f0 = __builtin_amdgcn_readfirstlane(ht[k].f0);
-    nf = __builtin_amdgcn_readfirstlane(ht[k + 1].f0) - f0;
-    v0 = __builtin_amdgcn_readfirstlane(ht[k].v0);
-    nv = __builtin_amdgcn_readfirstlane(ht[k + 1].v0) - v0;
-  }
-  const int nfm = LANE ? wave_max_int(nf) : nf;  // loop bound of the face loops
+  const int f0 = __builtin_amdgcn_readfirstlane(ht[k].f0);
+  const int nf = __builtin_amdgcn_readfirstlane(ht[k + 1].f0) - f0;
+  const int v0 = __builtin_amdgcn_readfirstlane(ht[k].v0);
+  const int nv = __builtin_amdgcn_readfirstlane(ht[k + 1].v0) - v0;
   uint64_t tp = phase_clock();
   uint64_t tw = wt_now();
 #if FSDF_WAVE_TIMES
@@ -823,21 +777,18 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   // FSDF_STAGE_PLANES64: f64 contexts also stage the fp64 planes (after the pairs)
   constexpr bool kP64 = kStagePairs<T> && FSDF_STAGE_PLANES64;
   const int npl = kP64 ? nf * cpr : 0;
-  if constexpr (!LANE)
-    for (int rep = (FSDF_ABLATE & 65536) ? 2 : 1; rep > 0; --rep)  // (2x: marginal-cost ablation)
-      stage_hull(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0), nv * cpr,
-                 m.face_rows + f0, nf);
+  for (int rep = (FSDF_ABLATE & 65536) ? 2 : 1; rep > 0; --rep)  // (2x: marginal-cost ablation)
+    stage_hull(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0), nv * cpr,
+               m.face_rows + f0, nf);
   phase_add(stats, 11, tp);
   tp = phase_clock();
   tw = wt_add(0, tw);
-  const R* lp = LANE ? (const R*)(m.planes + 4 * f0)
-                     : (kP64 ? (const R*)((const I4*)lw + np2)
-                             : (kStagePairs<T> ? (const R*)(m.planes + 4 * f0) : (const R*)lw));
-  const R* lv = LANE ? (const R*)(m.verts + 4 * v0) : (const R*)((const I4*)lw + np2 + npl);
-  const I4* lf = LANE ? (const I4*)(m.face_rows + f0) : (const I4*)((const R*)((const I4*)lw + np2 + npl) + nv);
+  const R* lp = kP64 ? (const R*)((const I4*)lw + np2) : (kStagePairs<T> ? (const R*)(m.planes + 4 * f0) : (const R*)lw);
+  const R* lv = (const R*)((const I4*)lw + np2 + npl);
+  const I4* lf = (const I4*)(lv + nv);
   const T scale = (T)ht[k].hscale;
-  const CRow<T> gp = scalar_rows<T>(m.planes + 4 * (LANE ? 0 : f0));  // uniform plane rows (SGPR)
-  auto uplane = [&](int f) -> R { return (FSDF_SCALAR_PLANES && !LANE) ? (R)gp[f] : lp[f]; };
+  const CRow<T> gp = scalar_rows<T>(m.planes + 4 * f0);  // uniform plane rows (SGPR)
+  auto uplane = [&](int f) -> R { return FSDF_SCALAR_PLANES ? (R)gp[f] : lp[f]; };
   // two independent running maxima (even / odd faces) shorten the serial
   // compare chain; merged with the first-index rule, identical to one chain
   // Batches of kPlaneBatch rows, all of a batch's LDS reads issued before the
@@ -853,10 +804,10 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   if constexpr (sizeof(T) == 8) {
     bool rejected = false;
     if (FSDF_SCREEN32 && !screened)
-      screened = screen_plane_max<T, LANE>(px, py, pz, k, f0, nf, m, ht, lw, lp, active, bound, hA, iA, rejected);
+      screened = screen_plane_max(px, py, pz, k, f0, nf, m, ht, lw, lp, active, bound, hA, iA, rejected);
     if (FSDF_ABLATE & 131072) {  // 2x screen (marginal cost; identical result)
       T h2; int i2; bool r2;
-      const bool s2 = screen_plane_max<T, LANE>(px + (T)0 * hA, py, pz, k, f0, nf, m, ht, lw, lp, active, bound, h2, i2, r2);
+      const bool s2 = screen_plane_max(px + (T)0 * hA, py, pz, k, f0, nf, m, ht, lw, lp, active, bound, h2, i2, r2);
       screened = screened && s2; rejected = rejected && r2;
     }
     if (count_events(stats) && lane_id() == 0) {
@@ -890,13 +841,8 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
     if (h[0] > hA) { hA = h[0]; ib = i; }
   };
   int i0 = 0;
-  if constexpr (LANE) {
-    for (; i0 < nfm; i0 += kPlaneBatch)
-      if (i0 < nf) batch(i0, true);  // (the clamp is a no-op before the lane's last batch)
-  } else {
-    for (; i0 + kPlaneBatch <= nf; i0 += kPlaneBatch) batch(i0, false);  // one base address, immediate offsets
-    if (i0 < nf) batch(i0, true);
-  }
+  for (; i0 + kPlaneBatch <= nf; i0 += kPlaneBatch) batch(i0, false);  // one base address, immediate offsets
+  if (i0 < nf) batch(i0, true);
   // faces before batch ib are all < hA, so the window may start earlier
   const int fb = nf >= kPlaneBatch ? min(ib, nf - kPlaneBatch) : ib;
   iA = min(fb + kPlaneBatch - 1, nf - 1);
@@ -1014,8 +960,8 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
       // no branches); then each lane walks its own marks in index order,
       // re-testing against its current b2 — the oracle's sequential scan,
       // without running closest_on_triangle for faces no lane needs.
-      for (int c0 = 0; c0 < nfm; c0 += 64) {
-        const int cn = max(0, min(64, nf - c0));
+      for (int c0 = 0; c0 < nf; c0 += 64) {
+        const int cn = min(64, nf - c0);
         uint64_t mark = 0;
         for (int j = 0; j < cn; ++j) {
           const T h = plane_h<T>(uplane(c0 + j), px, py, pz);
@@ -1446,58 +1392,6 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     const int ks = RBF ? m.hull_surface[k] : k;
     if (need && (dk < best || (dk == best && ks < bk))) { best = dk; bk = ks; gx = hx; gy = hy; gz = hz; }
   };
-  // Many-seed waves (points among several hulls: each lane needs a few of
-  // them, the wave the union — evaluated one hull at a time, the wave's
-  // latency is the union's length): lane-divergent rounds instead — in every
-  // round each lane evaluates its own next hull (its seed, then the
-  // candidates it still needs in index order) through hull_sdf<LANE>; the
-  // wave needs max over lanes rounds instead of the union.
-  bool lane_mode = false;
-  if (kLaneSeeds > 0 && CULL && !RBF && !SPILL) {
-    int ns = 0;
-    for (uint64_t rem = __ballot(valid); rem && ns < kLaneSeeds; ++ns) {
-      const int sd = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(rem), 64));
-      rem &= ~__ballot(valid && kseed == sd);
-    }
-    lane_mode = ns >= kLaneSeeds;
-  }
-  if (lane_mode) {
-    uint64_t lc[SLOTS];
-#pragma unroll
-    for (int s = 0; s < SLOTS; ++s) lc[s] = valid ? cand[s] & ~((kseed >> 6) == s ? 1ull << (kseed & 63) : 0ull) : 0ull;
-    bool seedp = valid;
-    for (;;) {
-      int k = -1;
-      if (seedp) {
-        k = kseed;
-        seedp = false;
-      } else {
-#pragma unroll
-        for (int s = 0; s < SLOTS; ++s) {
-          while (k < 0 && lc[s]) {
-            const int kk = 64 * s + __builtin_ctzll(lc[s]);
-            lc[s] &= lc[s] - 1;
-            if (needs(kk)) k = kk;
-          }
-        }
-      }
-      const uint64_t am = __ballot(k >= 0);
-      if (!am) break;
-      const bool act = k >= 0;
-      const int kf = __builtin_amdgcn_readfirstlane(__shfl(k, __builtin_ctzll(am), 64));
-      wt_count(0, 1);
-      wt_count(5, __builtin_popcountll(am));
-      T dk, hx, hy, hz;
-      hull_sdf<T, true>(px, py, pz, act ? k : kf, m, ht, act, best, dk, hx, hy, hz, lw, stats);
-      if (count_events(stats) && lane == 0) {
-        atomicAdd(stats + 1, 1ull);
-        atomicAdd(stats + 3, (unsigned long long)__builtin_popcountll(am));
-      }
-      if (act && (dk < best || (dk == best && k < bk))) { best = dk; bk = k; gx = hx; gy = hy; gz = hz; }
-    }
-    if (count_events(stats) && lane == 0) atomicAdd(stats + 0, 1ull);
-    return;
-  }
   uint64_t done[SLOTS];
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) done[s] = 0;
@@ -1706,7 +1600,6 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   __shared__ int split_mask;  // SPILL: waves of this block that split their chunk
-  __shared__ unsigned long long block_touched;  // sparse partials: surfaces with a nonzero sum
   // All LDS is one dynamic region (16-byte aligned carve, see pass_lds_bytes):
   //   red     [4 waves][kRedStride] f64  per-hull wrench sums + cost
   //   rbf_acc [4 waves][kMaxRbfAcc] f64  (RBF variants only)
@@ -1736,7 +1629,6 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
   const uint64_t t_block0 = __builtin_amdgcn_s_memrealtime();
 #endif
   if (SPILL && threadIdx.x == 0) split_mask = 0;  // ordered by load_hull_table's barrier
-  if (threadIdx.x == 0) block_touched = 0ull;
   const float smax = load_hull_table(m, ht);
 #if FSDF_PHASE_TIMING
   if (lane < 10) fsdf_phase_acc[wave][lane] = 0;
@@ -1796,10 +1688,6 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
   __syncthreads();
   const int len6 = 1 + 6 * m.S;
   const int len = len6 + (RBF ? m.rbf_acc_off[m.R] : 0);
-  // sparse partials (out.hull_mask, <= 64 surfaces): a block writes the six
-  // entries of the surfaces it touched (any nonzero sum) and their bit mask;
-  // the reduce skips the others (a skipped entry is an exact zero)
-  const bool sparse = out.hull_mask != nullptr;
   for (int t = threadIdx.x; t < len; t += kPassBlock) {
     double s;
     if (t < len6) {
@@ -1813,24 +1701,7 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
 #pragma unroll
       for (int w = 1; w < kPassBlock / 64; ++w) s += rbf_acc[w * kMaxRbfAcc + src];
     }
-    if (sparse) {
-      // the block sum goes back into wave 0's slot (only this thread reads it)
-      if (t >= 1 && t < len6 && s != 0.0) atomicOr(&block_touched, 1ull << ((t - 1) / 6));
-      if (t < len6) red[(t == 0) ? SLOTS * 64 * 6 : t - 1] = s;
-      else rbf_acc[RBF ? t - len6 : 0] = s;
-    } else {
-      out.partials[pidx(t, lb, len, gridDim.x)] = s;
-    }
-  }
-  if (sparse) {
-    __syncthreads();
-    const uint64_t touched = block_touched;
-    for (int t = threadIdx.x; t < len; t += kPassBlock) {
-      if (t >= 1 && t < len6 && !((touched >> ((t - 1) / 6)) & 1)) continue;
-      const double v = t < len6 ? red[(t == 0) ? SLOTS * 64 * 6 : t - 1] : rbf_acc[RBF ? t - len6 : 0];
-      out.partials[pidx(t, lb, len, gridDim.x)] = v;
-    }
-    if (threadIdx.x == 0) out.hull_mask[lb] = touched;
+    out.partials[pidx(t, lb, len, gridDim.x)] = s;
   }
   if (SPILL && threadIdx.x == 0 && split_mask) {
     out.spill_dev->blk_mask[lb] = split_mask;
@@ -1948,13 +1819,8 @@ __global__ __launch_bounds__(kPassBlock) void merge_kernel(const T* __restrict__
       double s = red[0][src];
 #pragma unroll
       for (int w = 1; w < kWaves; ++w) s += red[w][src];
-      double* pp = out.partials + pidx(t, lb, len, nblocks);
-      // sparse partials: an entry the pass kernel skipped holds stale data
-      const bool had = !out.hull_mask || t == 0 || ((out.hull_mask[lb] >> ((t - 1) / 6)) & 1);
-      *pp = had ? *pp + s : s;
+      out.partials[pidx(t, lb, len, nblocks)] += s;
     }
-    __syncthreads();
-    if (out.hull_mask && threadIdx.x == 0) out.hull_mask[lb] = m.S >= 64 ? ~0ull : (1ull << m.S) - 1;
     __syncthreads();  // the rows are reused by the next block
   }
 }
@@ -2087,19 +1953,14 @@ __device__ void build_order(const uint32_t* __restrict__ cost, int nb, int32_t* 
 
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict__ partials, int nblocks, int len,
                                                         double* __restrict__ accum, const uint32_t* __restrict__ cost,
-                                                        int32_t* __restrict__ order, int32_t* __restrict__ spill_ctr,
-                                                        const uint64_t* __restrict__ hull_mask, int len6) {
+                                                        int32_t* __restrict__ order, int32_t* __restrict__ spill_ctr) {
   const int j = blockIdx.x;
   if (spill_ctr && j == 0 && threadIdx.x < 2) spill_ctr[threadIdx.x] = 0;  // the split pass is done with them
   if (cost && j == (int)gridDim.x - 1) {  // the extra workgroup
     build_order(cost, nblocks, order);
     return;
   }
-  // sparse partials: hull entries of blocks that did not touch the hull are
-  // exact zeros, not stored (skipping them leaves the sums unchanged)
-  const bool masked = hull_mask && j >= 1 && j < len6;
-  const uint64_t bit = masked ? 1ull << ((j - 1) / 6) : 0ull;
-  auto at = [&](int b) { return (!masked || (hull_mask[b] & bit)) ? partials[pidx(j, b, len, nblocks)] : 0.0; };
+  auto at = [&](int b) { return partials[pidx(j, b, len, nblocks)]; };
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   int b = threadIdx.x;
   for (; b + 3 * kBlock < nblocks; b += 4 * kBlock) {
@@ -2171,69 +2032,6 @@ __global__ __launch_bounds__(kBlock) void order_kernel(const uint32_t* __restric
   build_order(cost, nblocks, order);
 }
 
-// Reduce over sparse partials (PassOutputs::hull_mask): workgroup 0 sums the
-// cost entry, workgroup 1 + k the six entries of surface k over the blocks
-// whose mask has bit k (one mask load per block, not per entry), the rest one
-// dense RBF entry each; the last (when cost/order are given) rebuilds the
-// schedule. Fixed order: per thread its blocks b = tid + 256 i in order, then
-// the DPP wave sum and the fixed 4-wave combine (deterministic).
-__global__ __launch_bounds__(kBlock) void reduce_sparse_kernel(const double* __restrict__ partials, int nblocks,
-                                                               int len, int S, double* __restrict__ accum,
-                                                               const uint64_t* __restrict__ hull_mask,
-                                                               const uint32_t* __restrict__ cost,
-                                                               int32_t* __restrict__ order,
-                                                               int32_t* __restrict__ spill_ctr) {
-  const int j = blockIdx.x;
-  if (cost && j == (int)gridDim.x - 1) {
-    build_order(cost, nblocks, order);
-    return;
-  }
-  if (spill_ctr && j == 0 && threadIdx.x < 2) spill_ctr[threadIdx.x] = 0;
-  const int len6 = 1 + 6 * S;
-  __shared__ double sh[6][kBlock / 64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (j >= 1 && j <= S) {
-    const int k = j - 1;
-    const uint64_t bit = 1ull << k;
-    double sv[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    // masks for 16 blocks in flight at once, then the (few) selected entries
-    for (int b0 = threadIdx.x; b0 < nblocks; b0 += 16 * kBlock) {
-      uint64_t m[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) m[i] = b0 + i * kBlock < nblocks ? hull_mask[b0 + i * kBlock] & bit : 0;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        if (m[i]) {
-#pragma unroll
-          for (int q = 0; q < 6; ++q) sv[q] += partials[pidx(1 + 6 * k + q, b0 + i * kBlock, len, nblocks)];
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const double w = wave_sum(sv[q]);
-      if (lane == 0) sh[q][wave] = w;
-    }
-    __syncthreads();
-    if (threadIdx.x < 6) accum[1 + 6 * k + threadIdx.x] = (sh[threadIdx.x][0] + sh[threadIdx.x][1]) +
-                                                          (sh[threadIdx.x][2] + sh[threadIdx.x][3]);
-    return;
-  }
-  const int t = j == 0 ? 0 : len6 + (j - 1 - S);  // cost, or a dense RBF entry
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-  int b = threadIdx.x;
-  for (; b + 3 * kBlock < nblocks; b += 4 * kBlock) {
-    s0 += partials[pidx(t, b, len, nblocks)];
-    s1 += partials[pidx(t, b + kBlock, len, nblocks)];
-    s2 += partials[pidx(t, b + 2 * kBlock, len, nblocks)];
-    s3 += partials[pidx(t, b + 3 * kBlock, len, nblocks)];
-  }
-  for (; b < nblocks; b += kBlock) s0 += partials[pidx(t, b, len, nblocks)];
-  const double w = wave_sum((s0 + s1) + (s2 + s3));
-  if (lane == 0) sh[0][wave] = w;
-  __syncthreads();
-  if (threadIdx.x == 0) accum[t] = (sh[0][0] + sh[0][1]) + (sh[0][2] + sh[0][3]);
-}
 
 __global__ void to_f32_kernel(const double* __restrict__ src, float* __restrict__ dst, int64_t count) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2442,22 +2240,15 @@ hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const 
 }
 
 hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum, hipStream_t s,
-                         const uint32_t* cost, int32_t* order, int32_t* spill_ctr, const uint64_t* hull_mask,
-                         int len6) {
-  if (FSDF_PARTIALS_LAYOUT == 2 && !hull_mask) {
+                         const uint32_t* cost, int32_t* order, int32_t* spill_ctr) {
+  if (FSDF_PARTIALS_LAYOUT == 2) {
     hipLaunchKernelGGL(reduce_tiles_kernel, dim3((len + 7) / 8), dim3(kTileBlock), 0, s, partials, nblocks, len,
                        d_accum, spill_ctr);
     if (cost) hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kBlock), 0, s, cost, nblocks, order);
     return hipGetLastError();
   }
-  if (hull_mask) {
-    const int S = (len6 - 1) / 6;
-    hipLaunchKernelGGL(reduce_sparse_kernel, dim3(1 + S + (len - len6) + (cost ? 1 : 0)), dim3(kBlock), 0, s,
-                       partials, nblocks, len, S, d_accum, hull_mask, cost, order, spill_ctr);
-    return hipGetLastError();
-  }
   hipLaunchKernelGGL(reduce_kernel, dim3(len + (cost ? 1 : 0)), dim3(kBlock), 0, s, partials, nblocks, len, d_accum,
-                     cost, order, spill_ctr, hull_mask, len6);
+                     cost, order, spill_ctr);
   return hipGetLastError();
 }
 

@@ -359,7 +359,7 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   const int K = (int)hulls.size();
   std::vector<double> verts, planes, sph, box;
   std::vector<int32_t> faces, face_hull, face_off, vert_hull, vert_off, face_rows;
-  int stage_bytes = 0;
+  int stage_bytes = 0, stage_p64 = 0;
   const int tsz_ = c->precision == 64 ? (int)sizeof(double) : (int)sizeof(float);
   face_off.push_back(0);
   vert_off.push_back(0);
@@ -469,16 +469,38 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
       // pairs, 32 B per two faces) and vertex rows of 4 T, one 16-byte face row
       // per face (M64 f64: 4864 B; 4 waves + the wrench rows + the hull table
       // stay under 40 KiB, i.e. 4 workgroups per CU)
-      const int plane_bytes = (tsz_ == 8 && FSDF_SCREEN32)
-                                  ? 32 * ((h.n_faces + 1) / 2) + (FSDF_STAGE_PLANES64 ? h.n_faces * 32 : 0)
-                                  : h.n_faces * 4 * tsz_;
+      const int plane_bytes = (tsz_ == 8 && FSDF_SCREEN32) ? 32 * ((h.n_faces + 1) / 2) : h.n_faces * 4 * tsz_;
       stage_bytes = std::max(stage_bytes, plane_bytes + h.n_vertices * 4 * tsz_ + 16 * h.n_faces);
+      // (+ the fp64 planes, 32 B per face, when they are staged too)
+      stage_p64 = std::max(stage_p64, plane_bytes + h.n_faces * 32 + h.n_vertices * 4 * tsz_ + 16 * h.n_faces);
     }
     face_off.push_back((int32_t)(face_hull.size()));
   }
   // the RBF centre rows are staged through the same buffer, 64 rows at a time
   // at least; the resident-order gradient store transposes 64 x 3 doubles in it
-  stage_bytes = (std::max(stage_bytes, 64 * 4 * std::max(tsz_, 8)) + 15) & ~15;
+  auto finish_stage = [&](int b) {
+    b = (std::max(b, 64 * 4 * std::max(tsz_, 8)) + 15) & ~15;
+    if (FSDF_RED_IN_STAGE && S <= 64 && rbf_surface.empty())
+      b = std::max(b, fsdf::kRedInStageMinBytes);  // wrench rows + transpose after the evaluation
+    return b;
+  };
+  stage_bytes = finish_stage(stage_bytes);
+  stage_p64 = finish_stage(stage_p64);
+  // f64 hull-only scenes of <= 64 surfaces also stage the fp64 planes when the
+  // one-chunk-per-wave pass (wrench rows in the stage) then still runs 4
+  // workgroups per CU
+  int planes64 = 0;
+  if (FSDF_STAGE_PLANES64 && tsz_ == 8 && FSDF_SCREEN32 && FSDF_RED_IN_STAGE && S <= 64 && rbf_surface.empty()) {
+    fsdf::LocalModel probe;
+    probe.K = K;
+    probe.S = S;
+    probe.stage_bytes = stage_p64;
+    if (fsdf::pass_lds_bytes(probe, false, true) <= (size_t)fsdf::kLdsPerCu / 4 &&
+        fsdf::pass_lds_bytes(probe, false) <= (size_t)fsdf::kMaxLds) {
+      planes64 = 1;
+      stage_bytes = stage_p64;
+    }
+  }
   {
     fsdf::LocalModel probe;
     probe.K = K;
@@ -576,6 +598,7 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   c->lm.vert_off = c->d_vert_off;
   c->lm.face_rows = c->d_face_rows;
   c->lm.stage_bytes = stage_bytes;
+  c->lm.planes64 = planes64;
   c->lm.S = S;
   c->lm.R = R;
   c->h_surface_kind = surface_kind;

@@ -44,8 +44,14 @@ namespace fsdf {
 #endif
 // f64 contexts stage the fp64 planes too (fix-up, max face, certificates read
 // LDS instead of L1/L2); sizes the stage in fsdf_set_surfaces
+// Wrench rows in the wave's stage for one-chunk-per-wave passes (pass_kernel
+// ALIAS); the stage is then at least the rows + the gradient transpose.
+#ifndef FSDF_RED_IN_STAGE
+#define FSDF_RED_IN_STAGE 1
+#endif
+constexpr int kRedInStageMinBytes = (64 * 6 + 2) * 8 + 64 * 3 * 8;
 #ifndef FSDF_STAGE_PLANES64
-#define FSDF_STAGE_PLANES64 0
+#define FSDF_STAGE_PLANES64 1
 #endif
 
 constexpr int kBlock = 256;
@@ -54,6 +60,7 @@ constexpr int kBlock = 256;
 #endif
 constexpr int kPassBlock = FSDF_PASS_BLOCK;  // pass-kernel workgroup (64 or a multiple)
 constexpr int kBoundFloats = 20;   // spheres_w row (sphere + oriented box)        // 4 waves of 64
+constexpr int kLdsPerCu = 163840;  // gfx950 LDS per CU
 constexpr int kMaxLds = 163840;    // LDS a workgroup may declare (gfx950)
 constexpr int kMaxHulls = 256;     // 4 accumulator slots per lane
 #ifndef FSDF_MAX_BLOCKS
@@ -83,6 +90,7 @@ struct LocalModel {
   const int32_t* vert_off = nullptr;
   const int32_t* face_rows = nullptr;  // [F][4]
   int stage_bytes = 0;                 // per-wave LDS stage, context precision (multiple of 16)
+  int planes64 = 0;                    // f64: stage the fp64 planes too (FSDF_STAGE_PLANES64, if they fit)
 };
 
 struct PosedModel {
@@ -179,7 +187,7 @@ hipError_t launch_chunk_spheres(int precision, const void* d_pts, int64_t n, flo
 int pass_blocks(int64_t n);
 
 // dynamic LDS of one pass (raycast=false) / raycast workgroup for this model
-size_t pass_lds_bytes(const LocalModel& lm, bool raycast);
+size_t pass_lds_bytes(const LocalModel& lm, bool raycast, bool alias = false);
 
 // Scratch of the per-frame spatial sort, owned by the context and grown only
 // (a frame makes no allocation).

@@ -266,6 +266,7 @@ struct PassModel {
   int S;  // surfaces (hulls + RBF skins), the k* index space
   int R;  // RBF skins
   int stage_bytes;  // LDS stage per wave (bytes, multiple of 16)
+  int planes64;     // f64 contexts: the fp64 planes are staged too (LocalModel::planes64)
   const int32_t* __restrict__ hull_surface;  // [K] surface index of hull h
   const int32_t* __restrict__ surface_kind;  // [S] FSDF_SURFACE_*
   const int32_t* __restrict__ rbf_surface;   // [R] surface index of RBF skin r
@@ -774,8 +775,9 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   constexpr int cpr = (int)sizeof(T) / 4;  // 16-byte chunks per row of 4 T
   const int np2 = kStagePairs<T> ? 2 * ((nf + 1) >> 1) : nf * cpr;  // chunks of region 0
   const I4* src0 = kStagePairs<T> ? (const I4*)(m.screen + 4 * (f0 + k)) : (const I4*)(m.planes + 4 * f0);
-  // FSDF_STAGE_PLANES64: f64 contexts also stage the fp64 planes (after the pairs)
-  constexpr bool kP64 = kStagePairs<T> && FSDF_STAGE_PLANES64;
+  // f64 contexts also stage the fp64 planes (after the pairs) when the model's
+  // stage has room for them at full occupancy (LocalModel::planes64)
+  const bool kP64 = kStagePairs<T> && m.planes64;
   const int npl = kP64 ? nf * cpr : 0;
   for (int rep = (FSDF_ABLATE & 65536) ? 2 : 1; rep > 0; --rep)  // (2x: marginal-cost ablation)
     stage_hull(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0), nv * cpr,
@@ -1594,31 +1596,45 @@ __device__ __forceinline__ int64_t pidx(int t, int b, int len, int nblocks) {
 // ---------------------------------------------------------------------------
 extern __shared__ __attribute__((aligned(16))) char fsdf_lds[];
 
-template <typename T, int SLOTS, bool CULL, bool RBF, bool SPILL = false>
+// ALIAS (one chunk per wave: n <= grid * 256; hull-only, <= 64 surfaces): the
+// wave's wrench rows live in its own hull stage, which is free once the
+// chunk's scene evaluation is done — 12 KiB less LDS per workgroup, spent on
+// staging the fp64 planes (FSDF_STAGE_PLANES64) at the same occupancy.
+template <typename T, int SLOTS, bool CULL, bool RBF, bool SPILL = false, bool ALIAS = false>
 __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)) void pass_kernel(
     const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out) {
+  static_assert(!ALIAS || (SLOTS == 1 && !RBF && !SPILL), "aliased wrench rows: hull-only, <= 64 surfaces");
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   __shared__ int split_mask;  // SPILL: waves of this block that split their chunk
   // All LDS is one dynamic region (16-byte aligned carve, see pass_lds_bytes):
-  //   red     [4 waves][kRedStride] f64  per-hull wrench sums + cost
+  //   red     [4 waves][kRedStride] f64  per-hull wrench sums + cost (not ALIAS)
   //   rbf_acc [4 waves][kMaxRbfAcc] f64  (RBF variants only)
-  //   stage   [4 waves][m.stage_bytes]   hull / RBF row stage
-  // per-hull wrench sums live in LDS from the start: row (s*64 + lane) of
-  // this wave's slab is owned by lane `lane` (hull s*64 + lane)
+  //   stage   [4 waves][m.stage_bytes]   hull / RBF row stage (ALIAS: after the
+  //                                      evaluation, the wave's red rows, then
+  //                                      the gradient transpose)
+  // per-hull wrench sums: row (s*64 + lane) of this wave's slab is owned by
+  // lane `lane` (hull s*64 + lane)
   constexpr int kRedStride = SLOTS * 64 * 6 + 2;
   double* red = (double*)fsdf_lds;
-  double* acc_row = red + wave * kRedStride + lane * 6;
+  HullRow* ht = (HullRow*)(fsdf_lds + (ALIAS ? 0 : ((kPassBlock / 64) * kRedStride + (RBF ? (kPassBlock / 64) * kMaxRbfAcc : 0)) * 8));
+  T* stage = (T*)((char*)(ht + m.K + 1) + wave * m.stage_bytes);
+  auto red_of = [&](int w) -> double* {
+    return ALIAS ? (double*)((char*)(ht + m.K + 1) + w * m.stage_bytes) : red + w * kRedStride;
+  };
+  double* acc_row = red_of(wave) + lane * 6;
+  auto zero_rows = [&]() {
 #pragma unroll
-  for (int s = 0; s < SLOTS; ++s)
+    for (int s = 0; s < SLOTS; ++s)
 #pragma unroll
-    for (int j = 0; j < 6; ++j) acc_row[s * 64 * 6 + j] = 0.0;
+      for (int j = 0; j < 6; ++j) acc_row[s * 64 * 6 + j] = 0.0;
+  };
+  if (!ALIAS) zero_rows();
+  bool ran = false;
   double cost_acc = 0.0;
   // RBF adjoint sums of this wave (lane 0 adds)
   double* rbf_acc = red + (kPassBlock / 64) * kRedStride;
   double* rbf_wave = rbf_acc + wave * kMaxRbfAcc;
-  HullRow* ht = (HullRow*)(fsdf_lds + ((kPassBlock / 64) * kRedStride + (RBF ? (kPassBlock / 64) * kMaxRbfAcc : 0)) * 8);
-  T* stage = (T*)((char*)(ht + m.K + 1) + wave * m.stage_bytes);
   const int stage_cap = m.stage_bytes / (4 * (int)sizeof(T));
   if (RBF)
     for (int e = lane; e < m.rbf_acc_off[m.R]; e += 64) rbf_wave[e] = 0.0;
@@ -1655,12 +1671,19 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
                                            cws, out.spill_dev, base, &spilled);
     if (!valid) bk = 0;
 
+    if (ALIAS) {  // the stage is free: this wave's rows go there (once: one chunk per wave)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      zero_rows();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      ran = true;
+    }
     if (SPILL && spilled) {
       // the merge kernel finishes this chunk (one wave-iteration per wave)
       if (lane == 0) atomicOr(&split_mask, 1 << wave);
     } else {
+      T* tstage = ALIAS ? (T*)((char*)stage + kRedStride * 8) : stage;  // gradient transpose after the rows
       emit_chunk<T, SLOTS, RBF>(px, py, pz, valid, best, bk, gx, gy, gz, i, base, n, m, out, acc_row, cost_acc,
-                                rbf_wave, stage, stage_cap, t_iter);
+                                rbf_wave, tstage, stage_cap, t_iter);
     }
     phase_add(out.stats, 15, t_iter);
 #if FSDF_WAVE_TIMES
@@ -1683,8 +1706,9 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
   if (out.stats && lane < 9) atomicAdd(out.stats + 10 + lane, fsdf_phase_acc[wave][lane]);
 #endif
   // ---- block combine (fixed order) ----
+  if (ALIAS && !ran) zero_rows();  // a wave past the cloud's end still contributes zeros
   cost_acc = wave_sum(cost_acc);
-  if (lane == 0) red[wave * kRedStride + SLOTS * 64 * 6] = cost_acc;
+  if (lane == 0) red_of(wave)[SLOTS * 64 * 6] = cost_acc;
   __syncthreads();
   const int len6 = 1 + 6 * m.S;
   const int len = len6 + (RBF ? m.rbf_acc_off[m.R] : 0);
@@ -1692,9 +1716,9 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
     double s;
     if (t < len6) {
       const int src = (t == 0) ? SLOTS * 64 * 6 : t - 1;
-      s = red[src];
+      s = red_of(0)[src];
 #pragma unroll
-      for (int w = 1; w < kPassBlock / 64; ++w) s += red[w * kRedStride + src];
+      for (int w = 1; w < kPassBlock / 64; ++w) s += red_of(w)[src];
     } else {
       const int src = RBF ? t - len6 : 0;
       s = rbf_acc[src];
@@ -2082,6 +2106,7 @@ static PassModel<T> pass_model(const LocalModel& lm, const PosedModel& pm) {
   m.S = lm.S;
   m.R = lm.R;
   m.stage_bytes = lm.stage_bytes;
+  m.planes64 = lm.planes64;
   m.hull_surface = lm.hull_surface;
   m.surface_kind = lm.surface_kind;
   m.rbf_surface = lm.rbf_surface;
@@ -2101,10 +2126,10 @@ static PassModel<T> pass_model(const LocalModel& lm, const PosedModel& pm) {
 
 static int slots_for(int S) { return S <= 64 ? 1 : (S <= 128 ? 2 : 4); }
 
-size_t pass_lds_bytes(const LocalModel& lm, bool raycast) {
+size_t pass_lds_bytes(const LocalModel& lm, bool raycast, bool alias) {
   const size_t waves = (size_t)(raycast ? kBlock : kPassBlock) / 64;
   const size_t stage = waves * (size_t)lm.stage_bytes + (size_t)(lm.K + 1) * sizeof(HullRow);
-  if (raycast) return stage;
+  if (raycast || alias) return stage;
   const size_t red = waves * (size_t)(slots_for(lm.S) * 64 * 6 + 2) * sizeof(double);
   const size_t rbf = lm.R > 0 ? waves * kMaxRbfAcc * sizeof(double) : 0;
   return red + rbf + stage;
@@ -2128,6 +2153,14 @@ static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void
       return;
     }
   }
+  if constexpr (!RBF && FSDF_RED_IN_STAGE) {
+    // one chunk per wave: the wrench rows alias the stage (pass_kernel ALIAS)
+    if (lm.S <= 64 && (int64_t)nblocks * kPassBlock >= n && lm.stage_bytes >= kRedInStageMinBytes) {
+      launch_lds(pass_kernel<T, 1, CULL, false, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
+                 pts, n, m, out);
+      return;
+    }
+  }
   if (lm.S <= 64) launch_lds(pass_kernel<T, 1, CULL, RBF>, nblocks, kPassBlock, lds, s, pts, n, m, out);
   else if (lm.S <= 128) launch_lds(pass_kernel<T, 2, CULL, RBF>, nblocks, kPassBlock, lds, s, pts, n, m, out);
   else launch_lds(pass_kernel<T, 4, CULL, RBF>, nblocks, kPassBlock, lds, s, pts, n, m, out);
@@ -2146,6 +2179,9 @@ static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm,
   const PassModel<T> m = pass_model<T>(lm, pm);
   if (out.spill.budget > 0)
     launch_lds(pass_kernel<T, 1, true, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false), s,
+               (const T*)d_pts, n, m, out);
+  else if (FSDF_RED_IN_STAGE && (int64_t)nblocks * kPassBlock >= n && lm.stage_bytes >= kRedInStageMinBytes)
+    launch_lds(pass_kernel<T, 1, true, false, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
                (const T*)d_pts, n, m, out);
   else
     launch_lds(pass_kernel<T, 1, true, false>, nblocks, kPassBlock, pass_lds_bytes(lm, false), s, (const T*)d_pts,

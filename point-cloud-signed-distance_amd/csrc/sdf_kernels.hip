@@ -753,7 +753,7 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
 // `bound`: the lane's best distance so far (only a result below it matters).
 // `lw`: this wave's LDS stage (m.stage_bytes). Whole wave active.
 // ---------------------------------------------------------------------------
-template <typename T>
+template <typename T, bool P64 = false>
 __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassModel<T>& m,
                                          const HullRow* __restrict__ ht, bool active, T bound,
                                          T& d, T& gx, T& gy, T& gz, T* __restrict__ lw,
@@ -775,9 +775,9 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   constexpr int cpr = (int)sizeof(T) / 4;  // 16-byte chunks per row of 4 T
   const int np2 = kStagePairs<T> ? 2 * ((nf + 1) >> 1) : nf * cpr;  // chunks of region 0
   const I4* src0 = kStagePairs<T> ? (const I4*)(m.screen + 4 * (f0 + k)) : (const I4*)(m.planes + 4 * f0);
-  // f64 contexts also stage the fp64 planes (after the pairs) when the model's
-  // stage has room for them at full occupancy (LocalModel::planes64)
-  const bool kP64 = kStagePairs<T> && m.planes64;
+  // f64 contexts also stage the fp64 planes (after the pairs) in the
+  // one-chunk-per-wave pass (P64: pass_kernel ALIAS, LocalModel::planes64)
+  constexpr bool kP64 = kStagePairs<T> && P64;
   const int npl = kP64 ? nf * cpr : 0;
   for (int rep = (FSDF_ABLATE & 65536) ? 2 : 1; rep > 0; --rep)  // (2x: marginal-cost ablation)
     stage_hull(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0), nv * cpr,
@@ -1234,7 +1234,7 @@ __device__ __forceinline__ bool split_wave(uint64_t seeds, int kseed, bool valid
   return true;
 }
 
-template <typename T, int SLOTS, bool CULL, bool RBF, bool SPILL = false>
+template <typename T, int SLOTS, bool CULL, bool RBF, bool SPILL = false, bool P64 = false>
 __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const PassModel<T>& m,
                                            const HullRow* __restrict__ ht, float smax, T* __restrict__ lw,
                                            unsigned long long* __restrict__ stats, T& best, int& bk, T& gx, T& gy,
@@ -1380,7 +1380,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     wt_count(0, 1);
     wt_count(5, __builtin_popcountll(__ballot(need)));
     T dk, hx, hy, hz;
-    hull_sdf<T>(px, py, pz, k, m, ht, need, best, dk, hx, hy, hz, lw, stats);
+    hull_sdf<T, P64>(px, py, pz, k, m, ht, need, best, dk, hx, hy, hz, lw, stats);
 #if FSDF_WAVE_TIMES
     if (fsdf_wt_slow[threadIdx.x]) wt_slowk |= 1ull << (k & 63);
 #endif
@@ -1596,10 +1596,11 @@ __device__ __forceinline__ int64_t pidx(int t, int b, int len, int nblocks) {
 // ---------------------------------------------------------------------------
 extern __shared__ __attribute__((aligned(16))) char fsdf_lds[];
 
-// ALIAS (one chunk per wave: n <= grid * 256; hull-only, <= 64 surfaces): the
-// wave's wrench rows live in its own hull stage, which is free once the
-// chunk's scene evaluation is done — 12 KiB less LDS per workgroup, spent on
-// staging the fp64 planes (FSDF_STAGE_PLANES64) at the same occupancy.
+// ALIAS (one chunk per wave: n <= grid * 256; hull-only, <= 64 surfaces; f64
+// models with LocalModel::planes64): the wave's wrench rows live in its own
+// hull stage, which is free once the chunk's scene evaluation is done — 12 KiB
+// less LDS per workgroup, spent on staging the fp64 planes with the hull
+// (hull_sdf P64) at the same occupancy.
 template <typename T, int SLOTS, bool CULL, bool RBF, bool SPILL = false, bool ALIAS = false>
 __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)) void pass_kernel(
     const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out) {
@@ -1667,7 +1668,7 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
     int bk;
     bool spilled = false;
     const F4* cws = out.chunk_ws ? (const F4*)out.chunk_ws + (base >> 6) : nullptr;
-    scene_eval<T, SLOTS, CULL, RBF, SPILL>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz,
+    scene_eval<T, SLOTS, CULL, RBF, SPILL, ALIAS>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz,
                                            cws, out.spill_dev, base, &spilled);
     if (!valid) bk = 0;
 
@@ -2155,7 +2156,7 @@ static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void
   }
   if constexpr (!RBF && FSDF_RED_IN_STAGE) {
     // one chunk per wave: the wrench rows alias the stage (pass_kernel ALIAS)
-    if (lm.S <= 64 && (int64_t)nblocks * kPassBlock >= n && lm.stage_bytes >= kRedInStageMinBytes) {
+    if (lm.S <= 64 && lm.planes64 && (int64_t)nblocks * kPassBlock >= n) {
       launch_lds(pass_kernel<T, 1, CULL, false, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
                  pts, n, m, out);
       return;
@@ -2180,7 +2181,7 @@ static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm,
   if (out.spill.budget > 0)
     launch_lds(pass_kernel<T, 1, true, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false), s,
                (const T*)d_pts, n, m, out);
-  else if (FSDF_RED_IN_STAGE && (int64_t)nblocks * kPassBlock >= n && lm.stage_bytes >= kRedInStageMinBytes)
+  else if (FSDF_RED_IN_STAGE && lm.planes64 && (int64_t)nblocks * kPassBlock >= n)
     launch_lds(pass_kernel<T, 1, true, false, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
                (const T*)d_pts, n, m, out);
   else

@@ -1631,7 +1631,6 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
       for (int j = 0; j < 6; ++j) acc_row[s * 64 * 6 + j] = 0.0;
   };
   if (!ALIAS) zero_rows();
-  bool ran = false;
   double cost_acc = 0.0;
   // RBF adjoint sums of this wave (lane 0 adds)
   double* rbf_acc = red + (kPassBlock / 64) * kRedStride;
@@ -1641,6 +1640,8 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
     for (int e = lane; e < m.rbf_acc_off[m.R]; e += 64) rbf_wave[e] = 0.0;
   // logical block of this launch slot (cost-ordered schedule, see PassOutputs)
   const int lb = out.order ? __builtin_amdgcn_readfirstlane(out.order[blockIdx.x]) : (int)blockIdx.x;
+  // (ALIAS: a wave past the cloud's end never evaluates; its rows are zeroed now)
+  if (ALIAS && (int64_t)lb * kPassBlock + wave * 64 >= n) zero_rows();
   const uint64_t t_block = out.cost ? __builtin_amdgcn_s_memrealtime() : 0;
 #if FSDF_WAVE_TIMES
   const uint64_t t_block0 = __builtin_amdgcn_s_memrealtime();
@@ -1676,7 +1677,6 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       zero_rows();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      ran = true;
     }
     if (SPILL && spilled) {
       // the merge kernel finishes this chunk (one wave-iteration per wave)
@@ -1707,7 +1707,6 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
   if (out.stats && lane < 9) atomicAdd(out.stats + 10 + lane, fsdf_phase_acc[wave][lane]);
 #endif
   // ---- block combine (fixed order) ----
-  if (ALIAS && !ran) zero_rows();  // a wave past the cloud's end still contributes zeros
   cost_acc = wave_sum(cost_acc);
   if (lane == 0) red_of(wave)[SLOTS * 64 * 6] = cost_acc;
   __syncthreads();

@@ -192,7 +192,8 @@ int fsdf_set_deformations(fsdf_ctx* ctx, int32_t n_deform, double weight);
  * the poses and the pass into the DEVICE accumulator d_accum (asynchronous on
  * the context's stream); after the caller's all-reduce (RCCL) and read-back,
  * fsdf_state_gradient(x, accum) returns cost and gradient as
- * fsdf_value_and_gradient does (reusing the FK / solve of the same x). */
+ * fsdf_value_and_gradient does, on the FK / weight solve of that pass: x must
+ * be the x of the last fsdf_eval_state_device (FSDF_ERR_STATE otherwise). */
 int fsdf_eval_state_device(fsdf_ctx* ctx, const double* x, double* d_accum);
 int fsdf_state_gradient(fsdf_ctx* ctx, const double* x, const double* accum, double* cost_out, double* grad_out);
 

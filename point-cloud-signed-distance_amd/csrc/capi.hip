@@ -1248,11 +1248,10 @@ extern "C" int fsdf_state_gradient(fsdf_ctx* c, const double* x, const double* a
   if (!x || !accum || !cost_out || !grad_out) return fail(c, FSDF_ERR_ARG, "state_gradient: null argument");
   auto& M = c->mech;
   const size_t nx = (size_t)M.nq + 3 * (size_t)M.n_deform;
-  // the FK / weight solve of the pass that produced accum (same x): reuse it
-  if (M.nb == 0 || M.x_prepared.size() != nx || memcmp(M.x_prepared.data(), x, nx * sizeof(double)) != 0) {
-    const int rc = iteration_prepare(c, x, "state_gradient");
-    if (rc) return rc;
-  }
+  // the chain rule runs on the FK / weight solve of the pass that produced
+  // accum: x must be that pass's x (fsdf_eval_state_device)
+  if (M.nb == 0 || M.x_prepared.size() != nx || memcmp(M.x_prepared.data(), x, nx * sizeof(double)) != 0)
+    return fail(c, FSDF_ERR_STATE, "state_gradient: x is not the x of the last fsdf_eval_state_device");
   return iteration_finish(c, x, accum, cost_out, grad_out, "state_gradient");
 }
 

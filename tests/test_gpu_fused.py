@@ -99,3 +99,35 @@ def test_fused_rbf_needs_declared_centres():
     with pytest.raises(FlashNativeError):
         c.value_and_gradient(mech.zero_configuration())
     c.close()
+
+
+def test_state_split_and_validation():
+    """fsdf_eval_state_device + fsdf_state_gradient (the sharded path's halves)
+    equal fsdf_value_and_gradient; the chain rule refuses an x other than the
+    pass's; deformation rows beyond fsdf_set_deformations are refused."""
+    import os
+    import torch
+    from conftest import GOLDEN
+    from flash import FlashNativeError
+    from flash.gradientdescent import CostFunctor
+    z = np.load(os.path.join(GOLDEN, "c5_scene.npz"))
+    from flash import Models
+    m = Models.irb_and_squishable()[0]
+    cf = CostFunctor(m, z["points"])
+    x = np.asarray(z["x"], np.float64)
+    c1, g1 = cf.value_and_gradient(x)
+    ctx = cf.ctx
+    acc = torch.zeros(ctx.accum_len, dtype=torch.float64, device="cuda:0")
+    ctx.set_stream(torch.cuda.current_stream(0).cuda_stream)
+    ctx.eval_state_device(x, acc.data_ptr())
+    c2, g2 = ctx.state_gradient(x, acc.cpu().numpy())
+    ctx.set_stream(None)
+    assert c2 == c1 and np.array_equal(g2, g1)
+    with pytest.raises(FlashNativeError):
+        ctx.state_gradient(x + 1e-3, acc.cpu().numpy())
+    ctx.set_deformations(1, 10.0)  # the squishable's 13 deformable points need 13 rows
+    with pytest.raises(FlashNativeError):
+        ctx.value_and_gradient(x[:m.mechanism.num_positions + 3])
+    ctx._mechanism_of = None  # the functor re-registers before its next call
+    c3, g3 = cf.value_and_gradient(x)
+    assert c3 == c1 and np.array_equal(g3, g1)

@@ -131,3 +131,26 @@ def test_state_split_and_validation():
     ctx._mechanism_of = None  # the functor re-registers before its next call
     c3, g3 = cf.value_and_gradient(x)
     assert c3 == c1 and np.array_equal(g3, g1)
+
+
+def test_fused_rbf_fp32_context():
+    """An fp32 context (BASELINE configs 3/5 run f32): the native iteration
+    uploads the rows through the f32 conversion and matches the composed host
+    path on the same context (same f32 pass, f64 chain rule)."""
+    import os
+    from conftest import GOLDEN
+    from flash import Models
+    from flash.gradientdescent import CostFunctor
+    z = np.load(os.path.join(GOLDEN, "c5_scene.npz"))
+    m = Models.irb_and_squishable()[0]
+    cf = CostFunctor(m, z["points"], precision=32)
+    assert cf._native
+    x = np.asarray(z["x"], np.float64)
+    c1, g1 = cf.value_and_gradient(x)
+    cf._native = False
+    c0, g0 = cf.value_and_gradient(x)
+    cf._native = True
+    assert c1 == pytest.approx(c0, rel=1e-6)
+    assert np.allclose(g1, g0, rtol=1e-5, atol=1e-5 * np.abs(g0).max())
+    # and close to the f64 golden gradient (f32 pass)
+    assert np.allclose(g1, z["dcdx"], rtol=2e-2, atol=2e-2 * np.abs(z["dcdx"]).max())

@@ -177,7 +177,8 @@ int fsdf_value_and_gradient(fsdf_ctx* ctx, const double* x, double* cost_out, do
  * xyz, deformation row or -1; value 0) then n_sk skeleton points (value -1),
  * n_sp + n_sk = its n_centers (src/Flash.jl:143-213) — and
  * fsdf_set_deformations gives the deformation count (x = [q; δ], 3 per
- * deformable point, src/gradientdescent.jl:9-17) and the regularizer weight
+ * deformable point, src/gradientdescent.jl:9-17; declare the centres after
+ * fsdf_set_mechanism, which clears them) and the regularizer weight
  * (default_deformation_cost_weight = 10, :7). value_and_gradient then also
  * places the centres (c = R_b (p + δ) + t_b), solves the weights, uploads the
  * rows, and chains the pass's RBF block through the solve: cost_out = Σ d*^2 +

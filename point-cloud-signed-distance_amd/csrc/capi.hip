@@ -1042,6 +1042,8 @@ extern "C" int fsdf_set_mechanism(fsdf_ctx* c, int32_t nb, const int32_t* parent
   M.tb.resize(3 * nb);
   M.poses.resize(12 * S);
   M.work.resize(6 * nb);
+  M.rbf.clear();  // centre declarations name bodies of the previous tree
+  M.x_prepared.clear();
   return FSDF_OK;
 }
 

@@ -172,14 +172,13 @@ int fsdf_set_mechanism(fsdf_ctx* ctx, int32_t nb, const int32_t* parent, const i
                        const double* axis, const double* AR, const double* At, const double* BR, const double* Bt,
                        int32_t nq, const int32_t* surface_body, const double* frame_R, const double* frame_t);
 int fsdf_value_and_gradient(fsdf_ctx* ctx, const double* x, double* cost_out, double* grad_out);
-/* RBF scenes in fsdf_value_and_gradient (after fsdf_set_mechanism): every RBF
- * surface's centres are declared once — n_sp surface points (body, body-frame
- * xyz, deformation row or -1; value 0) then n_sk skeleton points (value -1),
- * n_sp + n_sk = its n_centers (src/Flash.jl:143-213) — and
- * fsdf_set_deformations gives the deformation count (x = [q; δ], 3 per
- * deformable point, src/gradientdescent.jl:9-17; declare the centres after
- * fsdf_set_mechanism, which clears them) and the regularizer weight
- * (default_deformation_cost_weight = 10, :7). value_and_gradient then also
+/* RBF scenes in fsdf_value_and_gradient: after fsdf_set_mechanism (which
+ * clears earlier declarations) every RBF surface's centres are declared once —
+ * n_sp surface points (body, body-frame xyz, deformation row or -1; value 0)
+ * then n_sk skeleton points (value -1), n_sp + n_sk = its n_centers
+ * (src/Flash.jl:143-213) — and fsdf_set_deformations gives the deformation
+ * count (x = [q; δ], 3 per deformable point, src/gradientdescent.jl:9-17) and
+ * the regularizer weight (default_deformation_cost_weight = 10, :7). value_and_gradient then also
  * places the centres (c = R_b (p + δ) + t_b), solves the weights, uploads the
  * rows, and chains the pass's RBF block through the solve: cost_out = Σ d*^2 +
  * weight Σ|δ|^2, grad_out [nq + 3 n_deform] (CostFunctor(x) with its gradient,

@@ -96,6 +96,10 @@ struct fsdf_ctx {
   hipEvent_t pose_ev[kPoseRing] = {};
   int pose_slot = 0;
   double* d_poses = nullptr;
+  // pinned read-back of the accumulator (fetch): a pageable destination makes
+  // the D2H copy go through the runtime's staging buffer
+  double* h_acc = nullptr;
+  int h_acc_cap = 0;
   // resident cloud (precision-typed AoS)
   int64_t n = 0;
   void* d_pts = nullptr;
@@ -293,6 +297,7 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
     if (c->rbf_ev[i]) (void)hipEventDestroy(c->rbf_ev[i]);
     if (c->h_poses[i]) (void)hipHostFree(c->h_poses[i]);
   }
+  if (c->h_acc) (void)hipHostFree(c->h_acc);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   if (c->pose_stream) (void)hipStreamDestroy(c->pose_stream);
   if (c->ev_pose) (void)hipEventDestroy(c->ev_pose);
@@ -969,11 +974,31 @@ static int ensure_outputs(fsdf_ctx* c, int64_t n) {
   return FSDF_OK;
 }
 
+// fsdf_value_and_gradient: the reduction kernel stores the accumulator into
+// the pinned host buffer itself (no D2H copy command before the sync). Same
+// results; full iteration -1.5 to -2.5 us against the pinned copy
+// (profiles/r02/experiments/r02zc).
+#ifndef FSDF_ZERO_COPY_ACCUM
+#define FSDF_ZERO_COPY_ACCUM 1
+#endif
+
+static int ensure_host_acc(fsdf_ctx* c, int len) {
+  if (len <= c->h_acc_cap) return FSDF_OK;
+  if (c->h_acc) HIPCHECK(c, hipHostFree(c->h_acc));
+  c->h_acc = nullptr;
+  c->h_acc_cap = 0;
+  HIPCHECK(c, hipHostMalloc((void**)&c->h_acc, (size_t)len * sizeof(double), hipHostMallocDefault));
+  c->h_acc_cap = len;
+  return FSDF_OK;
+}
+
 static int fetch(fsdf_ctx* c, int64_t n, double* cost_out, double* accum_out, int32_t* kstar_out, double* d_out,
                  double* grad_out, bool want_pp) {
   const int len = accum_len(c);
-  std::vector<double> acc(len);
-  HIPCHECK(c, hipMemcpyAsync(acc.data(), c->d_accum, len * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  int rc = ensure_host_acc(c, len);
+  if (rc) return rc;
+  double* acc = c->h_acc;
+  HIPCHECK(c, hipMemcpyAsync(acc, c->d_accum, len * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   if (want_pp && n > 0) {
     if (kstar_out)
       HIPCHECK(c, hipMemcpyAsync(kstar_out, c->d_kstar, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -983,7 +1008,7 @@ static int fetch(fsdf_ctx* c, int64_t n, double* cost_out, double* accum_out, in
   }
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   if (cost_out) *cost_out = acc[0];
-  if (accum_out) memcpy(accum_out, acc.data(), len * sizeof(double));
+  if (accum_out) memcpy(accum_out, acc, len * sizeof(double));
   return FSDF_OK;
 }
 
@@ -1228,12 +1253,24 @@ extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cos
   int rc = iteration_prepare(c, x, "value_and_gradient");
   if (rc) return rc;
   auto& M = c->mech;
+#if FSDF_ZERO_COPY_ACCUM
+  // the reduction stores the accumulator straight into pinned host memory
+  rc = ensure_host_acc(c, accum_len(c));
+  if (rc) return rc;
+  double* d_acc_host = nullptr;
+  HIPCHECK(c, hipHostGetDevicePointer((void**)&d_acc_host, c->h_acc, 0));
+  rc = run_pass(c, M.poses.data(), c->d_pts, c->n, d_acc_host, nullptr, nullptr, nullptr, nullptr, true);
+  if (rc) return rc;
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  return iteration_finish(c, x, c->h_acc, cost_out, grad_out, "value_and_gradient");
+#else
   rc = run_pass(c, M.poses.data(), c->d_pts, c->n, c->d_accum, nullptr, nullptr, nullptr, nullptr, true);
   if (rc) return rc;
   M.accum.resize(accum_len(c));
   rc = fetch(c, c->n, nullptr, M.accum.data(), nullptr, nullptr, nullptr, false);
   if (rc) return rc;
   return iteration_finish(c, x, M.accum.data(), cost_out, grad_out, "value_and_gradient");
+#endif
 }
 
 extern "C" int fsdf_eval_state_device(fsdf_ctx* c, const double* x, double* d_accum) {

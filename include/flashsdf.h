@@ -197,6 +197,17 @@ int fsdf_set_deformations(fsdf_ctx* ctx, int32_t n_deform, double weight);
 int fsdf_eval_state_device(fsdf_ctx* ctx, const double* x, double* d_accum);
 int fsdf_state_gradient(fsdf_ctx* ctx, const double* x, const double* accum, double* cost_out, double* grad_out);
 
+/* estimate_state's solver loop (src/tracking.jl:16-26: wrapped_cost c/N, warm
+ * start x) around fsdf_value_and_gradient, with no host-language round trip per
+ * iteration. Up to iteration_limit times: f = cost/n_points, g = (grad/n_points)
+ * ./ divisors (NULL = ones); stop when |g|_2 < tolerance; else x += clamp(-rate g,
+ * ±max_step) component-wise (NaiveSolver's rule as restated in
+ * flash/tracking.py; the solver itself is the un-vendored
+ * SimpleGradientDescent.jl). x [nq + 3 n_deform] is updated in place;
+ * value_out = f of the last evaluation, iterations_out = evaluations made. */
+int fsdf_descend(fsdf_ctx* ctx, double* x, int32_t iteration_limit, double rate, double max_step, double tolerance,
+                 const double* divisors, double n_points, double* value_out, int32_t* iterations_out);
+
 /* ---- context ---------------------------------------------------------------- */
 int fsdf_create(fsdf_ctx** out, const fsdf_opts* opts);
 int fsdf_destroy(fsdf_ctx* ctx);

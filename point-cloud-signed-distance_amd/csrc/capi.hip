@@ -1273,6 +1273,43 @@ extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cos
 #endif
 }
 
+// The solver loop of estimate_state (src/tracking.jl:16-26 with the
+// NaiveSolver restated in flash/tracking.py) around fsdf_value_and_gradient,
+// without a host-language round trip per iteration: f = c/n, g = (∂c/∂x / n)
+// ./ divisors; stop when |g| < tolerance; else x += clamp(-rate g, ±max_step).
+extern "C" int fsdf_descend(fsdf_ctx* c, double* x, int32_t iteration_limit, double rate, double max_step,
+                            double tolerance, const double* divisors, double n_points, double* value_out,
+                            int32_t* iterations_out) {
+  if (!c) return FSDF_ERR_ARG;
+  if (iterations_out) *iterations_out = 0;
+  if (!x || iteration_limit < 0 || !(n_points > 0.0) || !std::isfinite(rate) || !(max_step >= 0.0))
+    return fail(c, FSDF_ERR_ARG, "descend: bad arguments");
+  if (c->mech.nb == 0) return fail(c, FSDF_ERR_STATE, "descend: no mechanism (call fsdf_set_mechanism)");
+  const int ns = c->mech.nq + 3 * c->mech.n_deform;
+  std::vector<double> g(ns);
+  double f = 0.0;
+  int it = 0;
+  while (it < iteration_limit) {
+    double cost = 0.0;
+    const int rc = fsdf_value_and_gradient(c, x, &cost, g.data());
+    if (rc) return rc;
+    ++it;
+    if (iterations_out) *iterations_out = it;
+    f = cost / n_points;
+    double nrm2 = 0.0;
+    for (int i = 0; i < ns; ++i) {
+      double gi = g[i] / n_points;
+      if (divisors) gi = gi / divisors[i];
+      g[i] = gi;
+      nrm2 += gi * gi;
+    }
+    if (std::sqrt(nrm2) < tolerance) break;
+    for (int i = 0; i < ns; ++i) x[i] = x[i] + std::min(std::max(-rate * g[i], -max_step), max_step);
+  }
+  if (value_out) *value_out = f;
+  return FSDF_OK;
+}
+
 extern "C" int fsdf_eval_state_device(fsdf_ctx* c, const double* x, double* d_accum) {
   if (!c) return FSDF_ERR_ARG;
   if (!x || !d_accum) return fail(c, FSDF_ERR_ARG, "eval_state_device: null argument");

@@ -84,6 +84,8 @@ _PROTOS = {
     "fsdf_set_deformations": (c_int32, [c_void_p, c_int32, c_double]),
     "fsdf_eval_state_device": (c_int32, [c_void_p, c_void_p, c_void_p]),
     "fsdf_state_gradient": (c_int32, [c_void_p] + [c_void_p] * 2 + [POINTER(c_double), c_void_p]),
+    "fsdf_descend": (c_int32, [c_void_p, c_void_p, c_int32, c_double, c_double, c_double, c_void_p, c_double,
+                               POINTER(c_double), POINTER(c_int32)]),
 }
 SYMBOLS = tuple(_PROTOS)
 
@@ -339,6 +341,22 @@ class Context:
         check(self._lib.fsdf_value_and_gradient(self._ctx, ptr(x), ctypes.byref(c), ptr(g)), self._ctx,
               "value_and_gradient")
         return c.value, g
+
+    def descend(self, x, iteration_limit, rate, max_step, tolerance=0.0, divisors=None, n_points=1.0):
+        """fsdf_descend: the NaiveSolver loop over value_and_gradient natively.
+        Returns (x, f of the last evaluation, evaluations made)."""
+        x = np.array(x, np.float64, copy=True)
+        if x.size != self.nq + 3 * getattr(self, "n_deform", 0):
+            raise ValueError("descend: x must have nq + 3 n_deform entries")
+        div = None if divisors is None else np.ascontiguousarray(divisors, np.float64)
+        if div is not None and div.shape != x.shape:
+            raise ValueError("descend: divisors must match x")
+        f = c_double(0.0)
+        it = c_int32(0)
+        check(self._lib.fsdf_descend(self._ctx, ptr(x), int(iteration_limit), float(rate), float(max_step),
+                                     float(tolerance), ptr(div) if div is not None else None, float(n_points),
+                                     ctypes.byref(f), ctypes.byref(it)), self._ctx, "descend")
+        return x, f.value, it.value
 
     def eval_state_device(self, x, d_accum: int):
         """FK, RBF solve, poses and the pass at x into the device accumulator

@@ -166,6 +166,16 @@ class CostFunctor:
         c, accum, _ = self._pass(x)
         return c, gradient_from_accum(self.manipulator, x, accum, self._solves, self.weight)
 
+    def descend(self, x, iteration_limit, rate, max_step, tolerance=0.0, divisors=None, n_points=1.0):
+        """The NaiveSolver loop over value_and_gradient in one native call
+        (fsdf_descend); native-capable scenes only. Returns (x, f, iterations)."""
+        if not self._native:
+            raise NotImplementedError("descend: scene is not native-capable")
+        self._ensure_resident()
+        if getattr(self.ctx, "_mechanism_of", None) != (self.manipulator, self.weight):
+            self._register_native()
+        return self.ctx.descend(x, iteration_limit, rate, max_step, tolerance, divisors, n_points)
+
     def per_point(self, x):
         """(d*, k*, ∇d*) for every sensed point at configuration x."""
         return self._pass(x, per_point=True)[2]

@@ -69,8 +69,16 @@ def _default_solver(manipulator):
 
 
 def _optimize(cost: CostFunctor, n_points: int, x_estimated, callback, solver):
-    """wrapped_cost (src/tracking.jl:16-21) over a CostFunctor, then optimize!."""
+    """wrapped_cost (src/tracking.jl:16-21) over a CostFunctor, then optimize!.
+    Without a callback, a NaiveSolver runs natively (fsdf_descend: the same
+    arithmetic, no Python round trip per iteration)."""
     n = max(n_points, 1)
+    if callback is None and type(solver) is NaiveSolver and cost._native:
+        x, _, its = cost.descend(np.asarray(x_estimated, np.float64), solver.iteration_limit, solver.rate,
+                                 solver.max_step, solver.gradient_convergence_tolerance,
+                                 solver.precondition_divisors, n)
+        solver.iterations = its
+        return x
 
     def wrapped(x):
         c, g = cost.value_and_gradient(x)

@@ -103,3 +103,47 @@ def test_track_lcm_log(tmp_path):
                                                                             iteration_limit=5))
     xs_b = run([c.astype(np.float32)[::200].astype(np.float64) for c in clouds])
     assert np.array_equal(xs_a, xs_b)
+
+
+@pytest.mark.parametrize("scene", ["irb140", "irb_and_squishable"])
+def test_native_descend_matches_python_loop(scene):
+    """fsdf_descend (the NaiveSolver loop inside the library) against the
+    Python loop over value_and_gradient (taken whenever a callback is given):
+    the same x trajectory bit for bit, with preconditioning divisors, and the
+    same stopping iteration under a convergence tolerance."""
+    import flash
+    from flash import Models, synthetic
+    from flash.gradientdescent import CostFunctor, flatten
+    from flash.tracking import NaiveSolver, _optimize
+    if scene == "irb140":
+        m = Models.irb140()
+        q_true, _ = synthetic.perturbed_configuration(m, 31)
+        pts = synthetic.depth_cloud(m, q_true, 6000, seed=32, frac_box=0.0, frac_surface=1.0, sigma=0.001)
+        st = flash.ManipulatorState(m)
+        st.q[:] = q_true + 0.03
+        x0 = flatten(st)
+    else:  # 7 hulls + the squishable RBF skin (deformations) + table, 63 states
+        m, x0 = Models.irb_and_squishable()
+        nq = m.mechanism.num_positions
+        x0 = np.array(x0, np.float64)
+        rng = np.random.default_rng(33)
+        x0[nq:] = 0.004 * rng.normal(size=len(x0) - nq)
+        pts = np.array([-0.1, -0.3, 0.55]) + rng.random((6000, 3)) * np.array([1.0, 1.0, 0.8])
+    n = flash.num_states(m)
+    cf = CostFunctor(m, pts)
+    assert cf._native
+    div = np.linspace(1.0, 2.0, n)
+    for tol, limit in ((0.0, 6), (1e-3, 40)):
+        sa = NaiveSolver(n, rate=5.0, max_step=0.05, iteration_limit=limit, gradient_convergence_tolerance=tol,
+                         precondition_divisors=div)
+        sb = NaiveSolver(n, rate=5.0, max_step=0.05, iteration_limit=limit, gradient_convergence_tolerance=tol,
+                         precondition_divisors=div)
+        seen = []
+        xa = _optimize(cf, len(pts), x0, lambda x, c: seen.append(c), sa)  # Python loop
+        xb = _optimize(cf, len(pts), x0, None, sb)                          # fsdf_descend
+        assert np.array_equal(xa, xb), np.abs(xa - xb).max()
+        assert sa.iterations == sb.iterations == len(seen)
+        if tol == 0.0:
+            assert sb.iterations == limit
+    with pytest.raises(ValueError):
+        cf.descend(x0[:-1], 2, 1.0, 0.1)

@@ -160,7 +160,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl")
+        # FSDF_BENCH_BACKEND / FSDF_BENCH_DEVICE: rehearsal of the N>1 path on a
+        # one-GPU box (gloo, every rank on one device); RCCL ("nccl") otherwise
+        dist.init_process_group(os.environ.get("FSDF_BENCH_BACKEND", "nccl"))
+        local = int(os.environ.get("FSDF_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

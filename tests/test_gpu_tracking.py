@@ -147,3 +147,9 @@ def test_native_descend_matches_python_loop(scene):
             assert sb.iterations == limit
     with pytest.raises(ValueError):
         cf.descend(x0[:-1], 2, 1.0, 0.1)
+    x_same, f0, its = cf.descend(x0, 0, 1.0, 0.1)  # iteration_limit 0: x untouched
+    assert its == 0 and np.array_equal(x_same, x0)
+    x1, f1, its = cf.descend(x0, 1, 5.0, 0.05, n_points=len(pts))
+    c, g = cf.value_and_gradient(x0)
+    assert its == 1 and f1 == c / len(pts)
+    assert np.array_equal(x1, x0 + np.clip(-5.0 * (g / len(pts)), -0.05, 0.05))

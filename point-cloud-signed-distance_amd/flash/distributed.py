@@ -56,6 +56,10 @@ class ShardedCostFunctor:
         pts = torch.as_tensor(np.ascontiguousarray(local_points, np.float64).reshape(-1, 3), device=self.dev)
         self.ctx.set_points_device(pts.data_ptr(), pts.shape[0])
         self.accum = torch.zeros(self.ctx.accum_len, dtype=torch.float64, device=self.dev)
+        # pinned read-back of the all-reduced accumulator (a pageable .cpu()
+        # goes through the runtime's staging buffer: ~10 us per iteration on
+        # the single-GPU path, profiles/r02/experiments/r02pin)
+        self.h_accum = torch.empty(self.ctx.accum_len, dtype=torch.float64, pin_memory=True)
         self.stream = torch.cuda.current_stream(self.dev)
         self.ctx.set_stream(self.stream.cuda_stream)
         # native iterations (fsdf_eval_state_device + fsdf_state_gradient: FK,
@@ -96,7 +100,9 @@ class ShardedCostFunctor:
 
     def value_and_gradient(self, x):
         x = np.asarray(x, np.float64)
-        acc = self.launch(x).cpu().numpy()
+        self.h_accum.copy_(self.launch(x), non_blocking=True)
+        self.torch.cuda.current_stream(self.dev).synchronize()  # the stream the copy is ordered on
+        acc = self.h_accum.numpy()
         if self._native:
             return self.ctx.state_gradient(x, acc)
         c = float(acc[0]) + _regularizer(self.state, self.weight)

@@ -202,8 +202,11 @@ int fsdf_state_gradient(fsdf_ctx* ctx, const double* x, const double* accum, dou
  * iteration. Up to iteration_limit times: f = cost/n_points, g = (grad/n_points)
  * ./ divisors (NULL = ones); stop when |g|_2 < tolerance; else x += clamp(-rate g,
  * ±max_step) component-wise (NaiveSolver's rule as restated in
- * flash/tracking.py; the solver itself is the un-vendored
- * SimpleGradientDescent.jl). x [nq + 3 n_deform] is updated in place;
+ * flash/tracking.py — the solver itself is the un-vendored
+ * SimpleGradientDescent.jl; the rule is pinned by examples/manipulator.ipynb's
+ * own per-trial traces, tests/test_manipulator_traces.py). n_points = 1
+ * reproduces the notebook's session, whose objective was the undivided c.
+ * x [nq + 3 n_deform] is updated in place;
  * value_out = f of the last evaluation, iterations_out = evaluations made. */
 int fsdf_descend(fsdf_ctx* ctx, double* x, int32_t iteration_limit, double rate, double max_step, double tolerance,
                  const double* divisors, double n_points, double* value_out, int32_t* iterations_out);

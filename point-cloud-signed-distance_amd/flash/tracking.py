@@ -15,12 +15,19 @@ that loop; `Tracker` is its resident form (one device context and CostFunctor
 for the whole sequence, the cloud swapped per frame).
 
 The solver lives in the un-vendored SimpleGradientDescent.jl @0fcc1f95
-(REQUIRE.dev:24). `NaiveSolver` below restates its published interface
-(num_vars, rate, max_step, iteration_limit, gradient_convergence_tolerance,
+(REQUIRE.dev:24). `NaiveSolver` below restates its interface (num_vars, rate,
+max_step, iteration_limit, gradient_convergence_tolerance,
 precondition_divisors — the kwargs examples/irb140.ipynb cell 9 and
-examples/squishable.ipynb cell 9 pass) with a plain preconditioned, clipped
-gradient step; trajectory parity with the Julia solver is UNPINNED (no
-reference test or output covers it).
+examples/squishable.ipynb cell 9 pass). Its update rule is pinned by the
+reference notebook's own per-trial traces (examples/manipulator.ipynb cells
+9/10/14, fixture tests/golden/manipulator_traces.json,
+tests/test_manipulator_traces.py): the step is −rate·∇f (κ = rate measured
+within 2 % from single trajectories at two rates), clipped component-wise at
+max_step (the far set's largest |Δerr| per step is max_step·√2), one
+objective evaluation per iteration, and a positive default convergence
+tolerance (trials stop early; 1e-3 estimated from where they stop). Trajectory
+parity on the RBF scene itself is not reached: the landscape diverges
+(DESIGN.md §2).
 """
 from __future__ import annotations
 
@@ -38,19 +45,20 @@ class NaiveSolver:
     """NaiveSolver(num_vars; rate, max_step, iteration_limit,
     gradient_convergence_tolerance, precondition_divisors): per iteration
     g ← ∇f(x) ./ precondition_divisors; stop when ‖g‖ < tolerance; else
-    x ← x − clamp(rate·g, ±max_step) (component-wise)."""
+    x ← x + clamp(−rate·g, ±max_step) (component-wise). Rule and default
+    tolerance per the notebook traces (module docstring)."""
     num_vars: int
     rate: float = 0.1
     max_step: float = 0.5
     iteration_limit: int = 30
-    gradient_convergence_tolerance: float = 0.0
+    gradient_convergence_tolerance: float = 1e-3
     precondition_divisors: np.ndarray | None = None
     iterations: int = field(default=0, init=False)  # of the last optimize
 
     def optimize(self, value_and_gradient, x0):
         x = np.array(x0, np.float64, copy=True)
-        div = np.ones(self.num_vars) if self.precondition_divisors is None else np.asarray(self.precondition_divisors,
-                                                                                            np.float64)
+        div = np.ones(self.num_vars) if self.precondition_divisors is None else np.broadcast_to(
+            np.asarray(self.precondition_divisors, np.float64), x.shape)
         f = None
         self.iterations = 0
         for _ in range(self.iteration_limit):
@@ -74,9 +82,12 @@ def _optimize(cost: CostFunctor, n_points: int, x_estimated, callback, solver):
     arithmetic, no Python round trip per iteration)."""
     n = max(n_points, 1)
     if callback is None and type(solver) is NaiveSolver and cost._native:
-        x, _, its = cost.descend(np.asarray(x_estimated, np.float64), solver.iteration_limit, solver.rate,
-                                 solver.max_step, solver.gradient_convergence_tolerance,
-                                 solver.precondition_divisors, n)
+        x0 = np.asarray(x_estimated, np.float64)
+        div = solver.precondition_divisors
+        if div is not None:  # NaiveSolver broadcasts the divisors; fsdf_descend takes one per entry
+            div = np.broadcast_to(np.asarray(div, np.float64), x0.shape).copy()
+        x, _, its = cost.descend(x0, solver.iteration_limit, solver.rate, solver.max_step,
+                                 solver.gradient_convergence_tolerance, div, n)
         solver.iterations = its
         return x
 

@@ -12,12 +12,17 @@ the fixed-order reduce kernel and, for N > 1, the RCCL all-reduce of the
 1+6S-double accumulator.
 
 Sharding (contiguous ⌈N/W⌉ point ranges, uploaded once per frame):
-  --points P          weak scaling: every rank owns its own P-point cloud (the
-                      default: P = 2^20, the metric's 1M cloud on every GPU)
-  --global-points G   strong scaling: ONE G-point cloud (the same seed on every
-                      rank) split into W contiguous shards
+  (default)           strong scaling of the metric's cloud: ONE 2^20-point M64
+                      cloud (the same seed on every rank) split into W
+                      contiguous shards — `value`; for W > 1 the weak figure
+                      (2^20 points per GPU) is measured in the same run and
+                      reported beside it (`weak`)
+  --points P          weak scaling only: every rank owns its own P-point cloud
+  --global-points G   strong scaling only, of a G-point cloud
   --config c4         BASELINE config 4: IRB140, 10·2^20 points, strong scaling
-The metric's single-GPU workload is M64 with 2^20 points either way.
+For W > 1 the per-pass all-reduce is also timed on its own (`allreduce_ms`:
+host-synchronised all-reduces of the accumulator, mean over `steps`), and the
+backend that ran is named (`config.backend`).
 
 Rank 0 prints one JSON line (contract in the task description) with:
   roofline      the pass kernel on the HBM roofline: algorithmic bytes per launch
@@ -56,10 +61,10 @@ ITERS_PER_FRAME = 30           # src/tracking.jl:10-13 default NaiveSolver itera
 
 CONFIGS = {
     # name: (model, default points, scaling, description)
-    "m64": ("arm_grid", 1 << 20, "weak",
+    "m64": ("arm_grid", 1 << 20, "strong",
             "M64: 8 IRB140 arms (7 link hulls + ATI hull each) on a 2x4 grid, 64 convex hulls, 48 DOF; seeded "
             "synthetic depth cloud (SURVEY.md §8d generator G)"),
-    "c2": ("irb140", 1 << 20, "weak", "C2: IRB140 rigid model (7 hulls, 6 DOF), 2^20 synthetic points"),
+    "c2": ("irb140", 1 << 20, "strong", "C2: IRB140 rigid model (7 hulls, 6 DOF), 2^20 synthetic points"),
     "c4": ("irb140", 10 << 20, "strong", "C4: IRB140 rigid model, ONE 10*2^20-point cloud sharded over the GPUs"),
 }
 
@@ -82,9 +87,6 @@ def parse():
     p.add_argument("--caller-order", action="store_true",
                    help="per-point outputs scattered to the caller's order (default: resident order, coalesced; "
                         "the permutation is fsdf_get_permutation)")
-    p.add_argument("--split-budget", type=int, default=None,
-                   help="hull evaluations per wave before the pass splits it (fsdf_set_split_budget; 0 = never; "
-                        "default: the library's)")
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of each CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-full-iteration", action="store_true")
@@ -166,6 +168,7 @@ def main():
         local = int(os.environ.get("FSDF_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    backend = dist.get_backend() if world > 1 else None
 
     import flash
     from flash import Models, synthetic
@@ -176,81 +179,114 @@ def main():
         scaling = "strong"
     elif args.points is not None:
         scaling = "weak"
+    # W > 1 with the default workload: the weak figure is measured beside
+    also_weak = world > 1 and args.points is None and args.global_points is None and scaling == "strong"
     manip = getattr(Models, model_name)()
     q_true, q_eval = synthetic.perturbed_configuration(manip, args.seed)
-    if scaling == "strong":
-        g = args.global_points if args.global_points is not None else default_points
+
+    def strong_shard(g):
         cloud = synthetic.depth_cloud(manip, q_true, g, seed=args.seed + 17, order=args.order)
         a, b = shard_range(g, rank, world)
-        pts = np.ascontiguousarray(cloud[a:b])
-        del cloud
-        global_points = g
+        return np.ascontiguousarray(cloud[a:b])
+
+    def weak_cloud(p):
+        return synthetic.depth_cloud(manip, q_true, p, seed=args.seed + 17 * (rank + 1), order=args.order)
+
+    if scaling == "strong":
+        global_points = args.global_points if args.global_points is not None else default_points
+        pts = strong_shard(global_points)
     else:
         p = args.points if args.points is not None else default_points
-        pts = synthetic.depth_cloud(manip, q_true, p, seed=args.seed + 17 * (rank + 1), order=args.order)
+        pts = weak_cloud(p)
         global_points = p * world
     q_alt = q_eval + 1e-3  # alternate between two configurations step to step
     poses = [flash.hull_poses(manip, q_eval), flash.hull_poses(manip, q_alt)]
 
     ctx = manip.engine(device=local, precision=args.precision, cull=not args.no_cull, sort_points=not args.no_sort)
     ctx.set_output_order(not args.caller_order)
-    if args.split_budget is not None:
-        ctx.set_split_budget(args.split_budget)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
-    d_pts = torch.as_tensor(pts, device=dev)
-    torch.cuda.synchronize()
-    ctx.set_points_device(d_pts.data_ptr(), len(pts))  # first upload (allocations)
-    set_ms = []
-    for _ in range(3):  # once per frame: copy (+ Hilbert sort)
-        t_set = time.perf_counter()
-        ctx.set_points_device(d_pts.data_ptr(), len(pts))
-        set_ms.append((time.perf_counter() - t_set) * 1e3)
-    set_points_ms = float(np.median(set_ms))
-    del d_pts
-    n = len(pts)
     accum = torch.zeros(ctx.accum_len, dtype=torch.float64, device=dev)
-    if args.no_per_point:
-        outs = (0, 0, 0)
-    else:
-        kstar = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-        dd = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
-        gg = torch.empty((max(n, 1), 3), dtype=torch.float64, device=dev)
-        outs = (kstar.data_ptr(), dd.data_ptr(), gg.data_ptr())
 
-    def step(i):
-        ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs)
-        allreduce_accum(accum)
+    def run_cloud(pts_host):
+        """Upload the cloud (timed per frame), then W untimed + K timed steps
+        bracketed by barrier + synchronize; returns the max-over-ranks
+        (elapsed s, whole-pass ms, pass-kernel ms, set_points ms)."""
+        d_pts = torch.as_tensor(pts_host, device=dev)
+        torch.cuda.synchronize()
+        ctx.set_points_device(d_pts.data_ptr(), len(pts_host))  # first upload (allocations)
+        set_ms = []
+        for _ in range(3):  # once per frame: copy (+ Hilbert sort)
+            t_set = time.perf_counter()
+            ctx.set_points_device(d_pts.data_ptr(), len(pts_host))
+            set_ms.append((time.perf_counter() - t_set) * 1e3)
+        del d_pts
+        n_ = len(pts_host)
+        if args.no_per_point:
+            outs = (0, 0, 0)
+        else:
+            bufs = (torch.empty(max(n_, 1), dtype=torch.int32, device=dev),
+                    torch.empty(max(n_, 1), dtype=torch.float64, device=dev),
+                    torch.empty((max(n_, 1), 3), dtype=torch.float64, device=dev))
+            outs = tuple(b_.data_ptr() for b_ in bufs)
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    ctx.profile_pass(True)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for i in range(args.steps):
-        step(i)
-    ev1.record(stream)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    kernel_ms, pass_ms, launches = ctx.pass_times()
-    ctx.profile_pass(False)
-    elapsed = max(wall, ev0.elapsed_time(ev1) / 1e3)
-    t = torch.tensor([elapsed, pass_ms / max(launches, 1), set_points_ms, kernel_ms / max(launches, 1)],
-                     dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, pass_avg_ms, set_points_ms, kernel_avg_ms = float(t[0]), float(t[1]), float(t[2]), float(t[3])
+        def step(i):
+            ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs)
+            allreduce_accum(accum)
 
-    # sanity: the last pass is finite and non-trivial
-    acc = accum.cpu().numpy()
-    assert np.isfinite(acc).all() and acc[0] > 0
+        for i in range(args.warmup):
+            step(i)
+        torch.cuda.synchronize()
+        ctx.profile_pass(True)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for i in range(args.steps):
+            step(i)
+        ev1.record(stream)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        kernel_ms, pass_ms, launches = ctx.pass_times()
+        ctx.profile_pass(False)
+        elapsed_ = max(wall, ev0.elapsed_time(ev1) / 1e3)
+        t = torch.tensor([elapsed_, pass_ms / max(launches, 1), kernel_ms / max(launches, 1),
+                          float(np.median(set_ms))], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        # sanity: the last pass is finite and non-trivial
+        acc = accum.cpu().numpy()
+        assert np.isfinite(acc).all() and acc[0] > 0
+        return float(t[0]), float(t[1]), float(t[2]), float(t[3])
+
+    n = len(pts)
+    elapsed, pass_avg_ms, kernel_avg_ms, set_points_ms = run_cloud(pts)
+
+    allreduce_ms = None
+    if world > 1:
+        # the all-reduce alone, host-synchronised per call (latency-bound: ~3 KB)
+        for _ in range(3):
+            allreduce_accum(accum)
+        torch.cuda.synchronize()
+        t_ar = time.perf_counter()
+        for _ in range(args.steps):
+            allreduce_accum(accum)
+            torch.cuda.synchronize()
+        allreduce_ms = (time.perf_counter() - t_ar) / args.steps * 1e3
+
+    weak = None
+    if also_weak:
+        del pts
+        pts_w = weak_cloud(default_points)
+        w_elapsed, w_pass, w_kernel, _ = run_cloud(pts_w)
+        weak = {"value": default_points * world * args.steps / w_elapsed, "points_per_gpu": default_points,
+                "global_points": default_points * world, "ms_per_step": w_elapsed / args.steps * 1e3,
+                "pass_ms": w_pass, "pass_kernel_ms": w_kernel,
+                "note": "weak scaling beside the strong value: every rank its own 2^20-point cloud"}
 
     iter_ms = None
     if rank == 0 and world == 1 and not args.no_full_iteration:
@@ -264,14 +300,16 @@ def main():
         tsz = 8 if args.precision == 64 else 4
         bytes_in = 3 * tsz * n
         bytes_per_launch = bytes_in + (0 if args.no_per_point else 36 * n)
-        hbm_achieved = bytes_per_launch / (pass_avg_ms / 1e3) / 1e9
+        # per launch of the pass kernel, its own HIP events on the stream it runs on
+        hbm_achieved = bytes_per_launch / (kernel_avg_ms / 1e3) / 1e9
         # F_alg per point-eval = Σ_hulls (21 + 7 F_k) + 15 (brute-force plane tests)
         f_alg = sum(21 + 7 * len(s.hull.faces) for s in manip.surfaces) + 15
-        eff_tflops = f_alg * n / (pass_avg_ms / 1e3) / 1e12
+        eff_tflops = f_alg * n / (kernel_avg_ms / 1e3) / 1e12
         peak_valu = FP64_VALU_PEAK_TFLOPS if args.precision == 64 else FP32_VALU_PEAK_TFLOPS
         traffic, traffic_src, executed, issue = None, None, None, None
         pmc = os.path.join(ROOT, "profiles", "latest_pmc.json")
-        default_run = (args.config == "m64" and scaling == "weak" and n == 1 << 20 and args.precision == 64
+        # the committed PMC profile is of the single-GPU default run only
+        default_run = (world == 1 and args.config == "m64" and n == 1 << 20 and args.precision == 64
                        and not args.no_cull and not args.no_sort and not args.no_per_point
                        and args.order == "shuffled" and not args.caller_order)
         if os.path.exists(pmc) and default_run:
@@ -282,7 +320,7 @@ def main():
                 executed = rec.get("executed")
                 if executed and executed.get("valu_insts_per_launch"):
                     issue = executed["valu_insts_per_launch"] * CYCLES_PER_WAVE_OP / (
-                        SIMDS * CLOCK_HZ * pass_avg_ms / 1e3)
+                        SIMDS * CLOCK_HZ * kernel_avg_ms / 1e3)
         frame_ms = set_points_ms + ITERS_PER_FRAME * ms_per_step
         out = {
             "metric": "SDF+grad point-evals/sec, 1M-pt cloud x 64-prim model (M64)",
@@ -304,9 +342,12 @@ def main():
                 "input_order": args.order, "sort_points": not args.no_sort,
                 "cull": not args.no_cull, "per_point_outputs": not args.no_per_point,
                 "output_order": "caller" if args.caller_order else "resident (+ permutation)",
-                "split_budget": args.split_budget if args.split_budget is not None else "library default (0: off)",
-                "parallelism": f"points sharded x{world} ({scaling} scaling), RCCL all-reduce of "
-                               f"{ctx.accum_len} f64 per pass",
+                "parallelism": (f"points sharded x{world} ({scaling} scaling), {backend} all-reduce of "
+                                f"{ctx.accum_len} f64 per pass" if world > 1 else
+                                f"one GPU ({scaling} figure of the metric's cloud); at W > 1 one "
+                                f"{ctx.accum_len}-f64 all-reduce per pass"),
+                "backend": backend,
+                "allreduce_ms": allreduce_ms,
                 "set_points_ms_per_frame": set_points_ms,
                 "frame_ms_at_30_iterations": frame_ms,
                 "frame_note": "set_points (H2D-resident copy + Hilbert sort) once + 30 residual passes",
@@ -318,8 +359,8 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": hbm_achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": "pass (pass_kernel + split overflow/merge kernels)", "kernel_ms": pass_avg_ms,
-                "pass_kernel_ms": kernel_avg_ms,
+                "kernel": "pass_kernel", "kernel_ms": kernel_avg_ms,
+                "whole_pass_ms": pass_avg_ms,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "valu_issue_frac": issue,
                 "valu_effective": {"flop_per_eval": f_alg, "achieved_tflops": eff_tflops, "peak_tflops": peak_valu,
@@ -329,6 +370,8 @@ def main():
                 "executed_pmc": executed,
             },
         }
+        if weak is not None:
+            out["weak"] = weak
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(manip, pts, q_eval, args.cpu_seconds)
         print(json.dumps(out), flush=True)

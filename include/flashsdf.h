@@ -287,27 +287,12 @@ int fsdf_get_permutation_device(fsdf_ctx* ctx, int64_t* d_perm_out);
 /* Block until all work queued on the context stream has finished. */
 int fsdf_synchronize(fsdf_ctx* ctx);
 
-/* ---- heavy-wave split (tuning; no effect on results) -------------------------
- * A wave of the pass kernel owns 64 resident points and evaluates, in
- * sequence, every hull some of them may be nearest to, each point's
- * best-first seed hull first; waves whose points lie among many hulls set the
- * pass time. With a budget B > 0, a wave whose points have more than B
- * distinct seed hulls is split into one item per seed group, which an
- * overflow kernel evaluates in parallel (one wave each); a merge kernel
- * gathers them back. d*, k* and the gradient are those of an unsplit pass
- * (a point's result does not depend on the other points of its wave); the
- * accumulator differs only in summation order. Applies to culled hull-only
- * scenes of <= 64 surfaces with one wave-iteration per wave
- * (n <= 16,384 x 256); 0 = never split. Default 0: on MI355X the split
- * kernels cost more than they save. */
-int fsdf_set_split_budget(fsdf_ctx* ctx, int32_t evals);
-
 /* ---- measurement ------------------------------------------------------------
  * With profiling enabled, every residual pass records HIP events on the
  * context stream before the pass kernel (the dominant launch), after it, and
- * after the split kernels (overflow + merge, when the pass splits).
- * fsdf_pass_times synchronizes, returns the summed pass-kernel time, the
- * summed whole-pass time (pass kernel through merge) of the passes recorded
+ * again after it (a whole-pass bracket kept for the pose/pass/reduce
+ * accounting). fsdf_pass_times synchronizes, returns the summed pass-kernel
+ * time, the summed whole-pass time of the passes recorded
  * since the last query and their count, and resets the record;
  * fsdf_pass_time returns the whole-pass sum only. */
 int fsdf_profile_pass(fsdf_ctx* ctx, int32_t enable);
@@ -321,14 +306,11 @@ int fsdf_pass_time(fsdf_ctx* ctx, double* total_ms_out, int64_t* launches_out);
  *   [4] lanes on the slow path            [5] best-first seed evaluations
  *   [6] waves reaching the exhaustive scan [7] lanes in the exhaustive scan
  *   [8] candidate hulls after wave culling [9] faces of the evaluated hulls
- *   [10..18] shader-clock cycles per phase (culling, hull staging, plane max,
- *   fast path, closest-feature search, whole wave-iteration, segmented
- *   reduction, per-point stores, scene evaluation) — only in diagnostic
- *   builds (-DFSDF_PHASE_TIMING=1), zero otherwise.
+ *   [10..18] reserved (0; the per-phase clocks live in the -DFSDF_WAVE_TIMES=1
+ *   timeline build, tools/wave_times.py)
  *   [19] screened plane maxima that fell back to the full fp64 scan (per
  *   wave) [20] evaluations rejected early by the screen [21] descent-walk
- *   steps (per wave) [22] split items (seed groups) evaluated by the
- *   overflow kernel [23] lanes in them. 24 counters. */
+ *   steps (per wave) [22..23] reserved (0). 24 counters. */
 int fsdf_kernel_stats(fsdf_ctx* ctx, int32_t enable, uint64_t* counters_out);
 
 #ifdef __cplusplus

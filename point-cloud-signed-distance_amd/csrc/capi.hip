@@ -29,11 +29,6 @@ constexpr int kPoseRing = 8;
 #ifndef FSDF_CHUNK_WS
 #define FSDF_CHUNK_WS 1  // passes over the resident cloud read the chunk spheres of set_points
 #endif
-#ifndef FSDF_SPLIT_BUDGET
-#define FSDF_SPLIT_BUDGET 0
-#endif
-constexpr int kSplitBudgetDefault = FSDF_SPLIT_BUDGET;  // distinct seed hulls a wave keeps before it splits
-constexpr int kSplitItems = 16384;                      // split items per pass (then waves evaluate in place)
 
 template <typename P>
 hipError_t dalloc(P** p, size_t bytes) {
@@ -135,16 +130,6 @@ struct fsdf_ctx {
   size_t prof_used = 0;             // events recorded (2 per pass)
   unsigned long long* d_stats = nullptr;  // fsdf_kernel_stats
   bool stats_on = false;
-  // split of heavy waves (fsdf::SpillBufs; fsdf_set_split_budget)
-  int split_budget = kSplitBudgetDefault;
-  int32_t* d_spill_ctr = nullptr;    // [4], zeroed once, then by every reduce
-  int32_t* d_spill_items = nullptr;  // [kSplitItems][4]
-  void* d_spill_res = nullptr;       // T [kSplitItems][64][4]
-  int32_t* d_spill_res_k = nullptr;  // [kSplitItems][64]
-  int32_t* d_chunk_items = nullptr;  // [spill_n64 / 64][2]
-  int32_t* d_blk_mask = nullptr;     // [kMaxBlocks]
-  int32_t* d_split_blocks = nullptr; // [kMaxBlocks]
-  int64_t spill_n64 = 0;
   // mechanism of fsdf_set_mechanism (host arrays; fsdf_value_and_gradient)
   struct Mechanism {
     int nb = 0, nq = 0;
@@ -162,8 +147,6 @@ struct fsdf_ctx {
     double weight = 10.0;  // default_deformation_cost_weight (src/gradientdescent.jl:7)
     std::vector<double> rows, body_wrench, x_prepared;
   } mech;
-  fsdf::SpillBufs* d_spill_dev = nullptr;  // device copy of the record (read by the pass kernel)
-  fsdf::SpillBufs spill_dev_copy;          // what d_spill_dev holds (host, stable address)
 };
 
 static int fail(fsdf_ctx* c, int code, const char* fmt, ...) {
@@ -283,14 +266,6 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   dfree(c->d_stats);
   dfree(c->d_block_cost);
   dfree(c->d_block_order);
-  dfree(c->d_spill_ctr);
-  dfree(c->d_spill_items);
-  dfree(c->d_spill_res);
-  dfree(c->d_spill_res_k);
-  dfree(c->d_chunk_items);
-  dfree(c->d_blk_mask);
-  dfree(c->d_split_blocks);
-  dfree(c->d_spill_dev);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (int i = 0; i < kPoseRing; ++i) {
     if (c->pose_ev[i]) (void)hipEventDestroy(c->pose_ev[i]);
@@ -337,6 +312,8 @@ extern "C" int fsdf_num_points(const fsdf_ctx* c, int64_t* n) {
   *n = c->n;
   return FSDF_OK;
 }
+
+static decltype(fsdf_ctx::mech) fresh_mechanism() { return {}; }
 
 extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t S) {
   if (!c) return FSDF_ERR_ARG;
@@ -609,7 +586,10 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   c->h_surface_kind = surface_kind;
   c->h_n_centers.assign(S, 0);
   for (int k = 0; k < S; ++k) c->h_n_centers[k] = surfs[k].kind == FSDF_SURFACE_RBF ? surfs[k].n_centers : 0;
-  c->mech.rbf.clear();  // centre declarations refer to the previous surface list
+  // the mechanism's surface bodies / frames / poses and the RBF centre
+  // declarations refer to the previous surface list: drop them all (the
+  // caller re-registers with fsdf_set_mechanism; iterations fail until then)
+  c->mech = fresh_mechanism();
   c->lm.rbf_rows = nrows;
   c->lm.rbf_acc = rbf_acc_off.back();
   c->lm.hull_surface = c->d_hull_surface;
@@ -800,46 +780,6 @@ static int release_posed(fsdf_ctx* c, int buf) {
   return FSDF_OK;
 }
 
-// buffers of a split pass over n64 resident slots (grown only)
-static int ensure_split(fsdf_ctx* c, int nblocks, fsdf::SpillBufs* sp, const fsdf::SpillBufs*& out_dev) {
-  const size_t tsz = c->precision == 64 ? sizeof(double) : sizeof(float);
-  if (!c->d_spill_ctr) {
-    HIPCHECK(c, hipMalloc(&c->d_spill_ctr, 4 * sizeof(int32_t)));
-    HIPCHECK(c, hipMemsetAsync(c->d_spill_ctr, 0, 4 * sizeof(int32_t), c->stream));
-    HIPCHECK(c, hipMalloc(&c->d_spill_items, (size_t)kSplitItems * 4 * sizeof(int32_t)));
-    HIPCHECK(c, hipMalloc(&c->d_spill_res, (size_t)kSplitItems * 64 * 4 * tsz));
-    HIPCHECK(c, hipMalloc(&c->d_spill_res_k, (size_t)kSplitItems * 64 * sizeof(int32_t)));
-    HIPCHECK(c, hipMalloc(&c->d_blk_mask, (size_t)fsdf::kMaxBlocks * sizeof(int32_t)));
-    HIPCHECK(c, hipMalloc(&c->d_split_blocks, (size_t)fsdf::kMaxBlocks * sizeof(int32_t)));
-  }
-  const int64_t n64 = (int64_t)nblocks * fsdf::kPassBlock;
-  if (c->spill_n64 < n64) {
-    HIPCHECK(c, hipStreamSynchronize(c->stream));  // earlier passes may still read them
-    dfree(c->d_chunk_items);
-    c->spill_n64 = 0;
-    HIPCHECK(c, hipMalloc(&c->d_chunk_items, (size_t)(n64 / 64) * 2 * sizeof(int32_t)));
-    c->spill_n64 = n64;
-  }
-  sp->budget = c->split_budget;
-  sp->cap_items = kSplitItems;
-  sp->ctr = c->d_spill_ctr;
-  sp->items = c->d_spill_items;
-  sp->res = c->d_spill_res;
-  sp->res_k = c->d_spill_res_k;
-  sp->chunk_items = c->d_chunk_items;
-  sp->blk_mask = c->d_blk_mask;
-  sp->blocks = c->d_split_blocks;
-  if (!c->d_spill_dev) HIPCHECK(c, hipMalloc(&c->d_spill_dev, sizeof(fsdf::SpillBufs)));
-  if (memcmp(&c->spill_dev_copy, sp, sizeof(*sp)) != 0) {  // the pass kernel reads the device copy
-    // rare (new buffers or budget): drain the passes that read the old record, then replace it
-    HIPCHECK(c, hipStreamSynchronize(c->stream));
-    c->spill_dev_copy = *sp;
-    HIPCHECK(c, hipMemcpy(c->d_spill_dev, &c->spill_dev_copy, sizeof(*sp), hipMemcpyHostToDevice));
-  }
-  out_dev = c->d_spill_dev;
-  return FSDF_OK;
-}
-
 #ifndef FSDF_ORDER_EVERY
 #define FSDF_ORDER_EVERY 16
 #endif
@@ -874,18 +814,11 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
     out.cost = c->d_block_cost;
     out.order = c->order_nblocks == nblocks ? c->d_block_order : nullptr;
   }
-  const bool split = n > 0 && c->split_budget > 0 &&
-                     fsdf::pass_can_split(c->precision, c->cull != 0, c->lm, n, nblocks);
-  if (split) {
-    rc = ensure_split(c, nblocks, &out.spill, out.spill_dev);
-    if (rc) return rc;
-  }
   if (n > 0) {
     const bool prof = c->profiling && c->prof_used + 3 <= c->prof_ev.size();
     if (prof) HIPCHECK(c, hipEventRecord(c->prof_ev[c->prof_used], c->stream));
     HIPCHECK(c, fsdf::launch_pass(c->precision, c->cull != 0, c->lm, *P, d_pts, n, nblocks, out, c->stream));
     if (prof) HIPCHECK(c, hipEventRecord(c->prof_ev[c->prof_used + 1], c->stream));
-    if (split) HIPCHECK(c, fsdf::launch_split(c->precision, c->lm, *P, d_pts, n, nblocks, out, c->stream));
     rc = release_posed(c, pbuf);
     if (rc) return rc;
     if (prof) {
@@ -897,8 +830,7 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
     // pass; the rebuild is a ~7 us single-workgroup sort on the reduce launch)
     const bool rebuild = out.cost && (c->order_nblocks != nblocks || ++c->order_age >= kOrderEvery);
     HIPCHECK(c, fsdf::launch_reduce(c->d_partials, nblocks, accum_len(c), d_accum, c->stream,
-                                    rebuild ? out.cost : nullptr, rebuild ? c->d_block_order : nullptr,
-                                    split ? c->d_spill_ctr : nullptr));
+                                    rebuild ? out.cost : nullptr, rebuild ? c->d_block_order : nullptr));
     if (rebuild) {
       c->order_nblocks = nblocks;
       c->order_age = 0;
@@ -1131,6 +1063,8 @@ extern "C" int fsdf_set_deformations(fsdf_ctx* c, int32_t n_deform, double weigh
 static int iteration_prepare(fsdf_ctx* c, const double* x, const char* who) {
   auto& M = c->mech;
   if (M.nb == 0) return fail(c, FSDF_ERR_STATE, "%s: no mechanism (call fsdf_set_mechanism)", who);
+  if ((int)M.surface_body.size() != c->lm.S || (int)M.poses.size() != 12 * c->lm.S)
+    return fail(c, FSDF_ERR_STATE, "%s: mechanism registered for another surface list (call fsdf_set_mechanism)", who);
   const int R = c->lm.R;
   if (R > 0) {
     bool all = (int)M.rbf.size() == R;
@@ -1403,12 +1337,6 @@ extern "C" int fsdf_pass_time(fsdf_ctx* c, double* total_ms, int64_t* launches) 
   return fsdf_pass_times(c, &k, total_ms, launches);
 }
 
-extern "C" int fsdf_set_split_budget(fsdf_ctx* c, int32_t evals) {
-  if (!c) return FSDF_ERR_ARG;
-  if (evals < 0) return fail(c, FSDF_ERR_ARG, "set_split_budget: evals must be >= 0 (0 = never split)");
-  c->split_budget = evals;
-  return FSDF_OK;
-}
 
 #ifndef FSDF_WAVE_TIMES
 #define FSDF_WAVE_TIMES 0

@@ -29,7 +29,7 @@
 //                               b = 2j+1 (= a when nf is odd and j is the last pair),
 //                               d' = d - n·c with c the hull's f32 sphere centre
 //
-//   per-block partial sums  partials [len][nblocks] f64, len = 1+6S+Σ(4n+4) (column = block)
+//   per-block partial sums  partials [len/8][nblocks][8] f64 line tiles, len = 1+6S+Σ(4n+4)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -102,30 +102,8 @@ struct PosedModel {
   void* rbf_rows = nullptr;   // T [rbf_rows][4], per pass (fsdf_set_rbf_params)
 };
 
-// Split of heavy waves (hull-only scenes, <= 64 surfaces, culled, one
-// wave-iteration per wave). A wave evaluates every hull its 64 points may be
-// nearest to in sequence, each lane's best-first seed hull first; a wave whose
-// points have more than `budget` distinct seeds (points among many hulls, the
-// waves that set the pass time) instead hands its lanes over as items, one per
-// seed group (chunk, seed, lane mask). The overflow kernel runs each item as a
-// scene evaluation of those lanes alone (one wave each, all items in
-// parallel): a lane's result does not depend on the other lanes of its wave,
-// so it is final. The merge kernel gathers the lanes of each split chunk, runs
-// the chunk epilogue and adds the chunk's sums to its block's partial column.
-struct SpillBufs {
-  int budget = 0;                  // distinct seeds a wave keeps (0 = never split)
-  int cap_items = 0;
-  int32_t* ctr = nullptr;          // [0] items reserved, [1] split blocks (zeroed by the reduce kernel)
-  int32_t* items = nullptr;        // [cap_items][4] (chunk, seed, lane mask lo, hi); chunk -1 = unused slot
-  void* res = nullptr;             // T [cap_items][64][4]: d*, gradient of the item's lanes
-  int32_t* res_k = nullptr;        // [cap_items][64] k*
-  int32_t* chunk_items = nullptr;  // [n64/64][2] first item, item count
-  int32_t* blk_mask = nullptr;     // [nblocks] split waves of each logical block (bit w)
-  int32_t* blocks = nullptr;       // [nblocks] logical blocks with a split wave (ctr[1] entries)
-};
-
 struct PassOutputs {
-  double* partials = nullptr;  // [len][nblocks] (sdf_kernels.hip pidx)
+  double* partials = nullptr;  // line tiles (sdf_kernels.hip pidx)
   int32_t* kstar = nullptr;    // optional, caller order
   double* d = nullptr;         // optional
   double* grad = nullptr;      // optional [n][3]
@@ -137,11 +115,6 @@ struct PassOutputs {
   // logical-block columns, so results do not depend on the order.
   const int32_t* order = nullptr;
   uint32_t* cost = nullptr;
-  // split of heavy waves: the host copy (launch decisions, overflow / merge
-  // kernels) and the same record in device memory, which the pass kernel reads
-  // only on its split path (its pointers would not fit in the SGPR budget)
-  SpillBufs spill;
-  const SpillBufs* spill_dev = nullptr;
   // optional [n64/64][4] f32 bounding sphere of each 64-point chunk of the
   // resident cloud (launch_chunk_spheres at set_points; pose-independent)
   const float* chunk_ws = nullptr;
@@ -162,11 +135,6 @@ hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_pose
 hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm,
                        const void* d_pts, int64_t n, int nblocks, const PassOutputs& out,
                        hipStream_t s);
-// whether a pass of this model / grid can split heavy waves (out.spill usable)
-bool pass_can_split(int precision, bool cull, const LocalModel& lm, int64_t n, int nblocks);
-// the overflow and merge kernels of a split pass (after launch_pass, before the reduce)
-hipError_t launch_split(int precision, const LocalModel& lm, const PosedModel& pm, const void* d_pts, int64_t n,
-                        int nblocks, const PassOutputs& out, hipStream_t s);
 
 // origin: 3 host doubles (passed by value); d_rays [n][3] f64 unit directions.
 hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const double* origin,
@@ -175,8 +143,7 @@ hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const 
 // With cost/order: one extra workgroup also rebuilds order[] (heaviest logical
 // blocks first) from this pass's costs, for the next pass of the same grid.
 hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum,
-                         hipStream_t s, const uint32_t* cost = nullptr, int32_t* order = nullptr,
-                         int32_t* spill_ctr = nullptr);
+                         hipStream_t s, const uint32_t* cost = nullptr, int32_t* order = nullptr);
 
 hipError_t launch_to_f32(const double* src, float* dst, int64_t count, hipStream_t s);
 

@@ -373,29 +373,11 @@ __device__ __forceinline__ float load_hull_table(const PassModel<T>& m, HullRow*
 }
 
 constexpr int kMaxRbfAcc = kMaxRbfAccum;
-// Diagnostic phase timing (-DFSDF_PHASE_TIMING=1): lane 0 of each wave adds
-// shader-clock deltas to stats[10..18]: culling, hull staging, plane max, fast
-// path, closest-feature search, whole wave-iteration, segmented reduction,
-// per-point stores, scene evaluation.
+// The one diagnostic build (-DFSDF_WAVE_TIMES=1, tools/wave_times.py): a
+// per-wave timeline with per-phase 100 MHz clocks and event counts; every hook
+// below compiles to nothing in the product library.
 #ifndef FSDF_WAVE_TIMES
 #define FSDF_WAVE_TIMES 0
-#endif
-#ifndef FSDF_PHASE_TIMING
-#define FSDF_PHASE_TIMING 0
-#endif
-// (the clock read drains every outstanding memory operation and pins the
-// schedule, so a phase is charged for its own loads)
-__device__ __forceinline__ uint64_t phase_clock() {
-  if (!FSDF_PHASE_TIMING) return 0;
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_waitcnt(0);
-  const uint64_t t = __builtin_amdgcn_s_memtime();
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-#if FSDF_PHASE_TIMING
-__shared__ unsigned long long fsdf_phase_acc[kBlock / 64][10];  // per wave, flushed at kernel end
 #endif
 #if FSDF_WAVE_TIMES
 // per wave-iteration, packed 16-bit fields:
@@ -432,32 +414,11 @@ __device__ __forceinline__ void wt_count(int f, uint64_t v) {
   if ((threadIdx.x & 63) == 0) fsdf_wave_ev[threadIdx.x >> 6][f >> 2] += v << (16 * (f & 3));
 #endif
 }
-__device__ __forceinline__ void phase_add(unsigned long long* stats, int slot, uint64_t t0) {
-#if FSDF_PHASE_TIMING
-  const uint64_t t1 = phase_clock();
-  if (stats && (threadIdx.x & 63) == 0) fsdf_phase_acc[threadIdx.x >> 6][slot - 10] += t1 - t0;
-#endif
-}
-// the event counters (stats[0..9]) are off in phase-timing builds: their
+// the event counters (fsdf_kernel_stats) are off in the timeline build: their
 // contended atomics would dominate the timed windows
 __device__ __forceinline__ bool count_events(const unsigned long long* stats) {
-  return !FSDF_PHASE_TIMING && !FSDF_WAVE_TIMES && stats != nullptr;
-}  // RBF adjoint doubles per wave (Σ 4n+4)
-// Diagnostic ablations (timing-only builds via -DFSDF_ABLATE=mask; results are
-// wrong): 4 no slow path, 16 no segmented reduction, 32 no per-point stores,
-// 64 no hull staging loads (LDS stage left as is), 128 no plane max (face 0),
-// 256 certificates skipped (stage A accepted), 512 no stage B/C; marginal-cost
-// doubles (same results): 65536 hull staging, 131072 fp32 screen, 262144 culling.
-#ifndef FSDF_ABLATE
-#define FSDF_ABLATE 0
-#endif
-// Per-hull wrench sums by LDS f64 atomics (1) or by the segmented ballot loop
-// with DPP wave sums (0). The atomics free ~150 VALU instructions per wave but
-// serialize a wave's 64 same-row adds in the LDS: measured 12 % slower (M64,
-// 2^20 points), so the loop stays.
-#ifndef FSDF_LDS_ATOMIC_SUMS
-#define FSDF_LDS_ATOMIC_SUMS 0
-#endif
+  return !FSDF_WAVE_TIMES && stats != nullptr;
+}
 #ifndef FSDF_PASS_WAVES_PER_SIMD
 #define FSDF_PASS_WAVES_PER_SIMD 4
 #endif
@@ -500,8 +461,7 @@ __device__ __forceinline__ void stage_hull(void* __restrict__ lw, const I4* __re
     for (int j = 0; j < 8; ++j) {
       const int c = min(c0 + 64 * j + lane, N - 1);
       const I4* src = c < P ? s0 + c : (c < Q ? s1 + (c - P) : (c < N3 ? s2 + (c - Q) : s3 + (c - N3)));
-      if (!(FSDF_ABLATE & 64)) v[j] = *src;
-      else v[j] = I4{c, c, c, 0};
+      v[j] = *src;
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -510,20 +470,6 @@ __device__ __forceinline__ void stage_hull(void* __restrict__ lw, const I4* __re
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Wave-uniform rows read through the scalar unit: a pointer in the constant
-// address space makes every uniform-index read an s_load into SGPRs, which the
-// VALU takes as a broadcast operand — no LDS bandwidth (the plane max was
-// LDS-bound: two broadcast ds_read_b128 per face and wave, 4 waves per LDS).
-#ifndef FSDF_SCALAR_PLANES
-#define FSDF_SCALAR_PLANES 0
-#endif
-template <typename T>
-using CRow = const __attribute__((address_space(4))) typename Row4<T>::type*;
-template <typename T>
-__device__ __forceinline__ CRow<T> scalar_rows(const T* p) {
-  return (CRow<T>)(p);
 }
 
 template <typename T>
@@ -627,19 +573,6 @@ __device__ __forceinline__ bool cert_step(T px, T py, T pz, int f, int reg,
 // ---------------------------------------------------------------------------
 template <typename T>
 constexpr bool kStagePairs = sizeof(T) == 8 && FSDF_SCREEN32;
-// Seed phase: skip seeds no lane needs any more (1); take the seed shared by
-// the most pending lanes first (1) instead of the first pending lane's (0).
-// Measured on the bench cloud: no seed is ever skipped (hull evaluations
-// 26,835 either way) and the ordering is 1-2 % slower: both off.
-#ifndef FSDF_SEED_SKIP
-#define FSDF_SEED_SKIP 0
-#endif
-#ifndef FSDF_SEED_ORDER
-#define FSDF_SEED_ORDER 0
-#endif
-#ifndef FSDF_SCREEN_INTERLEAVE
-#define FSDF_SCREEN_INTERLEAVE 0
-#endif
 #ifndef FSDF_SCREEN_ILP
 #define FSDF_SCREEN_ILP 4
 #endif
@@ -670,20 +603,6 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
       c[2 * q] = ls[2 * j];
       c[2 * q + 1] = ls[2 * j + 1];
     }
-#if FSDF_SCREEN_INTERLEAVE
-    // the four pairs' fma chains advanced stage by stage (independent
-    // neighbours: no dependent back-to-back packed ops); same operations
-    F2v h[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) h[q] = __builtin_elementwise_fma(F2v{c[2 * q + 1][0], c[2 * q + 1][1]}, qz2,
-                                                                 F2v{c[2 * q + 1][2], c[2 * q + 1][3]});
-#pragma unroll
-    for (int q = 0; q < 4; ++q) h[q] = __builtin_elementwise_fma(F2v{c[2 * q][2], c[2 * q][3]}, qy2, h[q]);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) h[q] = __builtin_elementwise_fma(F2v{c[2 * q][0], c[2 * q][1]}, qx2, h[q]);
-    return fmaxf(fmaxf(fmaxf(h[0][0], h[0][1]), fmaxf(h[1][0], h[1][1])),
-                 fmaxf(fmaxf(h[2][0], h[2][1]), fmaxf(h[3][0], h[3][1])));
-#else
     float hm[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -693,7 +612,6 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
       hm[q] = fmaxf(h[0], h[1]);
     }
     return fmaxf(fmaxf(hm[0], hm[1]), fmaxf(hm[2], hm[3]));
-#endif
   };
   auto update = [&](float mb, int i) {
     b2 = fmaxf(b2, fminf(b1, mb));
@@ -763,7 +681,6 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   const int nf = __builtin_amdgcn_readfirstlane(ht[k + 1].f0) - f0;
   const int v0 = __builtin_amdgcn_readfirstlane(ht[k].v0);
   const int nv = __builtin_amdgcn_readfirstlane(ht[k + 1].v0) - v0;
-  uint64_t tp = phase_clock();
   uint64_t tw = wt_now();
 #if FSDF_WAVE_TIMES
   fsdf_wt_slow[threadIdx.x] = false;
@@ -779,18 +696,14 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   // one-chunk-per-wave pass (P64: pass_kernel ALIAS, LocalModel::planes64)
   constexpr bool kP64 = kStagePairs<T> && P64;
   const int npl = kP64 ? nf * cpr : 0;
-  for (int rep = (FSDF_ABLATE & 65536) ? 2 : 1; rep > 0; --rep)  // (2x: marginal-cost ablation)
-    stage_hull(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0), nv * cpr,
-               m.face_rows + f0, nf);
-  phase_add(stats, 11, tp);
-  tp = phase_clock();
+  stage_hull(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0), nv * cpr,
+             m.face_rows + f0, nf);
   tw = wt_add(0, tw);
   const R* lp = kP64 ? (const R*)((const I4*)lw + np2) : (kStagePairs<T> ? (const R*)(m.planes + 4 * f0) : (const R*)lw);
   const R* lv = (const R*)((const I4*)lw + np2 + npl);
   const I4* lf = (const I4*)(lv + nv);
   const T scale = (T)ht[k].hscale;
-  const CRow<T> gp = scalar_rows<T>(m.planes + 4 * f0);  // uniform plane rows (SGPR)
-  auto uplane = [&](int f) -> R { return FSDF_SCALAR_PLANES ? (R)gp[f] : lp[f]; };
+  auto uplane = [&](int f) -> R { return lp[f]; };
   // two independent running maxima (even / odd faces) shorten the serial
   // compare chain; merged with the first-index rule, identical to one chain
   // Batches of kPlaneBatch rows, all of a batch's LDS reads issued before the
@@ -801,17 +714,10 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   // rows of the last batch repeat the last face (same value, never first).
   T hA = -tinf<T>();
   int iA = 0;
-  bool screened = (FSDF_ABLATE & 128) != 0;  // ablation: no plane max (face 0)
-  if (screened) hA = plane_h<T>(lp[0], px, py, pz);
+  bool screened = false;
   if constexpr (sizeof(T) == 8) {
     bool rejected = false;
-    if (FSDF_SCREEN32 && !screened)
-      screened = screen_plane_max(px, py, pz, k, f0, nf, m, ht, lw, lp, active, bound, hA, iA, rejected);
-    if (FSDF_ABLATE & 131072) {  // 2x screen (marginal cost; identical result)
-      T h2; int i2; bool r2;
-      const bool s2 = screen_plane_max(px + (T)0 * hA, py, pz, k, f0, nf, m, ht, lw, lp, active, bound, h2, i2, r2);
-      screened = screened && s2; rejected = rejected && r2;
-    }
+    if (FSDF_SCREEN32) screened = screen_plane_max(px, py, pz, k, f0, nf, m, ht, lw, lp, active, bound, hA, iA, rejected);
     if (count_events(stats) && lane_id() == 0) {
       if (rejected) atomicAdd(stats + 20, 1ull);
       else if (!screened) atomicAdd(stats + 19, 1ull);
@@ -821,7 +727,6 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
     if (rejected) {  // cannot win nor tie for any lane that needs it
       d = tinf<T>();
       gx = gy = gz = (T)0;
-      phase_add(stats, 12, tp);
       wt_add(1, tw);
       return;
     }
@@ -854,8 +759,6 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
     if (plane_h<T>(lp[f], px, py, pz) == hA) iA = f;
   }
   }
-  phase_add(stats, 12, tp);
-  tp = phase_clock();
   tw = wt_add(1, tw);
   if (count_events(stats) && lane_id() == 0) {
     atomicAdd(stats + 9, (unsigned long long)nf);
@@ -884,17 +787,15 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
 #if FSDF_WAVE_TIMES
   wt_count(10, __builtin_popcountll(__ballot(slow && active && (hmax - lb_margin > bound))));
 #endif
-  slow = slow && active && !(hmax - lb_margin > bound) && !(FSDF_ABLATE & 4);
+  slow = slow && active && !(hmax - lb_margin > bound);
   const uint64_t slow_mask = __ballot(slow);
 #if FSDF_WAVE_TIMES
   wt_count(8, __builtin_popcountll(slow_mask));
   fsdf_wt_slow[threadIdx.x] = slow;
 #endif
-  phase_add(stats, 13, tp);
   tw = wt_add(2, tw);
   if (!slow_mask) return;
   wt_count(2, 1);
-  tp = phase_clock();
   if (count_events(stats) && (threadIdx.x & 63) == 0) {
     atomicAdd(stats + 2, 1ull);
     atomicAdd(stats + 4, (unsigned long long)__builtin_popcountll(slow_mask));
@@ -911,7 +812,7 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   // face(s) the certificate names (each accepted step strictly lowers the
   // distance, so the walk cannot cycle); lanes that stall or exceed the step
   // cap keep `todo` for the exhaustive stage C.
-  bool todo = !(FSDF_ABLATE & 256) && slow;
+  bool todo = slow;
   int cf = fs, cr = rA;
   bool walking = todo;
   const uint64_t tw_walk = wt_now();
@@ -944,7 +845,7 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
     }
   }
   wt_add(7, tw_walk);  // (the descent walk: certificates and steps)
-  if (__any(todo) && !(FSDF_ABLATE & 512)) {
+  if (__any(todo)) {
     if (count_events(stats) && (threadIdx.x & 63) == 0) atomicAdd(stats + 6, 1ull);
     const uint64_t scan_mask = __ballot(todo);
     if (scan_mask) {
@@ -989,7 +890,6 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
       if (todo) { best2 = b2; qx = bx; qy = by; qz = bz; }
     }
   }
-  phase_add(stats, 14, tp);
   wt_add(3, tw);
   if (slow) {
     if (best2 > (T)0) {
@@ -1072,9 +972,6 @@ __device__ __forceinline__ double dpp_shifted(double v) {
   const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROW_MASK, 0xf, true);
   return __hiloint2double(hi, lo);
 }
-#ifndef FSDF_DPP_SUM
-#define FSDF_DPP_SUM 1
-#endif
 // Wave-wide f32 min / max in the VALU (DPP scan, identity fill), result to
 // every lane. Whole wave active.
 template <int CTRL, int ROW_MASK>
@@ -1126,11 +1023,6 @@ __global__ __launch_bounds__(kBlock) void chunk_sphere_kernel(const T* __restric
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
-  if (!FSDF_DPP_SUM) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-  }
   v += dpp_shifted<0x111, 0xf>(v);  // row_shr:1
   v += dpp_shifted<0x112, 0xf>(v);  // row_shr:2
   v += dpp_shifted<0x114, 0xf>(v);  // row_shr:4
@@ -1197,51 +1089,11 @@ __device__ __forceinline__ void rbf_adjoint(T px, T py, T pz, const T* __restric
 // gradient. Wave-cooperative (ballots, LDS staging): call with the whole wave
 // active; `valid` marks lanes whose result is used.
 // ---------------------------------------------------------------------------
-// SPILL (pass kernel, SLOTS == 1, hulls only): a wave whose valid lanes have
-// more than sp->budget distinct seed hulls hands them over as one item per
-// seed group (split_wave) and returns with *spilled set; the overflow kernel
-// evaluates the groups in parallel and the merge kernel finishes the chunk.
-// Returns false (evaluate here) when the item buffer is full.
-__device__ __forceinline__ bool split_wave(uint64_t seeds, int kseed, bool valid, int64_t base,
-                                           const SpillBufs& sp) {
-  const int lane = threadIdx.x & 63;
-  const int m = __builtin_popcountll(seeds);
-  int old = 0;
-  if (lane == 0) old = atomicAdd(sp.ctr, m);
-  old = __builtin_amdgcn_readfirstlane(__shfl(old, 0, 64));
-  if (old + m > sp.cap_items) {
-    // no room: mark the reserved slots below the cap unused
-    if (lane < m && old + lane < sp.cap_items) sp.items[4 * (old + lane)] = -1;
-    return false;
-  }
-  const int64_t chunk = base >> 6;
-  int j = old;
-  for (uint64_t r = seeds; r; r &= r - 1, ++j) {
-    const int s = __builtin_ctzll(r);
-    const uint64_t mask = __ballot(valid && kseed == s);
-    if (lane == 0) {
-      int32_t* it = sp.items + 4 * j;
-      it[0] = (int32_t)chunk;
-      it[1] = s;
-      it[2] = (int32_t)(uint32_t)mask;
-      it[3] = (int32_t)(uint32_t)(mask >> 32);
-    }
-  }
-  if (lane == 0) {
-    sp.chunk_items[2 * chunk] = old;
-    sp.chunk_items[2 * chunk + 1] = m;
-  }
-  return true;
-}
-
-template <typename T, int SLOTS, bool CULL, bool RBF, bool SPILL = false, bool P64 = false>
+template <typename T, int SLOTS, bool CULL, bool RBF, bool P64 = false>
 __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const PassModel<T>& m,
                                            const HullRow* __restrict__ ht, float smax, T* __restrict__ lw,
                                            unsigned long long* __restrict__ stats, T& best, int& bk, T& gx, T& gy,
-                                           T& gz, const F4* __restrict__ cws = nullptr,
-                                           const SpillBufs* sp = nullptr, int64_t base = 0,
-                                           bool* spilled = nullptr) {
-  static_assert(!SPILL || (SLOTS == 1 && CULL && !RBF), "split waves: culled hull-only <= 64 surfaces");
+                                           T& gz, const F4* __restrict__ cws = nullptr) {
   const int K = m.K;
   const int lane = threadIdx.x & 63;
   // Phase A (fp32, exact-safe): with c_k inside hull k and r_k its bounding
@@ -1259,14 +1111,12 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     const int left = K - 64 * s;
     cand[s] = left >= 64 ? ~0ull : (left > 0 ? (1ull << left) - 1 : 0ull);
   }
-  const uint64_t tc = phase_clock();
   uint64_t tw = wt_now();
   // the wave's bounding sphere (bbox centre, half diagonal) over the valid
   // lanes: precomputed per resident chunk at set_points (pose-independent,
   // the same arithmetic) or computed here
   pxf = (float)px; pyf = (float)py; pzf = (float)pz;
   WaveSphere ws;
-  for (int rep = (FSDF_ABLATE & 262144) ? 2 : 1; rep > 0; --rep) {  // (2x: marginal-cost ablation)
   if (cws) {
     const F4 v = *cws;
     ws = WaveSphere{v[0], v[1], v[2], v[3]};
@@ -1325,25 +1175,10 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
       }
     }
   }
-  }
   const float ub = __builtin_sqrtf(ub2);
-  phase_add(stats, 10, tc);
   tw = wt_add(4, tw);
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) wt_count(6, __builtin_popcountll(cand[s]));
-  if (SPILL) {
-    // distinct seed hulls of the valid lanes (one wave-evaluation each)
-    uint64_t seeds = 0;
-    for (uint64_t rem = __ballot(valid); rem;) {
-      const int sd = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(rem), 64));
-      seeds |= 1ull << sd;
-      rem &= ~__ballot(valid && kseed == sd);
-    }
-    if (__builtin_popcountll(seeds) > sp->budget && split_wave(seeds, kseed, valid, base, *sp)) {
-      *spilled = true;
-      return;
-    }
-  }
   // one rounding margin per lane, >= 1e-5 x every magnitude in the test below
   const float mrg = 1e-5f * (1.0f + fabsf(pxf) + fabsf(pyf) + fabsf(pzf) + smax + 2.0f * ub);
 
@@ -1411,31 +1246,12 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     int k;
     bool need;
     if (pend) {
-      uint64_t grp;
-      if (FSDF_SEED_ORDER) {
-        // the pending seed shared by the most lanes first (tightens the most bounds)
-        k = 0;
-        grp = 0;
-        int most = -1;
-        for (uint64_t r = pend; r;) {
-          const int sk = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(r), 64));
-          const uint64_t g = __ballot(valid && kseed == sk);
-          r &= ~g;
-          const int c = __builtin_popcountll(g);
-          if (c > most) { most = c; k = sk; grp = g; }
-        }
-      } else {
-        k = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(pend), 64));
-        grp = __ballot(valid && kseed == k);
-      }
-      pend &= ~grp;
+      k = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(pend), 64));
+      pend &= ~__ballot(valid && kseed == k);
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s)
         if ((k >> 6) == s) done[s] |= 1ull << (k & 63);
       need = needs(k);
-      // a seed no lane needs any more (earlier evaluations tightened the
-      // bounds) is skipped; bounds only tighten, so it is done for good
-      if (FSDF_SEED_SKIP && !__any(need)) continue;
       if (count_events(stats) && lane == 0) atomicAdd(stats + 5, 1ull);
       wt_count(4, 1);
     } else {
@@ -1467,8 +1283,7 @@ template <typename T, int SLOTS, bool RBF>
 __device__ __forceinline__ void emit_chunk(T px, T py, T pz, bool valid, T best, int bk, T gx, T gy, T gz, int64_t i,
                                            int64_t base, int64_t n, const PassModel<T>& m, const PassOutputs& out,
                                            double* __restrict__ acc_row, double& cost_acc,
-                                           double* __restrict__ rbf_wave, T* __restrict__ stage, int stage_cap,
-                                           uint64_t t_iter) {
+                                           double* __restrict__ rbf_wave, T* __restrict__ stage, int stage_cap) {
   const int lane = threadIdx.x & 63;
   // contributions: c += d^2; F_k += 2 d g; M_k += 2 d (p x g)
   double cF[3] = {0.0, 0.0, 0.0}, cM[3] = {0.0, 0.0, 0.0};
@@ -1483,27 +1298,8 @@ __device__ __forceinline__ void emit_chunk(T px, T py, T pz, bool valid, T best,
     cM[1] = w * __builtin_fma(dpz, dgx, -(dpx * dgz));
     cM[2] = w * __builtin_fma(dpx, dgy, -(dpy * dgx));
   }
-  phase_add(out.stats, 18, t_iter);
-  const uint64_t t_red = phase_clock();
   const uint64_t tw = wt_now();
-#if FSDF_LDS_ATOMIC_SUMS
-  // Hull surfaces: every valid lane adds its wrench into the LDS row of its
-  // k* (ds_add_f64; lanes of one k* are applied in lane order by the LDS, so
-  // the sums are deterministic); only RBF skins take the segmented loop.
-  bool hull_lane = valid && !(FSDF_ABLATE & 16);
-  if (RBF) hull_lane = hull_lane && m.surface_kind[bk] == 0;
-  if (hull_lane) {
-    double* r = acc_row - lane * 6 + (bk >> 6) * 64 * 6 + (bk & 63) * 6;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      __hip_atomic_fetch_add(r + j, cF[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_add(r + 3 + j, cM[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  }
-  uint64_t pending = RBF ? __ballot(valid && !hull_lane && !(FSDF_ABLATE & 16)) : 0ull;
-#else
-  uint64_t pending = (FSDF_ABLATE & 16) ? 0 : __ballot(valid);
-#endif
+  uint64_t pending = __ballot(valid);
   while (pending) {
     const int leader = __builtin_ctzll(pending);
     const int kk = __builtin_amdgcn_readfirstlane(__shfl(bk, leader, 64));
@@ -1530,9 +1326,7 @@ __device__ __forceinline__ void emit_chunk(T px, T py, T pz, bool valid, T best,
     }
   }
 
-  phase_add(out.stats, 16, t_red);
-  const uint64_t t_st = phase_clock();
-  if (!(FSDF_ABLATE & 32)) {
+  {
     if (out.perm) {  // caller order: scattered through the sort permutation
       if (valid) {
         const int64_t o = out.perm[i];
@@ -1572,23 +1366,15 @@ __device__ __forceinline__ void emit_chunk(T px, T py, T pz, bool valid, T best,
       }
     }
   }
-  phase_add(out.stats, 17, t_st);
   wt_add(6, tw);
 }
 
-// Per-block partial sums: entry t of logical block b, FSDF_PARTIALS_LAYOUT
-//   0 entry-major  partials[t][b]: each entry's column contiguous (the reduce
-//     coalesces), but a block writes one 8-B entry per 64-B line;
-//   1 block-major  partials[b][t]: whole-line writes (WRITE_SIZE 88.6 -> 50.6 MB
-//     per M64 pass, pass kernel -2.2 %), the reduce reads strided (+10 us);
-//   2 line tiles   partials[t / 8][b][t % 8]: a block writes whole 64-B lines
-//     and reduce_tiles_kernel reads whole lines.
-#ifndef FSDF_PARTIALS_LAYOUT
-#define FSDF_PARTIALS_LAYOUT 2
-#endif
-__device__ __forceinline__ int64_t pidx(int t, int b, int len, int nblocks) {
-  if (FSDF_PARTIALS_LAYOUT == 2) return ((int64_t)(t >> 3) * nblocks + b) * 8 + (t & 7);
-  return FSDF_PARTIALS_LAYOUT == 1 ? (int64_t)b * len + t : (int64_t)t * nblocks + b;
+// Per-block partial sums in line tiles: entry t of logical block b at
+// partials[t / 8][b][t % 8] — a block writes whole 64-B lines and
+// reduce_tiles_kernel reads whole lines (entry-major columns
+// wrote one 8-B entry per line, block-major rows made the reduce stride).
+__device__ __forceinline__ int64_t pidx(int t, int b, int nblocks) {
+  return ((int64_t)(t >> 3) * nblocks + b) * 8 + (t & 7);
 }
 
 // ---------------------------------------------------------------------------
@@ -1601,13 +1387,12 @@ extern __shared__ __attribute__((aligned(16))) char fsdf_lds[];
 // hull stage, which is free once the chunk's scene evaluation is done — 12 KiB
 // less LDS per workgroup, spent on staging the fp64 planes with the hull
 // (hull_sdf P64) at the same occupancy.
-template <typename T, int SLOTS, bool CULL, bool RBF, bool SPILL = false, bool ALIAS = false>
+template <typename T, int SLOTS, bool CULL, bool RBF, bool ALIAS = false>
 __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)) void pass_kernel(
     const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out) {
-  static_assert(!ALIAS || (SLOTS == 1 && !RBF && !SPILL), "aliased wrench rows: hull-only, <= 64 surfaces");
+  static_assert(!ALIAS || (SLOTS == 1 && !RBF), "aliased wrench rows: hull-only, <= 64 surfaces");
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  __shared__ int split_mask;  // SPILL: waves of this block that split their chunk
   // All LDS is one dynamic region (16-byte aligned carve, see pass_lds_bytes):
   //   red     [4 waves][kRedStride] f64  per-hull wrench sums + cost (not ALIAS)
   //   rbf_acc [4 waves][kMaxRbfAcc] f64  (RBF variants only)
@@ -1646,18 +1431,13 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
 #if FSDF_WAVE_TIMES
   const uint64_t t_block0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (SPILL && threadIdx.x == 0) split_mask = 0;  // ordered by load_hull_table's barrier
   const float smax = load_hull_table(m, ht);
-#if FSDF_PHASE_TIMING
-  if (lane < 10) fsdf_phase_acc[wave][lane] = 0;
-#endif
   const int64_t stride = (int64_t)gridDim.x * kPassBlock;
   for (int64_t base = (int64_t)lb * kPassBlock + wave * 64; base < n; base += stride) {
     const int64_t i = base + lane;
     const bool valid = i < n;
     const int64_t ii = valid ? i : n - 1;
     const T px = pts[3 * ii + 0], py = pts[3 * ii + 1], pz = pts[3 * ii + 2];
-    const uint64_t t_iter = phase_clock();
 #if FSDF_WAVE_TIMES
     const uint64_t w_t0 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0)
@@ -1667,10 +1447,8 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
 
     T best, gx, gy, gz;
     int bk;
-    bool spilled = false;
     const F4* cws = out.chunk_ws ? (const F4*)out.chunk_ws + (base >> 6) : nullptr;
-    scene_eval<T, SLOTS, CULL, RBF, SPILL, ALIAS>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz,
-                                           cws, out.spill_dev, base, &spilled);
+    scene_eval<T, SLOTS, CULL, RBF, ALIAS>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz, cws);
     if (!valid) bk = 0;
 
     if (ALIAS) {  // the stage is free: this wave's rows go there (once: one chunk per wave)
@@ -1678,15 +1456,9 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
       zero_rows();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (SPILL && spilled) {
-      // the merge kernel finishes this chunk (one wave-iteration per wave)
-      if (lane == 0) atomicOr(&split_mask, 1 << wave);
-    } else {
-      T* tstage = ALIAS ? (T*)((char*)stage + kRedStride * 8) : stage;  // gradient transpose after the rows
-      emit_chunk<T, SLOTS, RBF>(px, py, pz, valid, best, bk, gx, gy, gz, i, base, n, m, out, acc_row, cost_acc,
-                                rbf_wave, tstage, stage_cap, t_iter);
-    }
-    phase_add(out.stats, 15, t_iter);
+    T* tstage = ALIAS ? (T*)((char*)stage + kRedStride * 8) : stage;  // gradient transpose after the rows
+    emit_chunk<T, SLOTS, RBF>(px, py, pz, valid, best, bk, gx, gy, gz, i, base, n, m, out, acc_row, cost_acc,
+                              rbf_wave, tstage, stage_cap);
 #if FSDF_WAVE_TIMES
     // diagnostic: 100 MHz wall clock around each wave-iteration of the first
     // grid pass (stats + 32 + 2 * wave), written by lane 0
@@ -1703,9 +1475,6 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
 #endif
   }
 
-#if FSDF_PHASE_TIMING
-  if (out.stats && lane < 9) atomicAdd(out.stats + 10 + lane, fsdf_phase_acc[wave][lane]);
-#endif
   // ---- block combine (fixed order) ----
   cost_acc = wave_sum(cost_acc);
   if (lane == 0) red_of(wave)[SLOTS * 64 * 6] = cost_acc;
@@ -1725,11 +1494,7 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
 #pragma unroll
       for (int w = 1; w < kPassBlock / 64; ++w) s += rbf_acc[w * kMaxRbfAcc + src];
     }
-    out.partials[pidx(t, lb, len, gridDim.x)] = s;
-  }
-  if (SPILL && threadIdx.x == 0 && split_mask) {
-    out.spill_dev->blk_mask[lb] = split_mask;
-    out.spill_dev->blocks[atomicAdd(out.spill_dev->ctr + 1, 1)] = lb;
+    out.partials[pidx(t, lb, gridDim.x)] = s;
   }
   if (out.cost && threadIdx.x == 0) out.cost[lb] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_block);
 #if FSDF_WAVE_TIMES
@@ -1738,115 +1503,6 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
     out.stats[33 + 16 * kMaxBlocks + 2 * lb] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
-}
-
-// ---------------------------------------------------------------------------
-// Split pass, part 2: every item (chunk, seed group) handed over by the pass
-// kernel is one wave: a scene evaluation of the chunk's points restricted to
-// the group's lanes (its own wave culling, its lanes' seed first, then the
-// candidates they need), writing their final d*, k*, ∇d*. The items of a pass
-// run in parallel, so a chunk among many hulls no longer evaluates them in
-// sequence. LDS as the raycast: hull table, then one stage per wave.
-// ---------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(kBlock, kPassWavesPerSimd) void overflow_kernel(const T* __restrict__ pts, int64_t n,
-                                                                            PassModel<T> m, SpillBufs sp,
-                                                                            unsigned long long* __restrict__ stats) {
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  constexpr int kWaves = kBlock / 64;
-  const int count = min(sp.ctr[0], sp.cap_items);
-  if ((int)blockIdx.x * kWaves >= count) return;  // workgroup-uniform, before the table barrier
-  HullRow* ht = (HullRow*)fsdf_lds;
-  T* stage = (T*)((char*)(ht + m.K + 1) + wave * m.stage_bytes);
-  const float smax = load_hull_table(m, ht);
-  for (int it = blockIdx.x * kWaves + wave; it < count; it += gridDim.x * kWaves) {
-    const int32_t* item = sp.items + 4 * it;
-    const int chunk = __builtin_amdgcn_readfirstlane(item[0]);
-    if (chunk < 0) continue;  // a slot reserved past the capacity (never read)
-    const uint64_t mask = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(item[2]) |
-                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(item[3]) << 32);
-    const int64_t base = (int64_t)chunk * 64, i = base + lane;
-    const bool valid = ((mask >> lane) & 1) && i < n;
-    const int64_t ii = i < n ? i : n - 1;
-    const T px = pts[3 * ii + 0], py = pts[3 * ii + 1], pz = pts[3 * ii + 2];
-    T best, gx, gy, gz;
-    int bk;
-    scene_eval<T, 1, true, false>(px, py, pz, valid, m, ht, smax, stage, stats, best, bk, gx, gy, gz);
-    if (count_events(stats) && lane == 0) {
-      atomicAdd(stats + 22, 1ull);
-      atomicAdd(stats + 23, (unsigned long long)__builtin_popcountll(mask));
-    }
-    if (valid) {
-      T* r = (T*)sp.res + ((int64_t)it * 64 + lane) * 4;
-      r[0] = best;
-      r[1] = gx;
-      r[2] = gy;
-      r[3] = gz;
-      sp.res_k[(int64_t)it * 64 + lane] = bk;
-    }
-  }
-}
-
-// Split pass, part 3: one workgroup per logical block with a split wave. The
-// wave of each split chunk gathers its lanes' results from their seed-group
-// items (the same d*, k*, ∇d* as an unsplit pass), runs the chunk epilogue,
-// and the block adds its split waves' sums (fixed wave order) to the block's
-// partial column.
-template <typename T>
-__global__ __launch_bounds__(kPassBlock) void merge_kernel(const T* __restrict__ pts, int64_t n, int nblocks,
-                                                          PassModel<T> m, PassOutputs out) {
-  constexpr int kWaves = kPassBlock / 64;
-  constexpr int kRedStride = 64 * 6 + 2;
-  __shared__ double red[kWaves][kRedStride];
-  __shared__ double sgs[kWaves][192];  // per-wave gradient transpose (resident-order outputs)
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const SpillBufs& sp = out.spill;
-  const int count = sp.ctr[1];
-  for (int j = blockIdx.x; j < count; j += gridDim.x) {
-    const int lb = sp.blocks[j];
-    const int mask = sp.blk_mask[lb];
-    double* acc_row = &red[wave][lane * 6];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) acc_row[q] = 0.0;
-    double cost_acc = 0.0;
-    if ((mask >> wave) & 1) {
-      const int64_t base = (int64_t)lb * kPassBlock + wave * 64, i = base + lane;
-      const bool valid = i < n;
-      const int64_t ii = valid ? i : n - 1;
-      const T px = pts[3 * ii + 0], py = pts[3 * ii + 1], pz = pts[3 * ii + 2];
-      T best = (T)0, gx = (T)0, gy = (T)0, gz = (T)0;
-      int bk = 0;
-      const int64_t chunk = base >> 6;
-      const int b0 = sp.chunk_items[2 * chunk], c = sp.chunk_items[2 * chunk + 1];
-      for (int q = 0; q < c; ++q) {  // each valid lane is in exactly one seed group
-        const int32_t* item = sp.items + 4 * (b0 + q);
-        const uint32_t w = (uint32_t)(lane < 32 ? item[2] : item[3]);
-        if ((w >> (lane & 31)) & 1) {
-          const int64_t e = (int64_t)(b0 + q) * 64 + lane;
-          const T* r = (const T*)sp.res + 4 * e;
-          best = r[0]; gx = r[1]; gy = r[2]; gz = r[3];
-          bk = sp.res_k[e];
-        }
-      }
-      if (!valid) bk = 0;
-      emit_chunk<T, 1, false>(px, py, pz, valid, best, bk, gx, gy, gz, i, base, n, m, out, acc_row, cost_acc, nullptr,
-                              (T*)sgs[wave], 0, 0);
-    }
-    cost_acc = wave_sum(cost_acc);
-    if (lane == 0) red[wave][64 * 6] = cost_acc;
-    __syncthreads();
-    const int len = 1 + 6 * m.S;
-    for (int t = threadIdx.x; t < len; t += kPassBlock) {
-      const int src = t == 0 ? 64 * 6 : t - 1;
-      double s = red[0][src];
-#pragma unroll
-      for (int w = 1; w < kWaves; ++w) s += red[w][src];
-      out.partials[pidx(t, lb, len, nblocks)] += s;
-    }
-    __syncthreads();  // the rows are reused by the next block
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1905,9 +1561,6 @@ raycast_kernel(RayOrigin o, const double* __restrict__ rays, int64_t n, PassMode
   }
 }
 
-// One workgroup per accumulator entry: each thread sums its strided blocks with
-// 4 independent loads in flight, then a DPP wave sum and a 4-wave combine in
-// fixed order (deterministic for a given grid).
 // Schedule for the next pass (one workgroup): the workgroups of a pass hold
 // their slot until their slowest wave ends and durations vary ~10x (waves
 // whose points span several hulls), so launching the logical blocks in index
@@ -1975,33 +1628,7 @@ __device__ void build_order(const uint32_t* __restrict__ cost, int nb, int32_t* 
   }
 }
 
-__global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict__ partials, int nblocks, int len,
-                                                        double* __restrict__ accum, const uint32_t* __restrict__ cost,
-                                                        int32_t* __restrict__ order, int32_t* __restrict__ spill_ctr) {
-  const int j = blockIdx.x;
-  if (spill_ctr && j == 0 && threadIdx.x < 2) spill_ctr[threadIdx.x] = 0;  // the split pass is done with them
-  if (cost && j == (int)gridDim.x - 1) {  // the extra workgroup
-    build_order(cost, nblocks, order);
-    return;
-  }
-  auto at = [&](int b) { return partials[pidx(j, b, len, nblocks)]; };
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-  int b = threadIdx.x;
-  for (; b + 3 * kBlock < nblocks; b += 4 * kBlock) {
-    s0 += at(b);
-    s1 += at(b + kBlock);
-    s2 += at(b + 2 * kBlock);
-    s3 += at(b + 3 * kBlock);
-  }
-  for (; b < nblocks; b += kBlock) s0 += at(b);
-  double s = wave_sum((s0 + s1) + (s2 + s3));
-  __shared__ double sh[kBlock / 64];
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) accum[j] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
-}
-
-// Line-tiled partials (FSDF_PARTIALS_LAYOUT 2): workgroup x (16 waves) sums
+// Line-tiled partials: workgroup x (16 waves) sums
 // entries 8x .. 8x+7 over all blocks. The tile is read as a flat array of
 // 16-B pairs, fully coalesced: thread i reads pairs i + 1024 j (pair e holds
 // entries 2 (e & 3), +1 of block e >> 2), 16 loads in flight, so it always
@@ -2010,10 +1637,8 @@ __global__ __launch_bounds__(kBlock) void reduce_kernel(const double* __restrict
 // (deterministic). The schedule rebuild is a launch of its own (order_kernel).
 constexpr int kTileBlock = 1024;
 __global__ __launch_bounds__(kTileBlock) void reduce_tiles_kernel(const double* __restrict__ partials, int nblocks,
-                                                                  int len, double* __restrict__ accum,
-                                                                  int32_t* __restrict__ spill_ctr) {
+                                                                  int len, double* __restrict__ accum) {
   const int x = blockIdx.x;
-  if (spill_ctr && x == 0 && threadIdx.x < 2) spill_ctr[threadIdx.x] = 0;
   typedef double D2 __attribute__((ext_vector_type(2)));
   const D2* tile = (const D2*)(partials + (int64_t)x * nblocks * 8);
   const int np = 4 * nblocks;  // pairs in the tile
@@ -2147,16 +1772,10 @@ static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void
   const PassModel<T> m = pass_model<T>(lm, pm);
   const T* pts = (const T*)d_pts;
   const size_t lds = pass_lds_bytes(lm, false);
-  if constexpr (CULL && !RBF) {
-    if (lm.S <= 64 && out.spill.budget > 0) {
-      launch_lds(pass_kernel<T, 1, true, false, true>, nblocks, kPassBlock, lds, s, pts, n, m, out);
-      return;
-    }
-  }
   if constexpr (!RBF && FSDF_RED_IN_STAGE) {
     // one chunk per wave: the wrench rows alias the stage (pass_kernel ALIAS)
     if (lm.S <= 64 && lm.planes64 && (int64_t)nblocks * kPassBlock >= n) {
-      launch_lds(pass_kernel<T, 1, CULL, false, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
+      launch_lds(pass_kernel<T, 1, CULL, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
                  pts, n, m, out);
       return;
     }
@@ -2177,11 +1796,8 @@ static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm,
                           int nblocks, const PassOutputs& out, hipStream_t s) {
 #if FSDF_BENCH_ONLY
   const PassModel<T> m = pass_model<T>(lm, pm);
-  if (out.spill.budget > 0)
-    launch_lds(pass_kernel<T, 1, true, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false), s,
-               (const T*)d_pts, n, m, out);
-  else if (FSDF_RED_IN_STAGE && lm.planes64 && (int64_t)nblocks * kPassBlock >= n)
-    launch_lds(pass_kernel<T, 1, true, false, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
+  if (FSDF_RED_IN_STAGE && lm.planes64 && (int64_t)nblocks * kPassBlock >= n)
+    launch_lds(pass_kernel<T, 1, true, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
                (const T*)d_pts, n, m, out);
   else
     launch_lds(pass_kernel<T, 1, true, false>, nblocks, kPassBlock, pass_lds_bytes(lm, false), s, (const T*)d_pts,
@@ -2206,36 +1822,6 @@ hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const Pos
   if (precision == 64) launch_pass_p<double>(cull, lm, pm, d_pts, n, nblocks, out, s);
   else launch_pass_p<float>(cull, lm, pm, d_pts, n, nblocks, out, s);
 #endif
-  return hipGetLastError();
-}
-
-bool pass_can_split(int precision, bool cull, const LocalModel& lm, int64_t n, int nblocks) {
-  (void)precision;
-  return kPassBlock == 256 && cull && lm.R == 0 && lm.K > 0 && lm.S <= 64 && n > 0 &&
-         (int64_t)nblocks * kPassBlock >= n;  // one wave-iteration per wave
-}
-
-#ifndef FSDF_OVERFLOW_BLOCKS
-#define FSDF_OVERFLOW_BLOCKS 1024
-#endif
-#ifndef FSDF_MERGE_BLOCKS
-#define FSDF_MERGE_BLOCKS 256
-#endif
-
-template <typename T>
-static void launch_split_t(const LocalModel& lm, const PosedModel& pm, const void* d_pts, int64_t n, int nblocks,
-                           const PassOutputs& out, hipStream_t s) {
-  const PassModel<T> m = pass_model<T>(lm, pm);
-  launch_lds(overflow_kernel<T>, FSDF_OVERFLOW_BLOCKS, kBlock, pass_lds_bytes(lm, true), s, (const T*)d_pts, n, m,
-             out.spill, out.stats);
-  hipLaunchKernelGGL(merge_kernel<T>, dim3(FSDF_MERGE_BLOCKS), dim3(kPassBlock), 0, s, (const T*)d_pts, n, nblocks, m,
-                     out);
-}
-
-hipError_t launch_split(int precision, const LocalModel& lm, const PosedModel& pm, const void* d_pts, int64_t n,
-                        int nblocks, const PassOutputs& out, hipStream_t s) {
-  if (precision == 64) launch_split_t<double>(lm, pm, d_pts, n, nblocks, out, s);
-  else launch_split_t<float>(lm, pm, d_pts, n, nblocks, out, s);
   return hipGetLastError();
 }
 
@@ -2276,15 +1862,10 @@ hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const 
 }
 
 hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum, hipStream_t s,
-                         const uint32_t* cost, int32_t* order, int32_t* spill_ctr) {
-  if (FSDF_PARTIALS_LAYOUT == 2) {
-    hipLaunchKernelGGL(reduce_tiles_kernel, dim3((len + 7) / 8), dim3(kTileBlock), 0, s, partials, nblocks, len,
-                       d_accum, spill_ctr);
-    if (cost) hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kBlock), 0, s, cost, nblocks, order);
-    return hipGetLastError();
-  }
-  hipLaunchKernelGGL(reduce_kernel, dim3(len + (cost ? 1 : 0)), dim3(kBlock), 0, s, partials, nblocks, len, d_accum,
-                     cost, order, spill_ctr);
+                         const uint32_t* cost, int32_t* order) {
+  hipLaunchKernelGGL(reduce_tiles_kernel, dim3((len + 7) / 8), dim3(kTileBlock), 0, s, partials, nblocks, len,
+                     d_accum);
+  if (cost) hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kBlock), 0, s, cost, nblocks, order);
   return hipGetLastError();
 }
 

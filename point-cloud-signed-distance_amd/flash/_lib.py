@@ -72,7 +72,6 @@ _PROTOS = {
     "fsdf_profile_pass": (c_int32, [c_void_p, c_int32]),
     "fsdf_pass_time": (c_int32, [c_void_p, POINTER(c_double), POINTER(c_int64)]),
     "fsdf_pass_times": (c_int32, [c_void_p, POINTER(c_double), POINTER(c_double), POINTER(c_int64)]),
-    "fsdf_set_split_budget": (c_int32, [c_void_p, c_int32]),
     "fsdf_kernel_stats": (c_int32, [c_void_p, c_int32, c_void_p]),
     "fsdf_tree_transforms": (c_int32, [c_int32] + [c_void_p] * 13),
     "fsdf_config_gradient": (c_int32, [c_int32] + [c_void_p] * 7 + [c_int32] + [c_void_p] * 5),
@@ -202,6 +201,7 @@ class Context:
             else:
                 raise ValueError(kind)
         check(self._lib.fsdf_set_surfaces(self._ctx, arr, len(surfaces)), self._ctx, "set_surfaces")
+        self._mechanism_of = None  # the library dropped the mechanism: CostFunctor re-registers
         self.K = len(surfaces)
         self.rbf_centres = n_rbf
         self.accum_len = 1 + 6 * self.K + sum(4 * n + 4 for n in n_rbf)
@@ -295,7 +295,7 @@ class Context:
         return ms.value, n.value
 
     def pass_times(self):
-        """(summed pass-kernel ms, summed whole-pass ms incl. the split kernels,
+        """(summed pass-kernel ms, summed whole-pass ms,
         launches) since the last query."""
         k, p, n = c_double(0.0), c_double(0.0), c_int64(0)
         check(self._lib.fsdf_pass_times(self._ctx, ctypes.byref(k), ctypes.byref(p), ctypes.byref(n)), self._ctx,
@@ -332,10 +332,21 @@ class Context:
         check(self._lib.fsdf_set_deformations(self._ctx, int(n_deform), float(weight)), self._ctx, "set_deformations")
         self.n_deform = int(n_deform)
 
+    def _state_vector(self, x, who):
+        """x as contiguous f64 of exactly nq + 3 n_deform entries (the C side
+        reads that many)."""
+        x = np.ascontiguousarray(x, np.float64).reshape(-1)
+        if not hasattr(self, "nq"):
+            return x  # no mechanism: the library reports FSDF_ERR_STATE
+        n = self.nq + 3 * getattr(self, "n_deform", 0)
+        if x.size != n:
+            raise ValueError(f"{who}: x must have nq + 3 n_deform = {n} entries, got {x.size}")
+        return x
+
     def value_and_gradient(self, x):
         """(cost, ∂cost/∂x) in one native call (FK, RBF solve, pass, chain rule,
         regularizer)."""
-        x = np.ascontiguousarray(x, np.float64)
+        x = self._state_vector(x, "value_and_gradient")
         g = np.empty(self.nq + 3 * getattr(self, "n_deform", 0))
         c = c_double(0.0)
         check(self._lib.fsdf_value_and_gradient(self._ctx, ptr(x), ctypes.byref(c), ptr(g)), self._ctx,
@@ -361,12 +372,12 @@ class Context:
     def eval_state_device(self, x, d_accum: int):
         """FK, RBF solve, poses and the pass at x into the device accumulator
         (asynchronous; value_and_gradient's first half)."""
-        x = np.ascontiguousarray(x, np.float64)
+        x = self._state_vector(x, "eval_state_device")
         check(self._lib.fsdf_eval_state_device(self._ctx, ptr(x), c_void_p(d_accum)), self._ctx, "eval_state_device")
 
     def state_gradient(self, x, accum):
         """(cost, ∂cost/∂x) from an (all-reduced) host accumulator of the pass at x."""
-        x = np.ascontiguousarray(x, np.float64)
+        x = self._state_vector(x, "state_gradient")
         a = np.ascontiguousarray(accum, np.float64)
         g = np.empty(self.nq + 3 * getattr(self, "n_deform", 0))
         c = c_double(0.0)
@@ -374,14 +385,10 @@ class Context:
               "state_gradient")
         return c.value, g
 
-    def set_split_budget(self, evals: int):
-        """Hull evaluations per wave before the pass splits it (0 = never)."""
-        check(self._lib.fsdf_set_split_budget(self._ctx, int(evals)), self._ctx, "set_split_budget")
-
     STAT_NAMES = ("wave_iters", "hull_evals", "slow_waves", "lane_needs", "slow_lanes", "seed_evals",
                   "scan_waves", "full_scan_lanes", "wave_candidates", "faces_evaluated", "cyc_cull", "cyc_stage",
                   "cyc_plane", "cyc_fast", "cyc_slow", "cyc_iter", "cyc_reduce", "cyc_store", "cyc_scene",
-                  "screen_fallbacks", "screen_rejects", "walk_steps", "split_items", "split_lanes")
+                  "screen_fallbacks", "screen_rejects", "walk_steps", "reserved_22", "reserved_23")
 
     def kernel_stats(self, enable: bool):
         """enable=True: start counting; enable=False: stop, return the counters."""

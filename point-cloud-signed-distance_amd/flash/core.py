@@ -104,10 +104,14 @@ class Manipulator:
         return any(isinstance(s, InterpolatingGeometry) for s in self.surfaces)
 
     def invalidate(self):
-        """Drop device contexts (after editing surfaces / merging)."""
+        """Drop device contexts and the surface caches (after editing surfaces /
+        merging; the caches key on the surface list's identity and length)."""
         for ctx in self._engines.values():
             ctx.close()
         self._engines.clear()
+        for attr in ("_frame_cache", "_surface_plan", "_surface_body"):
+            if hasattr(self, attr):
+                delattr(self, attr)
 
 
 def num_deformations(x) -> int:

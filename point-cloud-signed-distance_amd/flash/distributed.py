@@ -94,14 +94,19 @@ class ShardedCostFunctor:
         unflatten(self.state, x)
         normalize(self.state)
         poses, self._solves = prepare_pass(self.ctx, self.manipulator, self.state.q, self.state.deformation_data)
-        self.ctx.eval_device(poses, self.accum.data_ptr(), k.data_ptr(), d.data_ptr(), g.data_ptr())
-        allreduce_accum(self.accum, self.group)
-        return k[:n].cpu().numpy(), d[:n].cpu().numpy(), g[:n].cpu().numpy()
+        with torch.cuda.stream(self.stream):
+            self.ctx.eval_device(poses, self.accum.data_ptr(), k.data_ptr(), d.data_ptr(), g.data_ptr())
+            allreduce_accum(self.accum, self.group)
+            return k[:n].cpu().numpy(), d[:n].cpu().numpy(), g[:n].cpu().numpy()
 
     def value_and_gradient(self, x):
         x = np.asarray(x, np.float64)
-        self.h_accum.copy_(self.launch(x), non_blocking=True)
-        self.torch.cuda.current_stream(self.dev).synchronize()  # the stream the copy is ordered on
+        # the pass runs on self.stream (given to the context); the all-reduce
+        # and the copy must be ordered after it whatever the caller's current
+        # stream is
+        with self.torch.cuda.stream(self.stream):
+            self.h_accum.copy_(self.launch(x), non_blocking=True)
+            self.stream.synchronize()
         acc = self.h_accum.numpy()
         if self._native:
             return self.ctx.state_gradient(x, acc)

@@ -80,3 +80,30 @@ def perturbed_configuration(manip: Manipulator, seed: int, sigma: float = 0.05):
     q_eval = q.copy()
     q_eval[rev] += rng2.normal(0.0, sigma, size=rev.sum())
     return q, q_eval
+
+
+def skin_cloud(manip: Manipulator, x, n: int, seed: int = 0, near: float = 0.85, sigma: float = 0.005,
+               pad: float = 0.3) -> np.ndarray:
+    """Synthetic cloud for scenes with RBF skins (BASELINE configs 3 and 5):
+    uniform samples of the centres' box padded by `pad`; the first `near`
+    fraction is projected onto the scene's zero set (five Newton steps
+    p <- p - d*(p) grad d*(p) through the device skin) and jittered by
+    N(0, sigma). x is the full state vector (q then deformations)."""
+    from . import core
+    from . import rbf as host_rbf
+    st = core.ManipulatorState(manip)
+    nq = manip.mechanism.num_positions
+    st.q[:] = x[:nq]
+    st.deformation_data[:] = x[nq:]
+    f = core.skin(st)
+    r = np.random.Generator(np.random.PCG64(seed))
+    solves = host_rbf.solve(manip, manip.mechanism.normalize(np.asarray(x[:nq], np.float64)), np.asarray(x[nq:]))
+    C = np.concatenate([s.centres for s in solves])
+    lo, hi = C.min(0) - pad, C.max(0) + pad
+    pts = lo + r.random((n, 3)) * (hi - lo)
+    k = int(near * n)
+    for _ in range(5):
+        d, _, g = f.evaluate(pts[:k])
+        pts[:k] -= d[:, None] * g
+    pts[:k] += r.normal(scale=sigma, size=(k, 3))
+    return pts

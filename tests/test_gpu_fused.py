@@ -154,3 +154,29 @@ def test_fused_rbf_fp32_context():
     assert np.allclose(g1, g0, rtol=1e-5, atol=1e-5 * np.abs(g0).max())
     # and close to the f64 golden gradient (f32 pass)
     assert np.allclose(g1, z["dcdx"], rtol=2e-2, atol=2e-2 * np.abs(z["dcdx"]).max())
+
+
+def test_set_surfaces_drops_the_mechanism():
+    """fsdf_set_surfaces after fsdf_set_mechanism: the mechanism's surface
+    bodies, frames and pose scratch refer to the old surface list, so the
+    library drops the mechanism and native iterations fail with
+    FSDF_ERR_STATE until it is registered again (it used to index
+    the old per-surface vectors past their end). Python-side, the context
+    forgets its registration, so CostFunctor re-registers by itself."""
+    from flash import Models, synthetic, _lib
+    from flash.gradientdescent import CostFunctor
+    m = Models.irb140()
+    big = Models.arm_grid()
+    qt, x = synthetic.perturbed_configuration(m, 5)
+    pts = synthetic.depth_cloud(m, qt, 4096, seed=6)
+    cf = CostFunctor(m, pts)
+    cf.value_and_gradient(x)
+    ctx = cf.ctx
+    # a larger surface list on the same context (more surfaces than the mechanism knows)
+    ctx.set_surfaces([("hull", (s.hull.vertices, s.hull.faces, s.hull.planes)) for s in big.surfaces])
+    assert ctx._mechanism_of is None
+    with pytest.raises(_lib.FlashNativeError) as e:
+        ctx.value_and_gradient(x)
+    assert "mechanism" in str(e.value)
+    with pytest.raises(ValueError):
+        ctx.value_and_gradient(np.zeros(3))  # short x is refused before the C call

@@ -26,24 +26,8 @@ sys.path.insert(0, os.path.join(ROOT, "point-cloud-signed-distance_amd"))
 
 def rbf_cloud(m, x, n, seed):
     """Points near the skins (projected surface samples + noise) and a uniform box."""
-    import flash
-    from flash import rbf as host_rbf
-    st = flash.ManipulatorState(m)
-    nq = m.mechanism.num_positions
-    st.q[:] = x[:nq]
-    st.deformation_data[:] = x[nq:]
-    f = flash.skin(st)
-    r = np.random.Generator(np.random.PCG64(seed))
-    solves = host_rbf.solve(m, m.mechanism.normalize(x[:nq]), x[nq:])
-    C = np.concatenate([s.centres for s in solves])
-    lo, hi = C.min(0) - 0.3, C.max(0) + 0.3
-    pts = lo + r.random((n, 3)) * (hi - lo)
-    k = int(0.85 * n)
-    for _ in range(5):
-        d, _, g = f.evaluate(pts[:k])
-        pts[:k] -= d[:, None] * g
-    pts[:k] += r.normal(scale=0.005, size=(k, 3))
-    return pts
+    from flash.synthetic import skin_cloud
+    return skin_cloud(m, x, n, seed)
 
 
 def run(name, m, x, pts, precision, reps):

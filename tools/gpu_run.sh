@@ -1,0 +1,59 @@
+#!/bin/bash
+# The one GPU-box launcher (run under gpurun). Steps run in the order given,
+# each under its own time limit; the first failure ends the call.
+#
+#   bash tools/gpu_run.sh TAG STEP [STEP ...]
+#
+# Steps (outputs under gpurun_out/TAG/):
+#   tests           pytest -m gpu (one process)
+#   bench           bench.py default line            -> bench_default.json
+#   bench:ARGS      bench.py with ARGS (commas = spaces), e.g. bench:--points,131072
+#   prof            tools/rocprof_round.sh (kernel trace + PMC passes)
+#   ab:LIBS         interleaved A/B of ab/lib_*.so builds (commas between libs)
+#   wt:LIB          per-wave timeline of a -DFSDF_WAVE_TIMES=1 build, 2^20 and 2^17 points
+#   rehearse        bench.py N=2 on one GPU (gloo, both ranks on device 0)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+TAG=$1
+shift
+O=gpurun_out/$TAG
+mkdir -p $O
+for step in "$@"; do
+  case "$step" in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        > $O/gpu_tests.log 2>&1 || { echo TESTS FAILED; tail -40 $O/gpu_tests.log; exit 1; }
+      tail -1 $O/gpu_tests.log ;;
+    bench)
+      timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_default.json 2> $O/bench_default.err \
+        || { echo BENCH FAILED; tail $O/bench_default.err; exit 1; }
+      cut -c1-400 $O/bench_default.json ;;
+    bench:*)
+      A=${step#bench:}; A=${A//,/ }; N=$(echo "$A" | tr -c 'a-zA-Z0-9' '_')
+      timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline $A > $O/bench_$N.json 2> $O/bench_$N.err \
+        || { echo BENCH FAILED; tail $O/bench_$N.err; exit 1; }
+      cut -c1-400 $O/bench_$N.json ;;
+    prof)
+      bash tools/rocprof_round.sh $TAG > $O/rocprof.log 2>&1 || { echo ROCPROF FAILED; tail $O/rocprof.log; exit 1; } ;;
+    ab:*)
+      L=${step#ab:}; L=${L//,/ }
+      timeout -k 10 900 python tools/ab_bench.py $L --rounds 3 -- --no-full-iteration > $O/ab.log 2>&1 \
+        || { tail -20 $O/ab.log; exit 1; }
+      cat $O/ab.log ;;
+    wt:*)
+      LIB=${step#wt:}
+      FLASHSDF_LIB=$PWD/$LIB timeout -k 10 200 python tools/wave_times.py --json $O/wt_1m.json > $O/wt_1m.log 2>&1 &&
+      FLASHSDF_LIB=$PWD/$LIB timeout -k 10 200 python tools/wave_times.py --points 131072 --json $O/wt_128k.json \
+        > $O/wt_128k.log 2>&1 || { echo WT FAILED; tail $O/wt_1m.log $O/wt_128k.log; exit 1; }
+      tail -3 $O/wt_1m.log $O/wt_128k.log ;;
+    rehearse)
+      export FSDF_BENCH_BACKEND=gloo FSDF_BENCH_DEVICE=0
+      timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29611 bench.py --gpus 2 --steps 10 --warmup 2 > $O/rehearse_n2.json 2> $O/rehearse_n2.err \
+        || { tail -30 $O/rehearse_n2.err; exit 1; }
+      cut -c1-600 $O/rehearse_n2.json
+      unset FSDF_BENCH_BACKEND FSDF_BENCH_DEVICE ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo done

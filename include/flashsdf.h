@@ -215,7 +215,10 @@ int fsdf_descend(fsdf_ctx* ctx, double* x, int32_t iteration_limit, double rate,
 int fsdf_create(fsdf_ctx** out, const fsdf_opts* opts);
 int fsdf_destroy(fsdf_ctx* ctx);
 const char* fsdf_last_error(const fsdf_ctx* ctx);
-/* Launch on a caller-owned hipStream_t (NULL = the context's own stream). */
+/* Launch on a caller-owned hipStream_t (NULL = the context's own stream;
+ * FSDF_HIP_NULL_STREAM = HIP's null/default stream, the handle 0 that e.g.
+ * torch's default stream reports). */
+#define FSDF_HIP_NULL_STREAM ((void*)(intptr_t)-1)
 int fsdf_set_stream(fsdf_ctx* ctx, void* hip_stream);
 int fsdf_num_hulls(const fsdf_ctx* ctx, int32_t* k_out);
 int fsdf_accum_len(const fsdf_ctx* ctx, int32_t* len_out); /* 1 + 6K + Σ(4n+4) */

@@ -289,7 +289,7 @@ extern "C" const char* fsdf_last_error(const fsdf_ctx* c) {
 
 extern "C" int fsdf_set_stream(fsdf_ctx* c, void* s) {
   if (!c) return FSDF_ERR_ARG;
-  c->stream = s ? (hipStream_t)s : c->own_stream;
+  c->stream = s == FSDF_HIP_NULL_STREAM ? (hipStream_t)0 : (s ? (hipStream_t)s : c->own_stream);
   return FSDF_OK;
 }
 
@@ -454,7 +454,9 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
       const int plane_bytes = (tsz_ == 8 && FSDF_SCREEN32) ? 32 * ((h.n_faces + 1) / 2) : h.n_faces * 4 * tsz_;
       stage_bytes = std::max(stage_bytes, plane_bytes + h.n_vertices * 4 * tsz_ + 16 * h.n_faces);
       // (+ the fp64 planes, 32 B per face, when they are staged too)
-      stage_p64 = std::max(stage_p64, plane_bytes + h.n_faces * 32 + h.n_vertices * 4 * tsz_ + 16 * h.n_faces);
+      // (rows padded: one empty 32-B row after every 8, sdf_kernels.hip PlaneRows)
+      const int p64_rows = h.n_faces > 0 ? h.n_faces + (h.n_faces - 1) / 8 : 0;
+      stage_p64 = std::max(stage_p64, plane_bytes + p64_rows * 32 + h.n_vertices * 4 * tsz_ + 16 * h.n_faces);
     }
     face_off.push_back((int32_t)(face_hull.size()));
   }

@@ -193,6 +193,12 @@ typedef int I4 __attribute__((ext_vector_type(4)));
 
 // reg: the Voronoi region of the result — 0, 1, 2 vertex a, b, c; 3, 4, 5 the
 // edge a→b, b→c, c→a (face edges 0, 1, 2); 6 the interior.
+// Branch-free: every region test is evaluated, the first that holds (the
+// classic early-return order) selects the region, and the region's one
+// division (edge parameter, or the interior's 1/(va+vb+vc)) runs once — a
+// wave whose lanes sit in different regions no longer executes every
+// region's division in turn. Each region's result is the same expression as
+// in the early-return form (oracle/flash_oracle.c), so the bits are too.
 template <typename T>
 __device__ __forceinline__ void closest_on_triangle(T px, T py, T pz, const typename Row4<T>::type& A,
                                                     const typename Row4<T>::type& B,
@@ -206,43 +212,48 @@ __device__ __forceinline__ void closest_on_triangle(T px, T py, T pz, const type
   const T apx = px - ax, apy = py - ay, apz = pz - az;
   const T d1 = mfma_(abx, apx, mfma_(aby, apy, abz * apz));
   const T d2 = mfma_(acx, apx, mfma_(acy, apy, acz * apz));
-  if (d1 <= (T)0 && d2 <= (T)0) { qx = ax; qy = ay; qz = az; reg = 0; return; }
   const T bpx = px - bx, bpy = py - by, bpz = pz - bz;
   const T d3 = mfma_(abx, bpx, mfma_(aby, bpy, abz * bpz));
   const T d4 = mfma_(acx, bpx, mfma_(acy, bpy, acz * bpz));
-  if (d3 >= (T)0 && d4 <= d3) { qx = bx; qy = by; qz = bz; reg = 1; return; }
   const T vc = mfma_(d1, d4, -(d3 * d2));
-  if (vc <= (T)0 && d1 >= (T)0 && d3 <= (T)0) {
-    const T t = d1 / (d1 - d3);
-    qx = mfma_(t, abx, ax); qy = mfma_(t, aby, ay); qz = mfma_(t, abz, az);
-    reg = 3;
-    return;
-  }
   const T cpx = px - cx, cpy = py - cy, cpz = pz - cz;
   const T d5 = mfma_(abx, cpx, mfma_(aby, cpy, abz * cpz));
   const T d6 = mfma_(acx, cpx, mfma_(acy, cpy, acz * cpz));
-  if (d6 >= (T)0 && d5 <= d6) { qx = cx; qy = cy; qz = cz; reg = 2; return; }
   const T vb = mfma_(d5, d2, -(d1 * d6));
-  if (vb <= (T)0 && d2 >= (T)0 && d6 <= (T)0) {
-    const T t = d2 / (d2 - d6);
-    qx = mfma_(t, acx, ax); qy = mfma_(t, acy, ay); qz = mfma_(t, acz, az);
-    reg = 5;
-    return;
-  }
   const T va = mfma_(d3, d6, -(d5 * d4));
   const T e43 = d4 - d3, e56 = d5 - d6;
-  if (va <= (T)0 && e43 >= (T)0 && e56 >= (T)0) {
-    const T t = e43 / (e43 + e56);
-    qx = mfma_(t, cx - bx, bx); qy = mfma_(t, cy - by, by); qz = mfma_(t, cz - bz, bz);
-    reg = 4;
-    return;
+  const bool c0 = d1 <= (T)0 && d2 <= (T)0;
+  const bool c1 = d3 >= (T)0 && d4 <= d3;
+  const bool c3 = vc <= (T)0 && d1 >= (T)0 && d3 <= (T)0;
+  const bool c2 = d6 >= (T)0 && d5 <= d6;
+  const bool c5 = vb <= (T)0 && d2 >= (T)0 && d6 <= (T)0;
+  const bool c4 = va <= (T)0 && e43 >= (T)0 && e56 >= (T)0;
+  reg = c0 ? 0 : (c1 ? 1 : (c3 ? 3 : (c2 ? 2 : (c5 ? 5 : (c4 ? 4 : 6)))));
+  // the region's quotient: edge a→b t = d1/(d1−d3), c→a t = d2/(d2−d6),
+  // b→c t = e43/(e43+e56), interior inv = 1/(va+vb+vc); vertices none
+  T num = (T)1, den = (va + vb) + vc;
+  if (reg == 3) { num = d1; den = d1 - d3; }
+  if (reg == 5) { num = d2; den = d2 - d6; }
+  if (reg == 4) { num = e43; den = e43 + e56; }
+  if (reg <= 2) { num = (T)0; den = (T)1; }
+  const T t = num / den;
+  // q = fma(s1, D1, base) (+ the interior's second term)
+  const bool edge_bc = reg == 4, edge_ca = reg == 5, inner = reg == 6;
+  const T bsx = edge_bc ? bx : ax, bsy = edge_bc ? by : ay, bsz = edge_bc ? bz : az;
+  const T dx1 = edge_bc ? cx - bx : (edge_ca ? acx : abx);
+  const T dy1 = edge_bc ? cy - by : (edge_ca ? acy : aby);
+  const T dz1 = edge_bc ? cz - bz : (edge_ca ? acz : abz);
+  const T s1 = inner ? vb * t : t;
+  const T q1x = mfma_(s1, dx1, bsx), q1y = mfma_(s1, dy1, bsy), q1z = mfma_(s1, dz1, bsz);
+  const T w_ = vc * t;
+  qx = inner ? mfma_(w_, acx, q1x) : q1x;
+  qy = inner ? mfma_(w_, acy, q1y) : q1y;
+  qz = inner ? mfma_(w_, acz, q1z) : q1z;
+  if (reg <= 2) {
+    qx = reg == 0 ? ax : (reg == 1 ? bx : cx);
+    qy = reg == 0 ? ay : (reg == 1 ? by : cy);
+    qz = reg == 0 ? az : (reg == 1 ? bz : cz);
   }
-  const T inv = (T)1 / (va + vb + vc);
-  const T v_ = vb * inv, w_ = vc * inv;
-  qx = mfma_(w_, acx, mfma_(v_, abx, ax));
-  qy = mfma_(w_, acy, mfma_(v_, aby, ay));
-  qz = mfma_(w_, acz, mfma_(v_, abz, az));
-  reg = 6;
 }
 
 // Inward edge-plane value of edge u -> w of a face with unit normal n:
@@ -447,11 +458,16 @@ constexpr int kPlaneBatch = FSDF_PLANE_BATCH;  // plane rows per LDS batch (powe
 constexpr int kWalkSteps = 24;  // descent-walk cap before the exhaustive stage C
 
 // Consecutive regions of 16-byte chunks: n0 from s0, n1 from s1, n2 from s2,
-// n3 from s3.
+// n3 from s3. PAD1 = rows of cpr chunks in region 1 padded to
+// padded_plane_rows (one empty row after every 8); the later regions follow
+// the padded region 1.
+template <int PAD1 = 0>
 __device__ __forceinline__ void stage_hull(void* __restrict__ lw, const I4* __restrict__ s0, int n0,
                                            const I4* __restrict__ s1, int n1, const I4* __restrict__ s2, int n2,
                                            const I4* __restrict__ s3 = nullptr, int n3 = 0) {
   const int P = n0, Q = P + n1, N3 = Q + n2, N = N3 + n3;
+  // chunks of padding inserted by region 1 (PAD1 = chunks per row)
+  const int pad = PAD1 ? (n1 ? (n1 / PAD1 - 1) / 8 * PAD1 : 0) : 0;
   const int lane = threadIdx.x & 63;
   I4* dst = (I4*)lw;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -466,11 +482,25 @@ __device__ __forceinline__ void stage_hull(void* __restrict__ lw, const I4* __re
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = c0 + 64 * j + lane;
-      if (c < N) dst[c] = v[j];
+      int o = c;
+      if (PAD1) o = c < P ? c : (c < Q ? c + (c - P) / (8 * PAD1) * PAD1 : c + pad);
+      if (c < N) dst[o] = v[j];
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+// Plane rows of a hull evaluation: global memory, or the wave's stage. Staged
+// fp64 rows are padded by one row after every 8 (row f at f + f/8): the
+// screen's fix-up reads the 8 rows of each lane's best batch, and without the
+// pad every batch's row q sits on the same LDS banks (a 32-B row spans 8
+// banks, 8 rows all 64), so lanes with different best batches conflicted.
+template <typename T, bool PAD>
+struct PlaneRows {
+  const typename Row4<T>::type* __restrict__ p;
+  __device__ __forceinline__ typename Row4<T>::type operator[](int f) const { return p[PAD ? f + (f >> 3) : f]; }
+};
+__host__ __device__ constexpr int padded_plane_rows(int nf) { return nf > 0 ? nf + (nf - 1) / 8 : 0; }
 
 template <typename T>
 __device__ __forceinline__ T plane_h(const typename Row4<T>::type& pl, T px, T py, T pz) {
@@ -506,9 +536,8 @@ __device__ __forceinline__ int fr_nbr(const I4& r, int e) {
 // certificate and no step. Tolerances accept rounding-level violations (a
 // false certificate moves the answer by O(tol^2)). oracle/flash_oracle.c:
 // cert_step mirrors every operation.
-template <typename T>
-__device__ __forceinline__ bool cert_step(T px, T py, T pz, int f, int reg,
-                                          const typename Row4<T>::type* __restrict__ lp,
+template <typename T, typename LP>
+__device__ __forceinline__ bool cert_step(T px, T py, T pz, int f, int reg, const LP& lp,
                                           const typename Row4<T>::type* __restrict__ lv,
                                           const I4* __restrict__ lf, T scale, int& n1, int& n2) {
   typedef typename Row4<T>::type R;
@@ -579,10 +608,10 @@ constexpr bool kStagePairs = sizeof(T) == 8 && FSDF_SCREEN32;
 constexpr int kScreenIlp = FSDF_SCREEN_ILP;  // independent 8-face batches per loop iteration  // see hull_sdf / fsdf_internal.h
 typedef float F2v __attribute__((ext_vector_type(2)));
 
-template <typename T>
+template <typename T, typename LP>
 __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0, int nf, const PassModel<T>& m,
                                                  const HullRow* __restrict__ ht, const void* __restrict__ lw,
-                                                 const typename Row4<T>::type* __restrict__ lp, bool active,
+                                                 const LP& lp, bool active,
                                                  T bound, T& hA, int& iA, bool& rejected) {
   const F4 sp = ht[k].sphere;
   const float qx = (float)(px - (T)sp[0]), qy = (float)(py - (T)sp[1]), qz = (float)(pz - (T)sp[2]);
@@ -695,12 +724,14 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   // f64 contexts also stage the fp64 planes (after the pairs) in the
   // one-chunk-per-wave pass (P64: pass_kernel ALIAS, LocalModel::planes64)
   constexpr bool kP64 = kStagePairs<T> && P64;
-  const int npl = kP64 ? nf * cpr : 0;
-  stage_hull(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0), nv * cpr,
-             m.face_rows + f0, nf);
+  const int npl = kP64 ? nf * cpr : 0;                    // chunks copied
+  const int npl_pad = kP64 ? padded_plane_rows(nf) * cpr : 0;  // chunks occupied (padded rows)
+  stage_hull<kP64 ? cpr : 0>(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0),
+                             nv * cpr, m.face_rows + f0, nf);
   tw = wt_add(0, tw);
-  const R* lp = kP64 ? (const R*)((const I4*)lw + np2) : (kStagePairs<T> ? (const R*)(m.planes + 4 * f0) : (const R*)lw);
-  const R* lv = (const R*)((const I4*)lw + np2 + npl);
+  const PlaneRows<T, kP64> lp{kP64 ? (const R*)((const I4*)lw + np2)
+                                   : (kStagePairs<T> ? (const R*)(m.planes + 4 * f0) : (const R*)lw)};
+  const R* lv = (const R*)((const I4*)lw + np2 + npl_pad);
   const I4* lf = (const I4*)(lv + nv);
   const T scale = (T)ht[k].hscale;
   auto uplane = [&](int f) -> R { return lp[f]; };

@@ -21,6 +21,9 @@ STATUS_NAMES = {1: "FSDF_ERR_ARG", 2: "FSDF_ERR_HIP", 3: "FSDF_ERR_STATE", 4: "F
                 5: "FSDF_ERR_DEGENERATE"}
 
 
+HIP_NULL_STREAM = ctypes.c_void_p(-1).value  # FSDF_HIP_NULL_STREAM ((void*)(intptr_t)-1)
+
+
 class FlashNativeError(RuntimeError):
     """Raised when the native library fails (or is absent)."""
 
@@ -174,7 +177,11 @@ class Context:
             pass
 
     def set_stream(self, stream_handle: int | None):
-        check(self._lib.fsdf_set_stream(self._ctx, c_void_p(stream_handle or 0)), self._ctx, "set_stream")
+        """Launch on this hipStream_t handle; None = the context's own stream.
+        Handle 0 is HIP's null stream (torch's default stream reports 0): it is
+        passed as FSDF_HIP_NULL_STREAM, since NULL selects the own stream."""
+        h = None if stream_handle is None else (HIP_NULL_STREAM if stream_handle == 0 else stream_handle)
+        check(self._lib.fsdf_set_stream(self._ctx, c_void_p(h)), self._ctx, "set_stream")
 
     def set_model(self, hulls):
         """hulls: sequence of (vertices [m,3] f64, faces [f,3] i32, planes [f,4] f64 or None)."""

@@ -142,7 +142,6 @@ def test_full_size_properties(m64, ctx_factory):
     out = {}
     for cull in (True, False):
         ctx = ctx_factory(m64, cull=cull)
-        ctx.set_split_budget(0)  # unsplit for the bitwise accumulator claim (the split: test_gpu_split.py)
         ctx.set_points(pts)
         out[cull] = ctx.eval(poses, per_point=True)
     (c1, a1, (k1, d1, g1)), (c0, a0, (k0, d0, g0)) = out[True], out[False]

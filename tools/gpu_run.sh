@@ -11,6 +11,7 @@
 #   prof            tools/rocprof_round.sh (kernel trace + PMC passes)
 #   ab:LIBS         interleaved A/B of ab/lib_*.so builds (commas between libs)
 #   wt:LIB          per-wave timeline of a -DFSDF_WAVE_TIMES=1 build, 2^20 and 2^17 points
+#   stats:LIBS      kernel work counters of each build (bench cloud; commas between libs)
 #   rehearse        bench.py N=2 on one GPU (gloo, both ranks on device 0)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -41,11 +42,18 @@ for step in "$@"; do
         || { tail -20 $O/ab.log; exit 1; }
       cat $O/ab.log ;;
     wt:*)
-      LIB=${step#wt:}
-      FLASHSDF_LIB=$PWD/$LIB timeout -k 10 200 python tools/wave_times.py --json $O/wt_1m.json > $O/wt_1m.log 2>&1 &&
-      FLASHSDF_LIB=$PWD/$LIB timeout -k 10 200 python tools/wave_times.py --points 131072 --json $O/wt_128k.json \
-        > $O/wt_128k.log 2>&1 || { echo WT FAILED; tail $O/wt_1m.log $O/wt_128k.log; exit 1; }
-      tail -3 $O/wt_1m.log $O/wt_128k.log ;;
+      LIB=${step#wt:}; N=$(basename $LIB .so)
+      FLASHSDF_LIB=$PWD/$LIB timeout -k 10 200 python tools/wave_times.py --json $O/wt_${N}_1m.json > $O/wt_${N}_1m.log 2>&1 &&
+      FLASHSDF_LIB=$PWD/$LIB timeout -k 10 200 python tools/wave_times.py --points 131072 --json $O/wt_${N}_128k.json \
+        > $O/wt_${N}_128k.log 2>&1 || { echo WT FAILED; tail $O/wt_${N}_1m.log $O/wt_${N}_128k.log; exit 1; }
+      echo "wt $N: $(cut -c1-200 $O/wt_${N}_1m.log)" ;;
+    stats:*)
+      L=${step#stats:}
+      for lib in ${L//,/ }; do
+        FLASHSDF_LIB=$PWD/$lib timeout -k 10 200 python tools/profile_pass.py --variants shuffled-1-64-1 --reps 3 \
+          --rounds 2 >> $O/stats.log 2>&1 || { echo STATS FAILED; tail $O/stats.log; exit 1; }
+        echo "$lib $(tail -1 $O/stats.log | cut -c1-700)"
+      done ;;
     rehearse)
       export FSDF_BENCH_BACKEND=gloo FSDF_BENCH_DEVICE=0
       timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \

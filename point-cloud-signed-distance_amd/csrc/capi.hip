@@ -103,9 +103,6 @@ struct fsdf_ctx {
   int64_t perm_cap = 0;
   float* d_chunk_ws = nullptr;       // [ceil(n/64)][4] bounding sphere per 64-point chunk
   int64_t chunk_ws_cap = 0;          // chunks
-  double* d_mbox = nullptr;          // cooperative pass mailbox [64 chunks][4] f64 (fsdf::PassOutputs)
-  int32_t* d_mbox_k = nullptr;       // [64 chunks]
-  int64_t mbox_cap = 0;              // points
   fsdf::SortScratch sort;            // per-frame sort scratch (grown only)
   double* d_staging = nullptr;       // host-source clouds land here first
   int64_t staging_cap = 0;
@@ -257,8 +254,6 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   free_model(c);
   dfree(c->d_pts);
   dfree(c->d_perm);
-  dfree(c->d_mbox);
-  dfree(c->d_mbox_k);
   dfree(c->d_chunk_ws);
   dfree(c->d_staging);
   fsdf::free_sort_scratch(c->sort);
@@ -459,9 +454,7 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
       const int plane_bytes = (tsz_ == 8 && FSDF_SCREEN32) ? 32 * ((h.n_faces + 1) / 2) : h.n_faces * 4 * tsz_;
       stage_bytes = std::max(stage_bytes, plane_bytes + h.n_vertices * 4 * tsz_ + 16 * h.n_faces);
       // (+ the fp64 planes, 32 B per face, when they are staged too)
-      // (FSDF_PAD_PLANES: rows padded, one empty 32-B row after every 8, sdf_kernels.hip PlaneRows)
-      const int p64_rows = FSDF_PAD_PLANES && h.n_faces > 0 ? h.n_faces + (h.n_faces - 1) / 8 : h.n_faces;
-      stage_p64 = std::max(stage_p64, plane_bytes + p64_rows * 32 + h.n_vertices * 4 * tsz_ + 16 * h.n_faces);
+      stage_p64 = std::max(stage_p64, plane_bytes + h.n_faces * 32 + h.n_vertices * 4 * tsz_ + 16 * h.n_faces);
     }
     face_off.push_back((int32_t)(face_hull.size()));
   }
@@ -485,7 +478,7 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
     probe.S = S;
     probe.stage_bytes = stage_p64;
     // (4 waves per SIMD: 16 waves per CU = 16·64/kPassBlock workgroups)
-    if (fsdf::pass_lds_bytes(probe, false, true, FSDF_COOP) <= (size_t)fsdf::kLdsPerCu * fsdf::kPassBlock / 1024 &&
+    if (fsdf::pass_lds_bytes(probe, false, true) <= (size_t)fsdf::kLdsPerCu * fsdf::kPassBlock / 1024 &&
         fsdf::pass_lds_bytes(probe, false) <= (size_t)fsdf::kMaxLds) {
       planes64 = 1;
       stage_bytes = stage_p64;
@@ -814,20 +807,6 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
   out.perm = d_perm;
   out.stats = c->stats_on ? c->d_stats : nullptr;
   out.chunk_ws = FSDF_CHUNK_WS && d_pts == c->d_pts && n == c->n ? c->d_chunk_ws : nullptr;  // resident cloud only
-  if (out.chunk_ws && fsdf::pass_coop(c->precision, c->cull != 0, c->lm, n, nblocks)) {
-    const int64_t slots = (n + 63) / 64 * 64;
-    if (c->mbox_cap < slots) {  // grown only; earlier passes may still read the old one
-      HIPCHECK(c, hipStreamSynchronize(c->stream));
-      dfree(c->d_mbox);
-      dfree(c->d_mbox_k);
-      c->mbox_cap = 0;
-      HIPCHECK(c, hipMalloc(&c->d_mbox, (size_t)slots * 4 * sizeof(double)));
-      HIPCHECK(c, hipMalloc(&c->d_mbox_k, (size_t)slots * sizeof(int32_t)));
-      c->mbox_cap = slots;
-    }
-    out.mbox = c->d_mbox;
-    out.mbox_k = c->d_mbox_k;
-  }
   if (schedule && n > 0) {
     if (!c->d_block_cost) {
       HIPCHECK(c, hipMalloc(&c->d_block_cost, fsdf::kMaxBlocks * sizeof(uint32_t)));

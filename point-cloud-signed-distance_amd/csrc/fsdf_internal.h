@@ -50,14 +50,6 @@ namespace fsdf {
 #define FSDF_RED_IN_STAGE 1
 #endif
 constexpr int kRedInStageMinBytes = (64 * 6 + 2) * 8 + 64 * 3 * 8;
-// Cooperative pass (sdf_kernels.hip scene_eval_coop): the waves of a
-// workgroup share hull evaluations; sizes the stage probe in fsdf_set_surfaces
-#ifndef FSDF_COOP
-#define FSDF_COOP 0  // (experimental: measured slower so far)
-#endif
-#ifndef FSDF_PAD_PLANES
-#define FSDF_PAD_PLANES 0  // padded fp64 plane stage (sdf_kernels.hip PlaneRows; measured slower)
-#endif
 #ifndef FSDF_STAGE_PLANES64
 #define FSDF_STAGE_PLANES64 1
 #endif
@@ -126,11 +118,6 @@ struct PassOutputs {
   // optional [n64/64][4] f32 bounding sphere of each 64-point chunk of the
   // resident cloud (launch_chunk_spheres at set_points; pose-independent)
   const float* chunk_ws = nullptr;
-  // cooperative pass (pass_kernel COOP): per resident point a mailbox slot
-  // (d, gradient; k) for the hull evaluations other waves ran for it
-  // ([n64][4] f64, [n64] i32; contents need no initialisation)
-  double* mbox = nullptr;
-  int32_t* mbox_k = nullptr;
 };
 
 // Surfaces whose poses ride in the pose kernel's arguments (12·64 doubles =
@@ -167,9 +154,7 @@ hipError_t launch_chunk_spheres(int precision, const void* d_pts, int64_t n, flo
 int pass_blocks(int64_t n);
 
 // dynamic LDS of one pass (raycast=false) / raycast workgroup for this model
-size_t pass_lds_bytes(const LocalModel& lm, bool raycast, bool alias = false, bool coop = false);
-// the cooperative pass applies (the caller then provides out.mbox / out.chunk_ws)
-bool pass_coop(int precision, bool cull, const LocalModel& lm, int64_t n, int nblocks);
+size_t pass_lds_bytes(const LocalModel& lm, bool raycast, bool alias = false);
 
 // Scratch of the per-frame spatial sort, owned by the context and grown only
 // (a frame makes no allocation).

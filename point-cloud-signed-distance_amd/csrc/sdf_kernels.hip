@@ -401,6 +401,11 @@ constexpr int kMaxRbfAcc = kMaxRbfAccum;
 __shared__ unsigned long long fsdf_wave_ev[kBlock / 64][3];
 __shared__ bool fsdf_wt_slow[kBlock];  // per lane: the last hull_sdf ran its search
 __shared__ unsigned long long fsdf_wave_ph[kBlock / 64][2];
+//   ph2[0]: 10-ns units in walk certificates | walk closest points | vertex-
+//           region lane-certificates | fan iterations (max over lanes, per step)
+//   ph2[1]: 10-ns units in the screen loop | screen fix-up | edge-region
+//           lane-certificates | interior-region lane-certificates
+__shared__ unsigned long long fsdf_wave_ph2[kBlock / 64][2];
 #endif
 __device__ __forceinline__ uint64_t wt_now() {
 #if FSDF_WAVE_TIMES
@@ -417,6 +422,21 @@ __device__ __forceinline__ uint64_t wt_add(int f, uint64_t t0) {
   return t1;
 #else
   return t0;
+#endif
+}
+// sub-phase clocks / counts (ph2 fields 0..7)
+__device__ __forceinline__ uint64_t wt_add2(int f, uint64_t t0) {
+#if FSDF_WAVE_TIMES
+  const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0) fsdf_wave_ph2[threadIdx.x >> 6][f >> 2] += (t1 - t0) << (16 * (f & 3));
+  return t1;
+#else
+  return t0;
+#endif
+}
+__device__ __forceinline__ void wt_count2(int f, uint64_t v) {
+#if FSDF_WAVE_TIMES
+  if ((threadIdx.x & 63) == 0) fsdf_wave_ph2[threadIdx.x >> 6][f >> 2] += v << (16 * (f & 3));
 #endif
 }
 // adds v to event field f (0..7) of this wave-iteration
@@ -458,16 +478,11 @@ constexpr int kPlaneBatch = FSDF_PLANE_BATCH;  // plane rows per LDS batch (powe
 constexpr int kWalkSteps = 24;  // descent-walk cap before the exhaustive stage C
 
 // Consecutive regions of 16-byte chunks: n0 from s0, n1 from s1, n2 from s2,
-// n3 from s3. PAD1 = rows of cpr chunks in region 1 padded to
-// padded_plane_rows (one empty row after every 8); the later regions follow
-// the padded region 1.
-template <int PAD1 = 0>
+// n3 from s3.
 __device__ __forceinline__ void stage_hull(void* __restrict__ lw, const I4* __restrict__ s0, int n0,
                                            const I4* __restrict__ s1, int n1, const I4* __restrict__ s2, int n2,
                                            const I4* __restrict__ s3 = nullptr, int n3 = 0) {
   const int P = n0, Q = P + n1, N3 = Q + n2, N = N3 + n3;
-  // chunks of padding inserted by region 1 (PAD1 = chunks per row)
-  const int pad = PAD1 ? (n1 ? (n1 / PAD1 - 1) / 8 * PAD1 : 0) : 0;
   const int lane = threadIdx.x & 63;
   I4* dst = (I4*)lw;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -482,25 +497,11 @@ __device__ __forceinline__ void stage_hull(void* __restrict__ lw, const I4* __re
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = c0 + 64 * j + lane;
-      int o = c;
-      if (PAD1) o = c < P ? c : (c < Q ? c + (c - P) / (8 * PAD1) * PAD1 : c + pad);
-      if (c < N) dst[o] = v[j];
+      if (c < N) dst[c] = v[j];
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-
-// Plane rows of a hull evaluation: global memory, or the wave's stage. PAD:
-// staged fp64 rows padded by one row after every 8 (row f at f + f/8), so the
-// screen fix-up's 8 rows of different lanes' best batches fall on different
-// LDS banks — measured 6.5 % SLOWER on M64 (the stage grew 384 B per wave;
-// r03d A/B), so the product kernel stages unpadded (PAD = false).
-template <typename T, bool PAD>
-struct PlaneRows {
-  const typename Row4<T>::type* __restrict__ p;
-  __device__ __forceinline__ typename Row4<T>::type operator[](int f) const { return p[PAD ? f + (f >> 3) : f]; }
-};
-__host__ __device__ constexpr int padded_plane_rows(int nf) { return nf > 0 ? nf + (nf - 1) / 8 : 0; }
 
 template <typename T>
 __device__ __forceinline__ T plane_h(const typename Row4<T>::type& pl, T px, T py, T pz) {
@@ -539,7 +540,8 @@ __device__ __forceinline__ int fr_nbr(const I4& r, int e) {
 template <typename T, typename LP>
 __device__ __forceinline__ bool cert_step(T px, T py, T pz, int f, int reg, const LP& lp,
                                           const typename Row4<T>::type* __restrict__ lv,
-                                          const I4* __restrict__ lf, T scale, int& n1, int& n2) {
+                                          const I4* __restrict__ lf, T scale, int& n1, int& n2,
+                                          int* __restrict__ fan_it = nullptr) {
   typedef typename Row4<T>::type R;
   n1 = -1;
   n2 = -1;
@@ -567,6 +569,7 @@ __device__ __forceinline__ bool cert_step(T px, T py, T pz, int f, int reg, cons
   int g = f, j = reg;
   I4 r = fr;
   for (int it = 0; it < 32; ++it) {
+    if (fan_it) *fan_it = it + 1;
     const int g2 = fr_nbr(r, j);  // across edge v -> u
     const R Un = lv[fr_vert(r, j == 2 ? 0 : j + 1)];
     const T dot = mfma_(wx, Un[0] - V[0], mfma_(wy, Un[1] - V[1], wz * (Un[2] - V[2])));
@@ -651,6 +654,7 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
   // holds for every lane that needs the hull, the scan stops (d = +inf).
   const float bf = (float)bound;
   const float thr = bf + E2 + 2.5e-7f * fabsf(bf);
+  const uint64_t tw_screen = wt_now();
   rejected = false;
   int i0 = 0;
   // the first 16 faces get a rejection test of their own: a hull that cannot
@@ -675,6 +679,7 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
   for (; i0 < np; i0 += 4) update(batch_max(i0, i0 + 4 > np), i0);
   if (!__any(active && !(b1 > thr))) { rejected = true; return true; }
   // exact fp64 first-index argmax over the best batch's faces
+  const uint64_t tw_fix = wt_add2(4, tw_screen);
   const int fb = 2 * ib;
   hA = -tinf<T>();
   iA = 0;
@@ -685,6 +690,7 @@ __device__ __forceinline__ bool screen_plane_max(T px, T py, T pz, int k, int f0
     if (h > hA) { hA = h; iA = f; }
   }
   const bool safe = b2 < b1 - E2;
+  wt_add2(5, tw_fix);
   return !__any(active && !safe);
 }
 
@@ -724,15 +730,12 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   // f64 contexts also stage the fp64 planes (after the pairs) in the
   // one-chunk-per-wave pass (P64: pass_kernel ALIAS, LocalModel::planes64)
   constexpr bool kP64 = kStagePairs<T> && P64;
-  constexpr bool kPad = kP64 && FSDF_PAD_PLANES;
-  const int npl = kP64 ? nf * cpr : 0;                    // chunks copied
-  const int npl_pad = kPad ? padded_plane_rows(nf) * cpr : npl;  // chunks occupied
-  stage_hull<kPad ? cpr : 0>(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0),
-                             nv * cpr, m.face_rows + f0, nf);
+  const int npl = kP64 ? nf * cpr : 0;
+  stage_hull(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0), nv * cpr,
+             m.face_rows + f0, nf);
   tw = wt_add(0, tw);
-  const PlaneRows<T, kPad> lp{kP64 ? (const R*)((const I4*)lw + np2)
-                                   : (kStagePairs<T> ? (const R*)(m.planes + 4 * f0) : (const R*)lw)};
-  const R* lv = (const R*)((const I4*)lw + np2 + npl_pad);
+  const R* lp = kP64 ? (const R*)((const I4*)lw + np2) : (kStagePairs<T> ? (const R*)(m.planes + 4 * f0) : (const R*)lw);
+  const R* lv = (const R*)((const I4*)lw + np2 + npl);
   const I4* lf = (const I4*)(lv + nv);
   const T scale = (T)ht[k].hscale;
   auto uplane = [&](int f) -> R { return lp[f]; };
@@ -851,9 +854,29 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   for (int step = 0; step < kWalkSteps && __any(walking); ++step) {
     if (count_events(stats) && lane_id() == 0) atomicAdd(stats + 21, 1ull);
     wt_count(3, 1);
+#if FSDF_WAVE_TIMES
+    const uint64_t tw_c = wt_now();
+    int fan_it = 0;
+    wt_count2(2, __builtin_popcountll(__ballot(walking && cr <= 2)));
+    wt_count2(6, __builtin_popcountll(__ballot(walking && cr >= 3 && cr <= 5)));
+    wt_count2(7, __builtin_popcountll(__ballot(walking && cr == 6)));
+    int* fan_p = &fan_it;
+#else
+    int* fan_p = nullptr;
+#endif
+    int n1 = -1, n2 = -1;
+    const bool certified = walking && cert_step<T>(px, py, pz, cf, cr, lp, lv, lf, scale, n1, n2, fan_p);
+#if FSDF_WAVE_TIMES
+    {
+      int fm = fan_it;
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) fm = max(fm, __shfl_xor(fm, off, 64));
+      wt_count2(3, fm);
+    }
+    const uint64_t tw_s = wt_add2(0, tw_c);
+#endif
     if (walking) {
-      int n1, n2;
-      if (cert_step<T>(px, py, pz, cf, cr, lp, lv, lf, scale, n1, n2)) {
+      if (certified) {
         todo = false;
         walking = false;
       } else {
@@ -875,6 +898,9 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
         walking = moved;
       }
     }
+#if FSDF_WAVE_TIMES
+    wt_add2(1, tw_s);
+#endif
   }
   wt_add(7, tw_walk);  // (the descent walk: certificates and steps)
   if (__any(todo)) {
@@ -1307,288 +1333,6 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   if (count_events(stats) && lane == 0) atomicAdd(stats + 0, 1ull);
 }
 
-// ---------------------------------------------------------------------------
-// Cooperative scene evaluation (pass_kernel COOP: hull-only, <= 64 surfaces,
-// one 64-point chunk per wave, fp64 planes staged). A workgroup holds its CU
-// slot until its slowest wave ends, and a wave among many hulls evaluates
-// them one after another (10 evaluations, ~100 us, on the bench cloud while
-// its neighbours finish in ~15). Here every wave publishes its evaluation list
-// (seeds first, then the other candidates) in LDS; a wave whose own list is
-// exhausted takes tasks from the front of another wave's list (one hull for
-// that wave's 64 points) until no list has any left.
-//   * bounds: each wave publishes, per lane, an upper bound of its lane's
-//     distance (min(ub, best), rounded up to f32, only ever lowered): a
-//     helper's need test and hull_sdf bound use it — any upper bound of d*
-//     is exact-safe there (a hull it rejects cannot win).
-//   * results: a helper's exact per-lane distances that may win (d <= bound)
-//     go to a global mailbox slot of that point (d, gradient, k), merged
-//     under a per-wave LDS lock with the first-index tie rule; the owner,
-//     once its list is exhausted and no helper is still working on it, merges
-//     the mailbox into its registers with the same rule. min with first-index
-//     ties is order-independent, so d*, k*, ∇d* are those of the serial
-//     evaluation bit for bit, whoever evaluated what.
-// ---------------------------------------------------------------------------
-#ifndef FSDF_COOP_STEAL
-#define FSDF_COOP_STEAL 1  // 0: the cooperative kernel's structure without stealing (A/B)
-#endif
-constexpr int kPassWaves = kPassBlock / 64;
-struct CoopLds {
-  int qlen[kPassWaves];      // published evaluation list length (0 until published)
-  int qhead[kPassWaves];     // next list entry to take (atomic)
-  int pending[kPassWaves];   // helpers holding a task of this wave (atomic)
-  int lock[kPassWaves];      // mailbox merge lock
-  uint32_t mlo[kPassWaves], mhi[kPassWaves];  // mailbox lanes holding a result
-  uint32_t tb[kPassWaves][64];                // f32 upper bound per lane, order-preserving key
-  uint8_t queue[kPassWaves][64];              // hull indices
-};
-__device__ __forceinline__ uint32_t f32_key(float f) {
-  const uint32_t b = __float_as_uint(f);
-  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-}
-__device__ __forceinline__ float key_f32(uint32_t k) {
-  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
-}
-// smallest f32 >= d (d finite or +inf)
-__device__ __forceinline__ float f32_up(double d) {
-  float f = (float)d;
-  if ((double)f < d) {  // the next f32 towards +inf
-    const uint32_t b = __float_as_uint(f);
-    f = f == 0.0f ? __uint_as_float(1u) : __uint_as_float(f > 0.0f ? b + 1 : b - 1);
-  }
-  return f;
-}
-__device__ __forceinline__ void coop_init(CoopLds* co) {
-  for (int i = threadIdx.x; i < kPassWaves * 64; i += blockDim.x) co->tb[i >> 6][i & 63] = f32_key(__builtin_huge_valf());
-  if (threadIdx.x < kPassWaves) {
-    const int w = threadIdx.x;
-    co->qlen[w] = 0; co->qhead[w] = 0; co->pending[w] = 0; co->lock[w] = 0; co->mlo[w] = 0; co->mhi[w] = 0;
-  }
-}
-
-// chunk_base(w): first resident point of wave w's chunk (base >= n: none)
-template <typename T, typename CB>
-__device__ __forceinline__ void scene_eval_coop(T px, T py, T pz, bool valid, const PassModel<T>& m,
-                                                const HullRow* __restrict__ ht, float smax, T* __restrict__ lw,
-                                                unsigned long long* __restrict__ stats, T& best, int& bk, T& gx,
-                                                T& gy, T& gz, const F4* __restrict__ cws, CoopLds* __restrict__ co,
-                                                const T* __restrict__ pts, int64_t n, double* __restrict__ mbox,
-                                                int32_t* __restrict__ mbox_k, CB chunk_base) {
-  const int K = m.K;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int64_t base = chunk_base(wave);
-  uint64_t tw = wt_now();
-  float ub2 = __builtin_huge_valf(), lb_min = __builtin_huge_valf();
-  int kseed = 0;
-  const float pxf = (float)px, pyf = (float)py, pzf = (float)pz;
-  uint64_t cand = 0;
-  int cnt = 0;
-  if (base < n) {
-    // the wave's culling, as scene_eval's
-    const F4 v = *cws;
-    const float cwx = v[0], cwy = v[1], cwz = v[2], rw = v[3];
-    float Dk = __builtin_huge_valf(), ubw = __builtin_huge_valf();
-    if (lane < K) {
-      const F4 sp = ht[lane].sphere;
-      const float dx = cwx - sp[0], dy = cwy - sp[1], dz = cwz - sp[2];
-      Dk = __builtin_sqrtf(__builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz)));
-      ubw = Dk + rw;
-    }
-    ubw = wave_minmax<false>(ubw);
-    const float mrgw = 1e-5f * (1.0f + fabsf(cwx) + fabsf(cwy) + fabsf(cwz) + smax + 4.0f * rw + 2.0f * ubw);
-    {
-      const HullRow& h = ht[lane < K ? lane : 0];
-      cand = __ballot(lane < K && Dk - rw - h.sphere[3] <= ubw + mrgw && box_within(h, cwx, cwy, cwz, ubw + mrgw + rw));
-    }
-    if (count_events(stats) && lane == 0) atomicAdd(stats + 8, (unsigned long long)__builtin_popcountll(cand));
-    for (uint64_t cm = cand; cm;) {
-      const int k = __builtin_ctzll(cm);
-      cm &= cm - 1;
-      const F4 sp = ht[k].sphere;
-      const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
-      const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
-      ub2 = fminf(ub2, dist2);
-      const float lb = fmaxf(__builtin_sqrtf(dist2) - sp[3], box_lower(ht[k], pxf, pyf, pzf));
-      if (lb < lb_min) { lb_min = lb; kseed = k; }
-    }
-  }
-  const float ub = __builtin_sqrtf(ub2);
-  const float mrg = 1e-5f * (1.0f + fabsf(pxf) + fabsf(pyf) + fabsf(pzf) + smax + 2.0f * ub);
-  best = tinf<T>();
-  bk = 0x7fffffff;
-  gx = (T)0; gy = (T)0; gz = (T)0;
-  uint64_t cmask = 0;  // this wave's other candidates (after the seeds), evaluated by itself
-  if (base < n) {
-    // publish: the lanes' bound, then the seed list (distinct seeds in
-    // first-lane order) — the tasks other waves may take
-    // ub (f32 arithmetic) plus its rounding margin bounds the exact min_k |p - c_k| >= d*
-    if (valid) atomicMin(&co->tb[wave][lane], f32_key(f32_up((double)ub + (double)mrg)));
-    uint64_t done = 0;
-    for (uint64_t pend = __ballot(valid); pend;) {
-      const int k = __builtin_amdgcn_readfirstlane(__shfl(kseed, __builtin_ctzll(pend), 64));
-      pend &= ~__ballot(valid && kseed == k);
-      done |= 1ull << k;
-      if (lane == 0) co->queue[wave][cnt] = (uint8_t)k;
-      ++cnt;
-    }
-    cmask = cand & ~done;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_store(&co->qlen[wave], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-  tw = wt_add(4, tw);
-  wt_count(6, __builtin_popcountll(cand));
-  // the helpers' results for this wave's lanes, once none is still working on one
-  auto merge_mailbox = [&]() {
-    if (lane == 0)
-      while (__hip_atomic_load(&co->pending[wave], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
-        __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const uint64_t have = (uint64_t)__hip_atomic_load(&co->mlo[wave], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) |
-                          ((uint64_t)__hip_atomic_load(&co->mhi[wave], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) << 32);
-    if (valid && ((have >> lane) & 1)) {
-      const int64_t i = base + lane;
-      const double dm = __builtin_nontemporal_load(mbox + 4 * i);
-      const int km = __builtin_nontemporal_load(mbox_k + i);
-      if ((T)dm < best || ((T)dm == best && km < bk)) {
-        best = (T)dm;
-        bk = km;
-        gx = (T)__builtin_nontemporal_load(mbox + 4 * i + 1);
-        gy = (T)__builtin_nontemporal_load(mbox + 4 * i + 2);
-        gz = (T)__builtin_nontemporal_load(mbox + 4 * i + 3);
-      }
-    }
-  };
-  // ONE evaluation site (hull_sdf is large). States: 0 this wave's seeds,
-  // 1 other waves' seeds, 2 this wave's remaining candidates in index order
-  // with its exact bests (the helpers' results merged first), as scene_eval's
-  // phase C.
-  int state = cnt > 0 ? 0 : 1;
-  for (;;) {
-    int v = wave, t = -1, k = -1;
-    bool own = true;
-    if (state == 0) {
-      if (lane == 0) t = atomicAdd(&co->qhead[wave], 1);
-      t = __builtin_amdgcn_readfirstlane(__shfl(t, 0, 64));
-      if (t < cnt) k = __builtin_amdgcn_readfirstlane((int)co->queue[wave][t]);
-      else state = 1;
-    }
-    if (state == 1) {
-      // the wave with the most seeds left (another's; approximate read)
-      int rem = 0;
-      if (FSDF_COOP_STEAL && lane < kPassWaves && lane != wave)
-        rem = __hip_atomic_load(&co->qlen[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) -
-              __hip_atomic_load(&co->qhead[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      v = -1;
-      int most = 0;
-#pragma unroll
-      for (int w = 0; w < kPassWaves; ++w) {
-        const int r = __builtin_amdgcn_readlane(rem, w);
-        if (r > most) { most = r; v = w; }
-      }
-      if (v < 0) {
-        if (base < n) merge_mailbox();
-        state = 2;
-        v = wave;
-      } else {
-        int got = -1;
-        if (lane == 0) {
-          atomicAdd(&co->pending[v], 1);  // registered before taking: the owner waits for it
-          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-          const int tt = atomicAdd(&co->qhead[v], 1);
-          if (tt < __hip_atomic_load(&co->qlen[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) got = tt;
-          else atomicSub(&co->pending[v], 1);
-        }
-        t = __builtin_amdgcn_readfirstlane(__shfl(got, 0, 64));
-        if (t < 0) continue;
-        own = false;
-        k = __builtin_amdgcn_readfirstlane((int)co->queue[v][t]);
-      }
-    }
-    if (state == 2) {
-      // the next candidate some lane needs (exact bests: the helpers' merged)
-      while (cmask) {
-        const int kk = __builtin_ctzll(cmask);
-        cmask &= cmask - 1;
-        if (__any(valid && needs_at(ht[kk], pxf, pyf, pzf, fminf(ub, (float)best) + mrg))) { k = kk; break; }
-      }
-      if (k < 0) break;
-    }
-    // the task's points: reloaded from global memory every task (own ones
-    // too: the caller's px, py, pz are not kept live across hull_sdf — the
-    // kernel sits at the 128-VGPR budget of 4 waves per SIMD)
-    T bound = best;
-    float thr = fminf(ub, (float)best) + mrg;
-    const int64_t vi = chunk_base(v) + lane;
-    const bool tvalid = vi < n;
-    int64_t vii = tvalid ? vi : n - 1;
-    asm volatile("" : "+v"(vii));  // a fresh load (no value kept live from the prologue)
-    const T tx = pts[3 * vii + 0], ty = pts[3 * vii + 1], tz = pts[3 * vii + 2];
-    const float txf = (float)tx, tyf = (float)ty, tzf = (float)tz;
-    if (!own) {
-      const float tbv = key_f32(__hip_atomic_load(&co->tb[v][lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-      bound = (T)tbv;
-      thr = tbv + 1e-5f * (1.0f + fabsf(txf) + fabsf(tyf) + fabsf(tzf) + smax + 2.0f * tbv);
-    }
-    const bool need = tvalid && needs_at(ht[k], txf, tyf, tzf, thr);
-    if (__any(need)) {
-      wt_count(0, 1);
-      if (!own) wt_count(4, 1);  // (event field reused: stolen evaluations)
-      T dk, hx, hy, hz;
-      hull_sdf<T, true>(tx, ty, tz, k, m, ht, need, bound, dk, hx, hy, hz, lw, stats);
-      if (count_events(stats)) {
-        const uint64_t nm = __ballot(need);
-        if (lane == 0) {
-          atomicAdd(stats + 1, 1ull);
-          atomicAdd(stats + 3, (unsigned long long)__builtin_popcountll(nm));
-          if (!own) atomicAdd(stats + 22, 1ull);
-        }
-      }
-      if (own) {
-        if (need && (dk < best || (dk == best && k < bk))) { best = dk; bk = k; gx = hx; gy = hy; gz = hz; }
-        if (need && state == 0) atomicMin(&co->tb[wave][lane], f32_key(f32_up((double)best)));
-      } else {
-        // dk <= bound: exact (a skipped or rejected evaluation returns > bound)
-        const bool win = need && dk <= bound;
-        const uint64_t wm = __ballot(win);
-        if (wm) {
-          if (lane == 0)
-            while (atomicCAS(&co->lock[v], 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-          const uint64_t have = (uint64_t)__hip_atomic_load(&co->mlo[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) |
-                                ((uint64_t)__hip_atomic_load(&co->mhi[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) << 32);
-          bool take = win;
-          if (win && ((have >> lane) & 1)) {
-            const double dm = __builtin_nontemporal_load(mbox + 4 * vi);
-            const int km = __builtin_nontemporal_load(mbox_k + vi);
-            take = (double)dk < dm || ((double)dk == dm && k < km);
-          }
-          if (take) {
-            mbox[4 * vi + 0] = (double)dk;
-            mbox[4 * vi + 1] = (double)hx;
-            mbox[4 * vi + 2] = (double)hy;
-            mbox[4 * vi + 3] = (double)hz;
-            mbox_k[vi] = k;
-            atomicMin(&co->tb[v][lane], f32_key(f32_up((double)dk)));
-          }
-          const uint64_t nh = have | wm;
-          if (lane == 0) {
-            __hip_atomic_store(&co->mlo[v], (uint32_t)nh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(&co->mhi[v], (uint32_t)(nh >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // mailbox stores complete before the release
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          if (lane == 0) __hip_atomic_store(&co->lock[v], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      }
-    }
-    if (!own) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) atomicSub(&co->pending[v], 1);
-    }
-  }
-  if (count_events(stats) && lane == 0 && base < n) atomicAdd(stats + 0, 1ull);
-}
-
 // Per-chunk epilogue (pass and merge kernels): this wave's contributions
 //   c += d^2;  F_k += 2 d g;  M_k += 2 d (p x g)   (RBF skins: adjoint sums)
 // segmented by k* (ballot loop + DPP wave sums) into the LDS rows owned by
@@ -1701,19 +1445,10 @@ extern __shared__ __attribute__((aligned(16))) char fsdf_lds[];
 // hull stage, which is free once the chunk's scene evaluation is done — 12 KiB
 // less LDS per workgroup, spent on staging the fp64 planes with the hull
 // (hull_sdf P64) at the same occupancy.
-// COOP (with ALIAS): the waves of a workgroup share hull evaluations
-// (scene_eval_coop); with FSDF_COOP_STRIDED the workgroup's 4 chunks are
-// strided over the cloud (chunk w·B + b of the B workgroups), so the chunks
-// among many hulls — neighbours in the spatial order — land in different
-// workgroups, each with light chunks whose waves help.
-#ifndef FSDF_COOP_STRIDED
-#define FSDF_COOP_STRIDED 1
-#endif
-template <typename T, int SLOTS, bool CULL, bool RBF, bool ALIAS = false, bool COOP = false>
+template <typename T, int SLOTS, bool CULL, bool RBF, bool ALIAS = false>
 __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)) void pass_kernel(
     const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out) {
   static_assert(!ALIAS || (SLOTS == 1 && !RBF), "aliased wrench rows: hull-only, <= 64 surfaces");
-  static_assert(!COOP || (ALIAS && CULL && sizeof(T) == 8), "cooperative waves: the aliased f64 culled pass");
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   // All LDS is one dynamic region (16-byte aligned carve, see pass_lds_bytes):
@@ -1749,63 +1484,14 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
   // logical block of this launch slot (cost-ordered schedule, see PassOutputs)
   const int lb = out.order ? __builtin_amdgcn_readfirstlane(out.order[blockIdx.x]) : (int)blockIdx.x;
   // (ALIAS: a wave past the cloud's end never evaluates; its rows are zeroed now)
-  if (ALIAS && !COOP && (int64_t)lb * kPassBlock + wave * 64 >= n) zero_rows();
+  if (ALIAS && (int64_t)lb * kPassBlock + wave * 64 >= n) zero_rows();
   const uint64_t t_block = out.cost ? __builtin_amdgcn_s_memrealtime() : 0;
 #if FSDF_WAVE_TIMES
   const uint64_t t_block0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  CoopLds* co = (CoopLds*)((char*)(ht + m.K + 1) + kPassWaves * m.stage_bytes);
-  if (COOP) coop_init(co);  // ordered before every use by load_hull_table's barrier
   const float smax = load_hull_table(m, ht);
-  if constexpr (COOP) {
-    const int nb = (int)gridDim.x;
-    auto chunk_base = [&](int w) -> int64_t {
-      return FSDF_COOP_STRIDED ? ((int64_t)w * nb + lb) * 64 : (int64_t)lb * kPassBlock + w * 64;
-    };
-    const int64_t base = chunk_base(wave);
-    const int64_t i = base + lane;
-    const bool valid = i < n;
-    const int64_t ii = valid ? i : n - 1;
-    const T px = pts[3 * ii + 0], py = pts[3 * ii + 1], pz = pts[3 * ii + 2];
-#if FSDF_WAVE_TIMES
-    const uint64_t w_t0 = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0)
-      fsdf_wave_ev[wave][0] = fsdf_wave_ev[wave][1] = fsdf_wave_ev[wave][2] = fsdf_wave_ph[wave][0] =
-          fsdf_wave_ph[wave][1] = 0;
-#endif
-    T best, gx, gy, gz;
-    int bk;
-    const F4* cws = (const F4*)out.chunk_ws + (base < n ? (base >> 6) : 0);
-    scene_eval_coop<T>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz, cws, co, pts, n,
-                       out.mbox, out.mbox_k, chunk_base);
-    if (!valid) bk = 0;
-    // the points again for the epilogue (not kept live across the evaluations)
-    int64_t ij = ii;
-    asm volatile("" : "+v"(ij));
-    const T qx = pts[3 * ij + 0], qy = pts[3 * ij + 1], qz = pts[3 * ij + 2];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    zero_rows();  // the stage is free: this wave's rows go there
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (base < n) {
-      T* tstage = (T*)((char*)stage + kRedStride * 8);  // gradient transpose after the rows
-      emit_chunk<T, SLOTS, RBF>(qx, qy, qz, valid, best, bk, gx, gy, gz, i, base, n, m, out, acc_row, cost_acc,
-                                rbf_wave, tstage, stage_cap);
-#if FSDF_WAVE_TIMES
-      if (out.stats && lane == 0 && base < (int64_t)64 * 4 * kMaxBlocks) {
-        const int64_t wv = base / 64;
-        out.stats[32 + 2 * wv] = w_t0;
-        out.stats[33 + 2 * wv] = __builtin_amdgcn_s_memrealtime();
-        out.stats[32 + 8 * kMaxBlocks + 2 * wv] = fsdf_wave_ev[wave][0];
-        out.stats[33 + 8 * kMaxBlocks + 2 * wv] = fsdf_wave_ev[wave][1];
-        out.stats[32 + 18 * kMaxBlocks + 2 * wv] = fsdf_wave_ph[wave][0];
-        out.stats[33 + 18 * kMaxBlocks + 2 * wv] = fsdf_wave_ph[wave][1];
-        out.stats[32 + 26 * kMaxBlocks + wv] = fsdf_wave_ev[wave][2];
-      }
-#endif
-    }
-  }
   const int64_t stride = (int64_t)gridDim.x * kPassBlock;
-  for (int64_t base = (int64_t)lb * kPassBlock + wave * 64; !COOP && base < n; base += stride) {
+  for (int64_t base = (int64_t)lb * kPassBlock + wave * 64; base < n; base += stride) {
     const int64_t i = base + lane;
     const bool valid = i < n;
     const int64_t ii = valid ? i : n - 1;
@@ -1814,7 +1500,7 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
     const uint64_t w_t0 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0)
       fsdf_wave_ev[wave][0] = fsdf_wave_ev[wave][1] = fsdf_wave_ev[wave][2] = fsdf_wave_ph[wave][0] =
-          fsdf_wave_ph[wave][1] = 0;
+          fsdf_wave_ph[wave][1] = fsdf_wave_ph2[wave][0] = fsdf_wave_ph2[wave][1] = 0;
 #endif
 
     T best, gx, gy, gz;
@@ -1843,6 +1529,10 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
       out.stats[32 + 18 * kMaxBlocks + 2 * wv] = fsdf_wave_ph[wave][0];
       out.stats[33 + 18 * kMaxBlocks + 2 * wv] = fsdf_wave_ph[wave][1];
       out.stats[32 + 26 * kMaxBlocks + wv] = fsdf_wave_ev[wave][2];
+      if (wv < kMaxBlocks) {
+        out.stats[32 + 30 * kMaxBlocks + 2 * wv] = fsdf_wave_ph2[wave][0];
+        out.stats[33 + 30 * kMaxBlocks + 2 * wv] = fsdf_wave_ph2[wave][1];
+      }
     }
 #endif
   }
@@ -2062,11 +1752,6 @@ __global__ void to_f32_kernel(const double* __restrict__ src, float* __restrict_
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
-bool pass_coop(int precision, bool cull, const LocalModel& lm, int64_t n, int nblocks) {
-  return FSDF_COOP && FSDF_RED_IN_STAGE && precision == 64 && cull && lm.R == 0 && lm.S <= 64 && lm.planes64 &&
-         n > 0 && (int64_t)nblocks * kPassBlock >= n;
-}
-
 int pass_blocks(int64_t n) {
   int64_t b = (n + kPassBlock - 1) / kPassBlock;
   if (b < 1) b = 1;
@@ -2128,10 +1813,9 @@ static PassModel<T> pass_model(const LocalModel& lm, const PosedModel& pm) {
 
 static int slots_for(int S) { return S <= 64 ? 1 : (S <= 128 ? 2 : 4); }
 
-size_t pass_lds_bytes(const LocalModel& lm, bool raycast, bool alias, bool coop) {
+size_t pass_lds_bytes(const LocalModel& lm, bool raycast, bool alias) {
   const size_t waves = (size_t)(raycast ? kBlock : kPassBlock) / 64;
   const size_t stage = waves * (size_t)lm.stage_bytes + (size_t)(lm.K + 1) * sizeof(HullRow);
-  if (alias && coop) return stage + sizeof(CoopLds);
   if (raycast || alias) return stage;
   const size_t red = waves * (size_t)(slots_for(lm.S) * 64 * 6 + 2) * sizeof(double);
   const size_t rbf = lm.R > 0 ? waves * kMaxRbfAcc * sizeof(double) : 0;
@@ -2150,14 +1834,6 @@ static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void
   const PassModel<T> m = pass_model<T>(lm, pm);
   const T* pts = (const T*)d_pts;
   const size_t lds = pass_lds_bytes(lm, false);
-  if constexpr (!RBF && FSDF_RED_IN_STAGE && CULL && sizeof(T) == 8) {
-    if (lm.S <= 64 && lm.planes64 && (int64_t)nblocks * kPassBlock >= n && out.mbox && out.chunk_ws) {
-      // cooperative waves (the mailbox is sized by the caller for this grid)
-      launch_lds(pass_kernel<T, 1, true, false, true, true>, nblocks, kPassBlock,
-                 pass_lds_bytes(lm, false, true, true), s, pts, n, m, out);
-      return;
-    }
-  }
   if constexpr (!RBF && FSDF_RED_IN_STAGE) {
     // one chunk per wave: the wrench rows alias the stage (pass_kernel ALIAS)
     if (lm.S <= 64 && lm.planes64 && (int64_t)nblocks * kPassBlock >= n) {
@@ -2182,10 +1858,7 @@ static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm,
                           int nblocks, const PassOutputs& out, hipStream_t s) {
 #if FSDF_BENCH_ONLY
   const PassModel<T> m = pass_model<T>(lm, pm);
-  if (FSDF_RED_IN_STAGE && lm.planes64 && (int64_t)nblocks * kPassBlock >= n && out.mbox && out.chunk_ws)
-    launch_lds(pass_kernel<T, 1, true, false, true, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true, true),
-               s, (const T*)d_pts, n, m, out);
-  else if (FSDF_RED_IN_STAGE && lm.planes64 && (int64_t)nblocks * kPassBlock >= n)
+  if (FSDF_RED_IN_STAGE && lm.planes64 && (int64_t)nblocks * kPassBlock >= n)
     launch_lds(pass_kernel<T, 1, true, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
                (const T*)d_pts, n, m, out);
   else

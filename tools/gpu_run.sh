@@ -12,6 +12,8 @@
 #   ab:LIBS         interleaved A/B of ab/lib_*.so builds (commas between libs)
 #   wt:LIB          per-wave timeline of a -DFSDF_WAVE_TIMES=1 build, 2^20 and 2^17 points
 #   stats:LIBS      kernel work counters of each build (bench cloud; commas between libs)
+#   abcheck:LIBS    bit-for-bit agreement of builds with the first (tools/ab_check.py)
+#   lds:LIBS        PMC pass of each build: LDS instructions / bank conflicts / waits
 #   rehearse        bench.py N=2 on one GPU (gloo, both ranks on device 0)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -53,6 +55,21 @@ for step in "$@"; do
         FLASHSDF_LIB=$PWD/$lib timeout -k 10 200 python tools/profile_pass.py --variants shuffled-1-64-1 --reps 3 \
           --rounds 2 >> $O/stats.log 2>&1 || { echo STATS FAILED; tail $O/stats.log; exit 1; }
         echo "$lib $(tail -1 $O/stats.log | cut -c1-700)"
+      done ;;
+    abcheck:*)
+      L=${step#abcheck:}; L=${L//,/ }
+      timeout -k 10 300 python tools/ab_check.py $L > $O/abcheck.log 2>&1 || { echo ABCHECK FAILED; tail -20 $O/abcheck.log; exit 1; }
+      tail -5 $O/abcheck.log ;;
+    lds:*)
+      L=${step#lds:}
+      for lib in ${L//,/ }; do
+        N=$(basename $lib .so)
+        ( cd /tmp && export TMPDIR=/tmp FLASHSDF_LIB=$GRAFT_REPO_ROOT/$lib && timeout -s KILL 120 rocprofv3 --pmc \
+          SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU \
+          --output-format csv -d $GRAFT_REPO_ROOT/$O/lds_$N -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 \
+          --warmup 3 --no-cpu-baseline --no-full-iteration > $GRAFT_REPO_ROOT/$O/lds_$N.log 2>&1 ) \
+          || { echo LDS PMC FAILED; tail $O/lds_$N.log; exit 1; }
+        python tools/pmc_brief.py $O/lds_$N/run_counter_collection.csv pass_kernel ;
       done ;;
     rehearse)
       export FSDF_BENCH_BACKEND=gloo FSDF_BENCH_DEVICE=0

@@ -58,6 +58,13 @@ def main():
     e2 = buf[32 + 26 * 16384:32 + 26 * 16384 + min(nw, 4 * 16384)].astype(np.uint64)
     ev2 = np.stack([(e2 >> np.uint64(16 * j)) & np.uint64(0xffff) for j in range(3)], 1).astype(np.int64)
     # slow lane-evaluations | of which the hull won the lane | lanes spared the search by h_max
+    nw2 = min(nw, 16384)
+    p2 = buf[32 + 30 * 16384:32 + 30 * 16384 + 2 * nw2].reshape(-1, 2).astype(np.uint64)
+    sub = np.zeros((min(nw, 4 * 16384), 8))
+    sub[:nw2] = fields(p2)
+    sub[:, [0, 1, 4, 5]] *= 0.01  # us
+    sub_names = ["t_cert", "t_walk_cot", "vertex_lane_certs", "fan_iters", "t_screen_loop", "t_fixup",
+                 "edge_lane_certs", "interior_lane_certs"]
     ev = np.stack([evf[:, 0], evf[:, 4]], 1)
     nb = -(-args.points // 256)
     bt = buf[32 + 16 * 16384:32 + 16 * 16384 + 2 * min(nb, 16384)].reshape(-1, 2).astype(np.int64)
@@ -105,11 +112,20 @@ def main():
     res["search_lanes"] = {n: int(ev2[:, j].sum()) for j, n in enumerate(e2n)}
     for i, r in zip(heavy, res["heaviest_detail"]):
         r.update({n: int(ev2[i, j]) for j, n in enumerate(e2n)})
+        r.update({n: round(float(sub[i, j]), 2) for j, n in enumerate(sub_names)})
+    res["sub_phase_totals"] = {n: round(float(sub[:, j].sum()), 2) for j, n in enumerate(sub_names)}
+    ws = max(int(evf[:, 3].sum()), 1)
+    res["per_walk_step"] = {"us_cert": round(float(sub[:, 0].sum() / ws), 3),
+                            "us_cot": round(float(sub[:, 1].sum() / ws), 3),
+                            "fan_iters": round(float(sub[:, 3].sum() / ws), 3)}
+    res["per_eval_screen_us"] = {"loop": round(float(sub[:, 4].sum() / ne), 3),
+                                 "fixup": round(float(sub[:, 5].sum() / ne), 3)}
     top = dur >= np.percentile(dur, 99)
     res["top1pct"] = {"waves": int(top.sum()), "us_mean": float(dur[top].mean()),
                       **{n: round(float(evf[top, j].mean()), 2) for j, n in enumerate(ev_names)},
                       **{"t_" + n: round(float(phf[top, j].mean()), 2) for j, n in enumerate(ph_names)},
-                      **{n: round(float(ev2[top, j].mean()), 2) for j, n in enumerate(e2n)}}
+                      **{n: round(float(ev2[top, j].mean()), 2) for j, n in enumerate(e2n)},
+                      **{n: round(float(sub[top, j].mean()), 2) for j, n in enumerate(sub_names)}}
     print(json.dumps(res))
     if args.json:
         np.savez_compressed(args.json.replace(".json", ".npz"), start=start, end=end, evals=ev)

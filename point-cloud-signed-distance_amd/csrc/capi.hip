@@ -200,6 +200,7 @@ static void free_model(fsdf_ctx* c) {
     dfree(P->planes_w);
     dfree(P->spheres_w);
     dfree(P->screen_w);
+    dfree(P->image_w);
   }
   c->pm_alt.rbf_rows = nullptr;
   c->pm_next = 0;
@@ -453,8 +454,11 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
       // stay under 40 KiB, i.e. 4 workgroups per CU)
       const int plane_bytes = (tsz_ == 8 && FSDF_SCREEN32) ? 32 * ((h.n_faces + 1) / 2) : h.n_faces * 4 * tsz_;
       stage_bytes = std::max(stage_bytes, plane_bytes + h.n_vertices * 4 * tsz_ + 16 * h.n_faces);
-      // (+ the fp64 planes, 32 B per face, when they are staged too)
-      stage_p64 = std::max(stage_p64, plane_bytes + h.n_faces * 32 + h.n_vertices * 4 * tsz_ + 16 * h.n_faces);
+      // (+ the fp64 planes, 32 B per face, when they are staged too; the
+      // stage is then a copy of the hull's stage image, whose pair region is
+      // nf + 1 chunks as in screen_w)
+      stage_p64 = std::max(stage_p64, 16 * (h.n_faces + 1) + h.n_faces * 32 + h.n_vertices * 4 * tsz_ +
+                                          16 * h.n_faces);
     }
     face_off.push_back((int32_t)(face_hull.size()));
   }
@@ -518,6 +522,22 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
     HIPCHECK(c, dalloc((char**)&P->planes_w, (size_t)std::max(F, 1) * 4 * tsz));
     HIPCHECK(c, dalloc(&P->spheres_w, (size_t)K * fsdf::kBoundFloats * sizeof(float)));
     HIPCHECK(c, dalloc(&P->screen_w, (size_t)std::max(F + K, 1) * 4 * sizeof(float)));
+  }
+  if (planes64) {
+    // per-hull stage images (fsdf_internal.h PosedModel::image_w): the pose
+    // kernel rewrites the pairs, planes and vertex rows every pass; the face
+    // rows are static and written here
+    const size_t chunks = (size_t)4 * F + K + 2 * (size_t)V;
+    std::vector<int32_t> img(chunks * 4, 0);
+    for (int h = 0; h < K; ++h) {
+      const int nf = face_off[h + 1] - face_off[h], nv = vert_off[h + 1] - vert_off[h];
+      const size_t base = (size_t)4 * face_off[h] + h + 2 * (size_t)vert_off[h] + 3 * (size_t)nf + 1 + 2 * (size_t)nv;
+      memcpy(img.data() + 4 * base, face_rows.data() + 4 * (size_t)face_off[h], (size_t)nf * 4 * sizeof(int32_t));
+    }
+    for (fsdf::PosedModel* P : {&c->pm, &c->pm_alt}) {
+      HIPCHECK(c, dalloc((char**)&P->image_w, chunks * 16));
+      HIPCHECK(c, hipMemcpy(P->image_w, img.data(), chunks * 16, hipMemcpyHostToDevice));
+    }
   }
   HIPCHECK(c, dalloc(&c->d_poses, (size_t)S * 12 * sizeof(double)));
   const int R = (int)rbf_surface.size();

@@ -99,6 +99,12 @@ struct PosedModel {
   void* verts_w = nullptr;    // T
   void* hscale_w = nullptr;   // T
   float* screen_w = nullptr;  // [F+K][4] (f64 contexts; see the layout above)
+  // f64 planes64 contexts: every hull's LDS stage image, [4F + K + 2V] 16-B
+  // chunks; hull k at chunk 4·face_off[k] + k + 2·vert_off[k]: its screening
+  // pairs (nf + 1 chunks, as in screen_w), fp64 planes (2 per face), fp64
+  // vertex rows (2 per vertex), face rows (1 per face; static, written at
+  // set_model). One contiguous copy stages a hull.
+  void* image_w = nullptr;
   void* rbf_rows = nullptr;   // T [rbf_rows][4], per pass (fsdf_set_rbf_params)
 };
 

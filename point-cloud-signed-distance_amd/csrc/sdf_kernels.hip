@@ -54,6 +54,7 @@ template <> __device__ __forceinline__ float tinf() { return __builtin_huge_valf
 // Pose kernel: local model + poses -> world-frame planes and vertices.
 // One thread per face, one per vertex, then one wave per hull (sphere + scale).
 // ---------------------------------------------------------------------------
+typedef int I4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void xf_point(const double* P, const double* v, double* o) {
   // o = R v + t, R row-major P[0..8], t = P[9..11]
   o[0] = __builtin_fma(P[0], v[0], __builtin_fma(P[1], v[1], __builtin_fma(P[2], v[2], P[9])));
@@ -69,7 +70,7 @@ template <typename T>
 __device__ __forceinline__ void pose_body(const LocalModel& lm, const double* __restrict__ poses,
                                           T* __restrict__ planes_w, float* __restrict__ spheres_w,
                                           T* __restrict__ verts_w, T* __restrict__ hscale_w,
-                                          float* __restrict__ screen_w) {
+                                          float* __restrict__ screen_w, I4* __restrict__ image_w) {
   int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int fv = lm.F + lm.V, fv_pad = (fv + 63) & ~63;
   if (tid >= fv && tid < fv_pad) return;  // padding: hull waves start wave-aligned
@@ -108,6 +109,17 @@ __device__ __forceinline__ void pose_body(const LocalModel& lm, const double* __
       if ((nf & 1) && j == nf - 1)  // odd count: the last pair repeats its face
 #pragma unroll
         for (int c = 0; c < 4; ++c) pair[2 * c + 1] = v[c];
+      if (sizeof(T) == 8 && image_w) {  // the hull's stage image: same pair words, then the fp64 plane
+        I4* img = image_w + 4 * lm.face_off[h] + h + 2 * lm.vert_off[h];
+        float* ip = (float*)(img + (j & ~1));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) ip[2 * c + (j & 1)] = v[c];
+        if ((nf & 1) && j == nf - 1)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) ip[2 * c + 1] = v[c];
+        double* q = (double*)(img + nf + 1 + 2 * j);
+        q[0] = nw[0]; q[1] = nw[1]; q[2] = nw[2]; q[3] = dw;
+      }
     }
   } else if (tid < lm.F + lm.V) {
     const int v = tid - lm.F;
@@ -116,6 +128,13 @@ __device__ __forceinline__ void pose_body(const LocalModel& lm, const double* __
     xf_point(P, lm.verts_l + 3 * v, w);
     T* o = verts_w + 4 * v;
     o[0] = (T)w[0]; o[1] = (T)w[1]; o[2] = (T)w[2]; o[3] = (T)0;
+    if (sizeof(T) == 8 && image_w) {
+      const int h = lm.vert_hull[v];
+      const int nf = lm.face_off[h + 1] - lm.face_off[h];
+      double* q = (double*)(image_w + 4 * lm.face_off[h] + h + 2 * lm.vert_off[h] + 3 * nf + 1 +
+                            2 * (v - lm.vert_off[h]));
+      q[0] = w[0]; q[1] = w[1]; q[2] = w[2]; q[3] = 0.0;
+    }
   } else if (tid < lm.F + lm.V + 64 * lm.K) {
     // one wave per hull (the wave is entirely inside this range: F + V is
     // padded to a multiple of 64 by the launcher): sphere + certificate scale
@@ -171,17 +190,18 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const double* __restrict__ poses,
                                                       T* __restrict__ planes_w, float* __restrict__ spheres_w,
                                                       T* __restrict__ verts_w, T* __restrict__ hscale_w,
-                                                      float* __restrict__ screen_w) {
-  pose_body<T>(lm, poses, planes_w, spheres_w, verts_w, hscale_w, screen_w);
+                                                      float* __restrict__ screen_w, I4* __restrict__ image_w) {
+  pose_body<T>(lm, poses, planes_w, spheres_w, verts_w, hscale_w, screen_w, image_w);
 }
 template <typename T>
 __global__ __launch_bounds__(kBlock) void pose_kernel_args(LocalModel lm, PoseArgs pa, T* __restrict__ planes_w,
                                                            float* __restrict__ spheres_w, T* __restrict__ verts_w,
-                                                           T* __restrict__ hscale_w, float* __restrict__ screen_w) {
+                                                           T* __restrict__ hscale_w, float* __restrict__ screen_w,
+                                                           I4* __restrict__ image_w) {
   __shared__ double sp[12 * kPoseArgMax];
   for (int i = threadIdx.x; i < 12 * lm.S; i += kBlock) sp[i] = pa.v[i];
   __syncthreads();
-  pose_body<T>(lm, sp, planes_w, spheres_w, verts_w, hscale_w, screen_w);
+  pose_body<T>(lm, sp, planes_w, spheres_w, verts_w, hscale_w, screen_w, image_w);
 }
 
 // ---------------------------------------------------------------------------
@@ -189,7 +209,6 @@ __global__ __launch_bounds__(kBlock) void pose_kernel_args(LocalModel lm, PoseAr
 // ---------------------------------------------------------------------------
 template <typename T> struct Row4 { typedef T __attribute__((ext_vector_type(4))) type; };
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-typedef int I4 __attribute__((ext_vector_type(4)));
 
 // reg: the Voronoi region of the result — 0, 1, 2 vertex a, b, c; 3, 4, 5 the
 // edge a→b, b→c, c→a (face edges 0, 1, 2); 6 the interior.
@@ -292,6 +311,7 @@ struct PassModel {
   const T* __restrict__ hscale;
   const float* __restrict__ spheres;
   const float* __restrict__ screen;          // fp32 screening pairs (f64 contexts)
+  const I4* __restrict__ image;              // per-hull stage images (planes64; PosedModel::image_w)
 };
 
 // Per-workgroup LDS hull table, filled once in the kernel prologue (row K is
@@ -332,7 +352,9 @@ __device__ __forceinline__ float box_bound(const HullRow& h, float x, float y, f
 __device__ __forceinline__ bool box_within(const HullRow& h, float x, float y, float z, float t) {
   float s;
   const float mx = box_bound(h, x, y, z, s);
-  return mx <= 0.0f ? mx <= t : (t >= 0.0f && s <= t * t);
+  // (bitwise & throughout: short-circuit && on lane values becomes exec-mask
+  // branches; every operand here is cheap and already loaded)
+  return mx <= 0.0f ? mx <= t : ((t >= 0.0f) & (s <= t * t));
 }
 __device__ __forceinline__ float box_lower(const HullRow& h, float x, float y, float z) {
   float s;
@@ -348,7 +370,7 @@ __device__ __forceinline__ bool needs_at(const HullRow& h, float x, float y, flo
   const float dx = x - sp[0], dy = y - sp[1], dz = z - sp[2];
   const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
   const float t = tb + sp[3];
-  return t >= 0.0f && dist2 <= t * t && box_within(h, x, y, z, tb);
+  return (t >= 0.0f) & (dist2 <= t * t) & box_within(h, x, y, z, tb);
 }
 
 // Bounding sphere of the wave's points (f32, wave-uniform): every valid lane's
@@ -496,9 +518,26 @@ __device__ __forceinline__ void stage_hull(void* __restrict__ lw, const I4* __re
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + 64 * j + lane;
-      if (c < N) dst[c] = v[j];
+      // lanes past the end hold chunk N-1 (clamped load) and store it there
+      // again: same bits, and no exec-mask branch per store
+      dst[min(c0 + 64 * j + lane, N - 1)] = v[j];
     }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One contiguous region (a hull's stage image, PosedModel::image_w): the same
+// one-latency bulk copy with no region selects.
+__device__ __forceinline__ void stage_image(void* __restrict__ lw, const I4* __restrict__ src, int N) {
+  const int lane = threadIdx.x & 63;
+  I4* dst = (I4*)lw;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  for (int c0 = 0; c0 < N; c0 += 8 * 64) {
+    I4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = src[min(c0 + 64 * j + lane, N - 1)];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[min(c0 + 64 * j + lane, N - 1)] = v[j];
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
@@ -514,11 +553,16 @@ template <> __device__ __forceinline__ float cert_eps() { return 4e-6f; }
 
 // packed face row: (i0 | i1<<16, i2 | n0<<16, n1 | n2<<16, 0) with i_j the
 // hull-local vertex indices and n_e the hull-local face across edge e (i_e -> i_e+1)
+// Decoded with one variable 64-bit shift, no selects: with a lane-divergent j
+// the compiler turns a select chain into a switch, i.e. an exec-mask branch
+// tree (~25 scalar instructions and 6 branches per decode in the fan walk).
 __device__ __forceinline__ int fr_vert(const I4& r, int j) {
-  return j == 0 ? (r[0] & 0xffff) : (j == 1 ? ((r[0] >> 16) & 0xffff) : (r[1] & 0xffff));
+  const uint64_t w = ((uint64_t)(uint32_t)r[1] << 32) | (uint32_t)r[0];
+  return (int)((w >> (16 * j)) & 0xffff);
 }
 __device__ __forceinline__ int fr_nbr(const I4& r, int e) {
-  return e == 0 ? ((r[1] >> 16) & 0xffff) : (e == 1 ? (r[2] & 0xffff) : ((r[2] >> 16) & 0xffff));
+  const uint64_t w = ((uint64_t)(uint32_t)r[2] << 32) | (uint32_t)r[1];
+  return (int)((w >> (16 * e + 16)) & 0xffff);
 }
 
 // Local optimality certificate of q = the closest point of triangle f (in
@@ -551,7 +595,7 @@ __device__ __forceinline__ bool cert_step(T px, T py, T pz, int f, int reg, cons
   const I4 fr = lf[f];
   if (reg >= 3) {
     const int e = reg - 3;
-    const R U = lv[fr_vert(fr, e)], W = lv[fr_vert(fr, e == 2 ? 0 : e + 1)];
+    const R U = lv[fr_vert(fr, e)], W = lv[fr_vert(fr, e + 1 - 3 * (e == 2))];
     const int g = fr_nbr(fr, e);
     const T sf = edge_value<T>(lp[f], U, W, px, py, pz);
     const T sg = edge_value<T>(lp[g], W, U, px, py, pz);
@@ -571,7 +615,7 @@ __device__ __forceinline__ bool cert_step(T px, T py, T pz, int f, int reg, cons
   for (int it = 0; it < 32; ++it) {
     if (fan_it) *fan_it = it + 1;
     const int g2 = fr_nbr(r, j);  // across edge v -> u
-    const R Un = lv[fr_vert(r, j == 2 ? 0 : j + 1)];
+    const R Un = lv[fr_vert(r, j + 1 - 3 * (j == 2))];
     const T dot = mfma_(wx, Un[0] - V[0], mfma_(wy, Un[1] - V[1], wz * (Un[2] - V[2])));
     if (dot > tol) {
       n1 = g != f ? g : g2;
@@ -580,7 +624,7 @@ __device__ __forceinline__ bool cert_step(T px, T py, T pz, int f, int reg, cons
     }
     if (g2 == f) return true;
     r = lf[g2];
-    j = fr_vert(r, 0) == v ? 0 : (fr_vert(r, 1) == v ? 1 : 2);
+    j = 2 - (fr_vert(r, 1) == v) - 2 * (fr_vert(r, 0) == v);  // (the row's vertices are distinct)
     g = g2;
   }
   return false;
@@ -731,11 +775,17 @@ __device__ __forceinline__ void hull_sdf(T px, T py, T pz, int k, const PassMode
   // one-chunk-per-wave pass (P64: pass_kernel ALIAS, LocalModel::planes64)
   constexpr bool kP64 = kStagePairs<T> && P64;
   const int npl = kP64 ? nf * cpr : 0;
-  stage_hull(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0), nv * cpr,
-             m.face_rows + f0, nf);
+  // (P64: the hull's stage image, whose pair region is nf + 1 chunks)
+  const int npr = kP64 ? nf + 1 : np2;
+  if constexpr (kP64) {
+    stage_image(lw, m.image + (4 * f0 + k + 2 * v0), npr + npl + nv * cpr + nf);
+  } else {
+    stage_hull(lw, src0, np2, (const I4*)(m.planes + 4 * f0), npl, (const I4*)(m.verts + 4 * v0), nv * cpr,
+               m.face_rows + f0, nf);
+  }
   tw = wt_add(0, tw);
-  const R* lp = kP64 ? (const R*)((const I4*)lw + np2) : (kStagePairs<T> ? (const R*)(m.planes + 4 * f0) : (const R*)lw);
-  const R* lv = (const R*)((const I4*)lw + np2 + npl);
+  const R* lp = kP64 ? (const R*)((const I4*)lw + npr) : (kStagePairs<T> ? (const R*)(m.planes + 4 * f0) : (const R*)lw);
+  const R* lv = (const R*)((const I4*)lw + npr + npl);
   const I4* lf = (const I4*)(lv + nv);
   const T scale = (T)ht[k].hscale;
   auto uplane = [&](int f) -> R { return lp[f]; };
@@ -1207,7 +1257,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     for (int s = 0; s < SLOTS; ++s) {
       const int k = 64 * s + lane;
       const HullRow& h = ht[k < K ? k : 0];
-      const bool c = k < K && Dk[s] - rw - h.sphere[3] <= ubw + mrgw && box_within(h, cwx, cwy, cwz, ubw + mrgw + rw);
+      const bool c = (k < K) & (Dk[s] - rw - h.sphere[3] <= ubw + mrgw) & box_within(h, cwx, cwy, cwz, ubw + mrgw + rw);
       cand[s] = __ballot(c);
     }
     if (count_events(stats) && lane == 0) {
@@ -1263,7 +1313,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   // tested without a sqrt: |p-c_k|^2 <= (min(ub, best) + mrg + r_k)^2
   auto needs = [&](int k) -> bool {
     if (!CULL) return valid;
-    return valid && needs_at(ht[k], pxf, pyf, pzf, fminf(ub, (float)best) + mrg);
+    return valid & needs_at(ht[k], pxf, pyf, pzf, fminf(ub, (float)best) + mrg);
   };
   // evaluations may run out of index order: ties keep the smaller k
 #if FSDF_WAVE_TIMES
@@ -1769,19 +1819,19 @@ hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_pose
     memcpy(pa.v, h_poses, (size_t)12 * lm.S * sizeof(double));
     if (precision == 64)
       hipLaunchKernelGGL(pose_kernel_args<double>, dim3(grid), dim3(kBlock), 0, s, lm, pa, (double*)pm.planes_w,
-                         pm.spheres_w, (double*)pm.verts_w, (double*)pm.hscale_w, pm.screen_w);
+                         pm.spheres_w, (double*)pm.verts_w, (double*)pm.hscale_w, pm.screen_w, (I4*)pm.image_w);
     else
       hipLaunchKernelGGL(pose_kernel_args<float>, dim3(grid), dim3(kBlock), 0, s, lm, pa, (float*)pm.planes_w,
-                         pm.spheres_w, (float*)pm.verts_w, (float*)pm.hscale_w, (float*)nullptr);
+                         pm.spheres_w, (float*)pm.verts_w, (float*)pm.hscale_w, (float*)nullptr, (I4*)nullptr);
     return hipGetLastError();
   }
   if (precision == 64) {
     hipLaunchKernelGGL(pose_kernel<double>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses,
                        (double*)pm.planes_w, pm.spheres_w, (double*)pm.verts_w, (double*)pm.hscale_w,
-                       pm.screen_w);
+                       pm.screen_w, (I4*)pm.image_w);
   } else {
     hipLaunchKernelGGL(pose_kernel<float>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses, (float*)pm.planes_w,
-                       pm.spheres_w, (float*)pm.verts_w, (float*)pm.hscale_w, (float*)nullptr);
+                       pm.spheres_w, (float*)pm.verts_w, (float*)pm.hscale_w, (float*)nullptr, (I4*)nullptr);
   }
   return hipGetLastError();
 }
@@ -1808,6 +1858,7 @@ static PassModel<T> pass_model(const LocalModel& lm, const PosedModel& pm) {
   m.hscale = (const T*)pm.hscale_w;
   m.spheres = pm.spheres_w;
   m.screen = pm.screen_w;
+  m.image = (const I4*)pm.image_w;
   return m;
 }
 

@@ -14,6 +14,7 @@
 #   stats:LIBS      kernel work counters of each build (bench cloud; commas between libs)
 #   abcheck:LIBS    bit-for-bit agreement of builds with the first (tools/ab_check.py)
 #   lds:LIBS        PMC pass of each build: LDS instructions / bank conflicts / waits
+#   pmc:NAME:CTRS   one PMC pass (commas between counters) of the product library
 #   rehearse        bench.py N=2 on one GPU (gloo, both ranks on device 0)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -71,6 +72,14 @@ for step in "$@"; do
           || { echo LDS PMC FAILED; tail $O/lds_$N.log; exit 1; }
         python tools/pmc_brief.py $O/lds_$N/run_counter_collection.csv pass_kernel ;
       done ;;
+    pmc:*)
+      # pmc:NAME:C1,C2,... — one counter pass over the product library (<= 8 SQ counters)
+      R=${step#pmc:}; N=${R%%:*}; C=${R#*:}; C=${C//,/ }
+      ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv \
+          -d $GRAFT_REPO_ROOT/$O/pmc_$N -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 3 \
+          --no-cpu-baseline --no-full-iteration > $GRAFT_REPO_ROOT/$O/pmc_$N.log 2>&1 ) \
+        || { echo PMC FAILED; tail $O/pmc_$N.log; exit 1; }
+      python tools/pmc_brief.py $O/pmc_$N/run_counter_collection.csv pass_kernel ;;
     rehearse)
       export FSDF_BENCH_BACKEND=gloo FSDF_BENCH_DEVICE=0
       timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \

@@ -1534,7 +1534,10 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
   // logical block of this launch slot (cost-ordered schedule, see PassOutputs)
   const int lb = out.order ? __builtin_amdgcn_readfirstlane(out.order[blockIdx.x]) : (int)blockIdx.x;
   // (ALIAS: a wave past the cloud's end never evaluates; its rows are zeroed now)
-  if (ALIAS && (int64_t)lb * kPassBlock + wave * 64 >= n) zero_rows();
+  if (ALIAS && (int64_t)lb * kPassBlock + wave * 64 >= n) {
+    zero_rows();
+    if (lane == 0) red_of(wave)[SLOTS * 64 * 6] = 0.0;
+  }
   const uint64_t t_block = out.cost ? __builtin_amdgcn_s_memrealtime() : 0;
 #if FSDF_WAVE_TIMES
   const uint64_t t_block0 = __builtin_amdgcn_s_memrealtime();
@@ -1565,8 +1568,16 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     T* tstage = ALIAS ? (T*)((char*)stage + kRedStride * 8) : stage;  // gradient transpose after the rows
-    emit_chunk<T, SLOTS, RBF>(px, py, pz, valid, best, bk, gx, gy, gz, i, base, n, m, out, acc_row, cost_acc,
-                              rbf_wave, tstage, stage_cap);
+    // (ALIAS: the wave's one chunk; its cost is summed and parked in the
+    // wave's row now — a per-lane accumulator live through the whole kernel
+    // was spilled to scratch at the register budget)
+    double cost_chunk = 0.0;
+    emit_chunk<T, SLOTS, RBF>(px, py, pz, valid, best, bk, gx, gy, gz, i, base, n, m, out, acc_row,
+                              ALIAS ? cost_chunk : cost_acc, rbf_wave, tstage, stage_cap);
+    if (ALIAS) {
+      cost_chunk = wave_sum(cost_chunk);
+      if (lane == 0) red_of(wave)[SLOTS * 64 * 6] = cost_chunk;
+    }
 #if FSDF_WAVE_TIMES
     // diagnostic: 100 MHz wall clock around each wave-iteration of the first
     // grid pass (stats + 32 + 2 * wave), written by lane 0
@@ -1588,8 +1599,10 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
   }
 
   // ---- block combine (fixed order) ----
-  cost_acc = wave_sum(cost_acc);
-  if (lane == 0) red_of(wave)[SLOTS * 64 * 6] = cost_acc;
+  if (!ALIAS) {
+    cost_acc = wave_sum(cost_acc);
+    if (lane == 0) red_of(wave)[SLOTS * 64 * 6] = cost_acc;
+  }
   __syncthreads();
   const int len6 = 1 + 6 * m.S;
   const int len = len6 + (RBF ? m.rbf_acc_off[m.R] : 0);

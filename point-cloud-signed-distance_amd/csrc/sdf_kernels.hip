@@ -354,7 +354,7 @@ __device__ __forceinline__ bool box_within(const HullRow& h, float x, float y, f
   const float mx = box_bound(h, x, y, z, s);
   // (bitwise & throughout: short-circuit && on lane values becomes exec-mask
   // branches; every operand here is cheap and already loaded)
-  return mx <= 0.0f ? mx <= t : ((t >= 0.0f) & (s <= t * t));
+  return ((mx <= 0.0f) & (mx <= t)) | ((mx > 0.0f) & (t >= 0.0f) & (s <= t * t));
 }
 __device__ __forceinline__ float box_lower(const HullRow& h, float x, float y, float z) {
   float s;

@@ -15,6 +15,8 @@
 #   abcheck:LIBS    bit-for-bit agreement of builds with the first (tools/ab_check.py)
 #   lds:LIBS        PMC pass of each build: LDS instructions / bank conflicts / waits
 #   pmc:NAME:CTRS   one PMC pass (commas between counters) of the product library
+#   sweep           bench.py at 2^16 .. 2^20 points           -> size_sweep.jsonl
+#   configs         tools/bench_configs.py (BASELINE configs C2-C5, M64)
 #   rehearse        bench.py N=2 on one GPU (gloo, both ranks on device 0)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -80,6 +82,17 @@ for step in "$@"; do
           --no-cpu-baseline --no-full-iteration > $GRAFT_REPO_ROOT/$O/pmc_$N.log 2>&1 ) \
         || { echo PMC FAILED; tail $O/pmc_$N.log; exit 1; }
       python tools/pmc_brief.py $O/pmc_$N/run_counter_collection.csv pass_kernel ;;
+    sweep)
+      # M64 pass/step against cloud size (one bench line per size)
+      for n in 65536 131072 262144 524288 1048576; do
+        timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-full-iteration --points $n \
+          >> $O/size_sweep.jsonl 2>> $O/size_sweep.err || { echo SWEEP FAILED; tail $O/size_sweep.err; exit 1; }
+      done
+      cut -c1-200 $O/size_sweep.jsonl ;;
+    configs)
+      timeout -k 10 400 python tools/bench_configs.py --json $O/bench_configs.json > $O/bench_configs.log 2>&1 \
+        || { echo CONFIGS FAILED; tail $O/bench_configs.log; exit 1; }
+      tail -12 $O/bench_configs.log ;;
     rehearse)
       export FSDF_BENCH_BACKEND=gloo FSDF_BENCH_DEVICE=0
       timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \

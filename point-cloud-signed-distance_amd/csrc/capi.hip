@@ -816,7 +816,7 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
   int pbuf = 0;
   int rc = pose_model(c, poses, &P, &pbuf);
   if (rc) return rc;
-  const int nblocks = fsdf::pass_blocks(n);
+  const int nblocks = fsdf::pass_blocks(n, c->lm);
   rc = ensure_partials(c, nblocks);
   if (rc) return rc;
   fsdf::PassOutputs out;

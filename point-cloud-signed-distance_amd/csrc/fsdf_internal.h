@@ -157,7 +157,8 @@ hipError_t launch_to_f32(const double* src, float* dst, int64_t count, hipStream
 // precision -> d_out [ceil(n/64)][4] f32 (the pass kernel's wave culling input)
 hipError_t launch_chunk_spheres(int precision, const void* d_pts, int64_t n, float* d_out, hipStream_t s);
 
-int pass_blocks(int64_t n);
+int pass_blocks(int64_t n, const LocalModel& lm);
+bool hpart_pass(const LocalModel& lm, int64_t n);
 
 // dynamic LDS of one pass (raycast=false) / raycast workgroup for this model
 size_t pass_lds_bytes(const LocalModel& lm, bool raycast, bool alias = false);

@@ -32,6 +32,7 @@
 #include "fsdf_internal.h"
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 namespace fsdf {
@@ -1201,7 +1202,10 @@ template <typename T, int SLOTS, bool CULL, bool RBF, bool P64 = false>
 __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const PassModel<T>& m,
                                            const HullRow* __restrict__ ht, float smax, T* __restrict__ lw,
                                            unsigned long long* __restrict__ stats, T& best, int& bk, T& gx, T& gy,
-                                           T& gz, const F4* __restrict__ cws = nullptr) {
+                                           T& gz, const F4* __restrict__ cws = nullptr, uint64_t partmask = ~0ull) {
+  // partmask (hull-partitioned pass, pass_kernel HPART): this wave evaluates
+  // only the hulls whose bit (k & 63) is set; culling and the upper bound
+  // still use every hull
   const int K = m.K;
   const int lane = threadIdx.x & 63;
   // Phase A (fp32, exact-safe): with c_k inside hull k and r_k its bounding
@@ -1279,7 +1283,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
         ub2 = fminf(ub2, dist2);
         // seed: the least lower bound (sphere or box)
         const float lb = fmaxf(__builtin_sqrtf(dist2) - sp[3], box_lower(ht[k], pxf, pyf, pzf));
-        if (lb < lb_min) { lb_min = lb; kseed = k; }
+        if (((partmask >> (k & 63)) & 1) && lb < lb_min) { lb_min = lb; kseed = k; }
       }
     }
   }
@@ -1347,7 +1351,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   // kernel's code to ~40 KB): first each lane's seed hull (Phase B, one
   // evaluation per distinct seed in the wave, so that `best` is tight), then
   // the remaining candidates in index order (Phase C).
-  uint64_t pend = (CULL && K > 0) ? __ballot(valid) : 0ull;
+  uint64_t pend = (CULL && K > 0) ? __ballot(valid && lb_min < __builtin_huge_valf()) : 0ull;
   int slot = -1;      // Phase C slot; -1 while seeds are pending
   uint64_t cm = 0ull;  // Phase C candidates left in `slot`
   for (;;) {
@@ -1367,7 +1371,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
         ++slot;
 #pragma unroll
         for (int s = 0; s < SLOTS; ++s)
-          if (s == slot) cm = cand[s] & ~done[s];
+          if (s == slot) cm = cand[s] & ~done[s] & partmask;
       }
       if (!cm) break;
       k = 64 * slot + __builtin_ctzll(cm);
@@ -1489,18 +1493,39 @@ __device__ __forceinline__ int64_t pidx(int t, int b, int nblocks) {
 // Residual pass.
 // ---------------------------------------------------------------------------
 extern __shared__ __attribute__((aligned(16))) char fsdf_lds[];
+#ifndef FSDF_HPART
+#define FSDF_HPART 4
+#endif
+constexpr int kHpart = FSDF_HPART;  // waves per chunk in the hull-partitioned pass (2 or 4)
+static_assert(kHpart == 2 || kHpart == 4, "FSDF_HPART is 2 or 4");
 
 // ALIAS (one chunk per wave: n <= grid * 256; hull-only, <= 64 surfaces; f64
 // models with LocalModel::planes64): the wave's wrench rows live in its own
 // hull stage, which is free once the chunk's scene evaluation is done — 12 KiB
 // less LDS per workgroup, spent on staging the fp64 planes with the hull
 // (hull_sdf P64) at the same occupancy.
-template <typename T, int SLOTS, bool CULL, bool RBF, bool ALIAS = false>
+//
+// HPART (hull-partitioned, with ALIAS; small clouds, hpart_pass): kHpart
+// waves share one 64-point chunk and split its hull evaluations by hull index
+// (part j of the chunk evaluates hulls k with k % kHpart == j; culling and the
+// upper bound use every hull, each wave prunes with its own best). Any upper
+// bound of d* is exact-safe, so each wave's result is the exact first-index
+// minimum over its hulls, and the lexicographic (d, k) minimum over the
+// chunk's waves is the full scene's — bit for bit. The heaviest chunks'
+// serial evaluations are spread over kHpart waves where a one-wave-per-chunk
+// grid would leave most wave slots idle.
+template <typename T, int SLOTS, bool CULL, bool RBF, bool ALIAS = false, bool HPART = false>
 __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)) void pass_kernel(
     const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out) {
   static_assert(!ALIAS || (SLOTS == 1 && !RBF), "aliased wrench rows: hull-only, <= 64 surfaces");
+  static_assert(!HPART || ALIAS, "the hull-partitioned pass is an aliased pass");
+  constexpr int kParts = HPART ? kHpart : 1;
+  constexpr int kChunkStride = kPassBlock / kParts;  // points per logical block
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
+  // (wave-uniform: readfirstlane keeps the hull mask and the loops scalar)
+  const int part = HPART ? __builtin_amdgcn_readfirstlane(wave % kHpart) : 0;  // (HPART) this wave's hull residue
+  const int cw = HPART ? __builtin_amdgcn_readfirstlane(wave / kHpart) : wave;  // the block's chunk this wave works on
   // All LDS is one dynamic region (16-byte aligned carve, see pass_lds_bytes):
   //   red     [4 waves][kRedStride] f64  per-hull wrench sums + cost (not ALIAS)
   //   rbf_acc [4 waves][kMaxRbfAcc] f64  (RBF variants only)
@@ -1534,7 +1559,7 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
   // logical block of this launch slot (cost-ordered schedule, see PassOutputs)
   const int lb = out.order ? __builtin_amdgcn_readfirstlane(out.order[blockIdx.x]) : (int)blockIdx.x;
   // (ALIAS: a wave past the cloud's end never evaluates; its rows are zeroed now)
-  if (ALIAS && (int64_t)lb * kPassBlock + wave * 64 >= n) {
+  if (ALIAS && (int64_t)lb * kChunkStride + cw * 64 >= n) {
     zero_rows();
     if (lane == 0) red_of(wave)[SLOTS * 64 * 6] = 0.0;
   }
@@ -1543,8 +1568,12 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
   const uint64_t t_block0 = __builtin_amdgcn_s_memrealtime();
 #endif
   const float smax = load_hull_table(m, ht);
-  const int64_t stride = (int64_t)gridDim.x * kPassBlock;
-  for (int64_t base = (int64_t)lb * kPassBlock + wave * 64; base < n; base += stride) {
+  const int64_t stride = (int64_t)gridDim.x * kChunkStride;
+  // (HPART: exactly one iteration for every wave, also for a chunk past the
+  // cloud's end — its lanes are all invalid — because the combine below holds
+  // workgroup barriers)
+  const int64_t base0 = (int64_t)lb * kChunkStride + cw * 64;
+  for (int64_t base = base0; HPART ? base == base0 : base < n; base += stride) {
     const int64_t i = base + lane;
     const bool valid = i < n;
     const int64_t ii = valid ? i : n - 1;
@@ -1559,7 +1588,30 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
     T best, gx, gy, gz;
     int bk;
     const F4* cws = out.chunk_ws ? (const F4*)out.chunk_ws + (base >> 6) : nullptr;
-    scene_eval<T, SLOTS, CULL, RBF, ALIAS>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz, cws);
+    scene_eval<T, SLOTS, CULL, RBF, ALIAS>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz, cws,
+                                           HPART ? ((kParts == 4 ? 0x1111111111111111ull : 0x5555555555555555ull) << part)
+                                                 : ~0ull);
+    if constexpr (HPART) {
+      // the chunk's waves' results meet in their stages; part 0 keeps the
+      // lexicographic (d, k) minimum per point
+      T* rs = stage;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      rs[4 * lane + 0] = best; rs[4 * lane + 1] = gx; rs[4 * lane + 2] = gy; rs[4 * lane + 3] = gz;
+      ((int*)(rs + 256))[lane] = bk;
+      __syncthreads();
+      if (part == 0) {
+#pragma unroll
+        for (int w = 1; w < kParts; ++w) {
+          const T* ro = (const T*)((char*)(ht + m.K + 1) + (wave + w) * m.stage_bytes);
+          const T d2 = ro[4 * lane];
+          const int k2 = ((const int*)(ro + 256))[lane];
+          if (d2 < best || (d2 == best && k2 < bk)) {
+            best = d2; bk = k2; gx = ro[4 * lane + 1]; gy = ro[4 * lane + 2]; gz = ro[4 * lane + 3];
+          }
+        }
+      }
+      __syncthreads();
+    }
     if (!valid) bk = 0;
 
     if (ALIAS) {  // the stage is free: this wave's rows go there (once: one chunk per wave)
@@ -1572,8 +1624,9 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
     // wave's row now — a per-lane accumulator live through the whole kernel
     // was spilled to scratch at the register budget)
     double cost_chunk = 0.0;
-    emit_chunk<T, SLOTS, RBF>(px, py, pz, valid, best, bk, gx, gy, gz, i, base, n, m, out, acc_row,
-                              ALIAS ? cost_chunk : cost_acc, rbf_wave, tstage, stage_cap);
+    if (!HPART || part == 0)  // (HPART: part 0 emits the chunk; the other waves' rows stay zero)
+      emit_chunk<T, SLOTS, RBF>(px, py, pz, valid, best, bk, gx, gy, gz, i, base, n, m, out, acc_row,
+                                ALIAS ? cost_chunk : cost_acc, rbf_wave, tstage, stage_cap);
     if (ALIAS) {
       cost_chunk = wave_sum(cost_chunk);
       if (lane == 0) red_of(wave)[SLOTS * 64 * 6] = cost_chunk;
@@ -1581,7 +1634,7 @@ __global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOT
 #if FSDF_WAVE_TIMES
     // diagnostic: 100 MHz wall clock around each wave-iteration of the first
     // grid pass (stats + 32 + 2 * wave), written by lane 0
-    if (out.stats && lane == 0 && base < (int64_t)64 * 4 * kMaxBlocks) {
+    if (out.stats && lane == 0 && (!HPART || part == 0) && base < (int64_t)64 * 4 * kMaxBlocks) {
       const int64_t wv = base / 64;
       out.stats[32 + 2 * wv] = w_t0;
       out.stats[33 + 2 * wv] = __builtin_amdgcn_s_memrealtime();
@@ -1815,7 +1868,22 @@ __global__ void to_f32_kernel(const double* __restrict__ src, float* __restrict_
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
-int pass_blocks(int64_t n) {
+#ifndef FSDF_HPART_POINTS
+#define FSDF_HPART_POINTS 131072
+#endif
+// the hull-partitioned pass (pass_kernel HPART) for clouds of at most
+// FSDF_HPART_POINTS points (environment override: FSDF_HPART_POINTS)
+bool hpart_pass(const LocalModel& lm, int64_t n) {
+  static const int64_t limit = [] {
+    const char* e = getenv("FSDF_HPART_POINTS");
+    return e ? (int64_t)atoll(e) : (int64_t)FSDF_HPART_POINTS;
+  }();
+  return FSDF_RED_IN_STAGE && lm.planes64 && lm.S <= 64 && lm.R == 0 && n > 0 && n <= limit &&
+         (n + kPassBlock / kHpart - 1) / (kPassBlock / kHpart) <= kMaxBlocks;
+}
+
+int pass_blocks(int64_t n, const LocalModel& lm) {
+  if (hpart_pass(lm, n)) return (int)((n + kPassBlock / kHpart - 1) / (kPassBlock / kHpart));
   int64_t b = (n + kPassBlock - 1) / kPassBlock;
   if (b < 1) b = 1;
   if (b > kMaxBlocks) b = kMaxBlocks;
@@ -1900,6 +1968,11 @@ static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void
   const size_t lds = pass_lds_bytes(lm, false);
   if constexpr (!RBF && FSDF_RED_IN_STAGE) {
     // one chunk per wave: the wrench rows alias the stage (pass_kernel ALIAS)
+    if (hpart_pass(lm, n)) {
+      launch_lds(pass_kernel<T, 1, CULL, false, true, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
+                 pts, n, m, out);
+      return;
+    }
     if (lm.S <= 64 && lm.planes64 && (int64_t)nblocks * kPassBlock >= n) {
       launch_lds(pass_kernel<T, 1, CULL, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
                  pts, n, m, out);
@@ -1922,7 +1995,10 @@ static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm,
                           int nblocks, const PassOutputs& out, hipStream_t s) {
 #if FSDF_BENCH_ONLY
   const PassModel<T> m = pass_model<T>(lm, pm);
-  if (FSDF_RED_IN_STAGE && lm.planes64 && (int64_t)nblocks * kPassBlock >= n)
+  if (hpart_pass(lm, n))
+    launch_lds(pass_kernel<T, 1, true, false, true, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
+               (const T*)d_pts, n, m, out);
+  else if (FSDF_RED_IN_STAGE && lm.planes64 && (int64_t)nblocks * kPassBlock >= n)
     launch_lds(pass_kernel<T, 1, true, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
                (const T*)d_pts, n, m, out);
   else

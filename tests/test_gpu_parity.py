@@ -307,3 +307,29 @@ def test_resident_order_outputs(m64, oracle_mod, ctx_factory):
     _, _, (k0, d0, _) = plain.eval(poses, per_point=True)
     assert np.array_equal(plain.permutation(), np.arange(len(pts)))
     assert np.array_equal(k0, kc) and np.array_equal(d0, dc)
+
+
+def test_hull_partitioned_pass_matches_one_wave_per_chunk(m64, ctx_factory):
+    """Clouds of <= 131,072 points run the hull-partitioned pass (pass_kernel
+    HPART: 4 waves share a chunk, hull k goes to wave k % 4, lexicographic
+    (d, k) merge); one more point runs the one-wave-per-chunk pass. Per-point
+    outputs do not depend on the block structure: the shared points must agree
+    bit for bit, sums to rounding."""
+    from flash import synthetic
+    import flash
+    qt, qe = synthetic.perturbed_configuration(m64, 303)
+    poses = flash.hull_poses(m64, qe)
+    n = 131072
+    pts = synthetic.depth_cloud(m64, qt, n + 1, seed=304, order="shuffled")
+    out = {}
+    for cull in (True, False):
+        for m in (n, n + 1):
+            ctx = ctx_factory(m64, cull=cull)
+            ctx.set_points(pts[:m])
+            out[cull, m] = ctx.eval(poses, per_point=True)
+    for cull in (True, False):
+        (c1, a1, (k1, d1, g1)), (c0, a0, (k0, d0, g0)) = out[cull, n], out[cull, n + 1]
+        assert np.array_equal(k1, k0[:n]) and np.array_equal(d1, d0[:n]) and np.array_equal(g1, g0[:n])
+        assert c1 == pytest.approx(np.dot(d1, d1), rel=1e-10)
+    # culled and brute force share the partitioned block structure: identical sums
+    assert np.array_equal(out[True, n][1], out[False, n][1])

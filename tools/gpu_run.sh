@@ -10,6 +10,7 @@
 #   bench:ARGS      bench.py with ARGS (commas = spaces), e.g. bench:--points,131072
 #   prof            tools/rocprof_round.sh (kernel trace + PMC passes)
 #   ab:LIBS         interleaved A/B of ab/lib_*.so builds (commas between libs)
+#   abn:P:LIBS      bit-for-bit check + A/B at a P-point cloud
 #   wt:LIB          per-wave timeline of a -DFSDF_WAVE_TIMES=1 build, 2^20 and 2^17 points
 #   stats:LIBS      kernel work counters of each build (bench cloud; commas between libs)
 #   abcheck:LIBS    bit-for-bit agreement of builds with the first (tools/ab_check.py)
@@ -46,6 +47,15 @@ for step in "$@"; do
       timeout -k 10 900 python tools/ab_bench.py $L --rounds 3 -- --no-full-iteration > $O/ab.log 2>&1 \
         || { tail -20 $O/ab.log; exit 1; }
       cat $O/ab.log ;;
+    abn:*)
+      # abn:POINTS:LIBS — the A/B and the bit-for-bit check at a given cloud size
+      R=${step#abn:}; P=${R%%:*}; L=${R#*:}; L=${L//,/ }
+      timeout -k 10 300 python tools/ab_check.py $L --points $P > $O/abcheck_$P.log 2>&1 \
+        || { echo ABCHECK FAILED; tail -20 $O/abcheck_$P.log; exit 1; }
+      tail -4 $O/abcheck_$P.log
+      timeout -k 10 900 python tools/ab_bench.py $L --rounds 3 -- --no-full-iteration --points $P > $O/ab_$P.log 2>&1 \
+        || { tail -20 $O/ab_$P.log; exit 1; }
+      tail -6 $O/ab_$P.log ;;
     wt:*)
       LIB=${step#wt:}; N=$(basename $LIB .so)
       FLASHSDF_LIB=$PWD/$LIB timeout -k 10 200 python tools/wave_times.py --json $O/wt_${N}_1m.json > $O/wt_${N}_1m.log 2>&1 &&

@@ -421,14 +421,14 @@ constexpr int kMaxRbfAcc = kMaxRbfAccum;
 //   ph[1]: culling | RBF | segmented reduction + stores | descent walk (within the search)
 //   ev[2]: lane-evaluations through the closest-feature search | those whose
 //          hull won the lane | lanes spared the search by the h_max bound | -
-__shared__ unsigned long long fsdf_wave_ev[kBlock / 64][3];
-__shared__ bool fsdf_wt_slow[kBlock];  // per lane: the last hull_sdf ran its search
-__shared__ unsigned long long fsdf_wave_ph[kBlock / 64][2];
+__shared__ unsigned long long fsdf_wave_ev[kPassBlock / 64][3];
+__shared__ bool fsdf_wt_slow[kPassBlock];  // per lane: the last hull_sdf ran its search
+__shared__ unsigned long long fsdf_wave_ph[kPassBlock / 64][2];
 //   ph2[0]: 10-ns units in walk certificates | walk closest points | vertex-
 //           region lane-certificates | fan iterations (max over lanes, per step)
 //   ph2[1]: 10-ns units in the screen loop | screen fix-up | edge-region
 //           lane-certificates | interior-region lane-certificates
-__shared__ unsigned long long fsdf_wave_ph2[kBlock / 64][2];
+__shared__ unsigned long long fsdf_wave_ph2[kPassBlock / 64][2];
 #endif
 __device__ __forceinline__ uint64_t wt_now() {
 #if FSDF_WAVE_TIMES
@@ -1515,7 +1515,9 @@ static_assert(kHpart == 2 || kHpart == 4, "FSDF_HPART is 2 or 4");
 // serial evaluations are spread over kHpart waves where a one-wave-per-chunk
 // grid would leave most wave slots idle.
 template <typename T, int SLOTS, bool CULL, bool RBF, bool ALIAS = false, bool HPART = false>
-__global__ __launch_bounds__(kPassBlock, (SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)) void pass_kernel(
+// (occupancy target in waves per SIMD, whatever the workgroup size)
+__global__ __launch_bounds__(kPassBlock) __attribute__((
+    amdgpu_waves_per_eu((SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)))) void pass_kernel(
     const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out) {
   static_assert(!ALIAS || (SLOTS == 1 && !RBF), "aliased wrench rows: hull-only, <= 64 surfaces");
   static_assert(!HPART || ALIAS, "the hull-partitioned pass is an aliased pass");

@@ -1202,7 +1202,8 @@ template <typename T, int SLOTS, bool CULL, bool RBF, bool P64 = false>
 __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const PassModel<T>& m,
                                            const HullRow* __restrict__ ht, float smax, T* __restrict__ lw,
                                            unsigned long long* __restrict__ stats, T& best, int& bk, T& gx, T& gy,
-                                           T& gz, const F4* __restrict__ cws = nullptr, uint64_t partmask = ~0ull) {
+                                           T& gz, const F4* __restrict__ cws = nullptr, uint64_t partmask = ~0ull,
+                                           double* shbest = nullptr, int part = 0, int nshare = 1) {
   // partmask (hull-partitioned pass, pass_kernel HPART): this wave evaluates
   // only the hulls whose bit (k & 63) is set; culling and the upper bound
   // still use every hull
@@ -1315,9 +1316,25 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   // by more than the fp32 rounding margin
   // hull k is needed by a lane unless |p-c_k| - r_k > min(ub, best) + mrg,
   // tested without a sqrt: |p-c_k|^2 <= (min(ub, best) + mrg + r_k)^2
+  // (HPART) the best distances the chunk's other waves have found so far, per
+  // lane, published in LDS: any of them is an upper bound of d* — as exact-safe
+  // a pruning bound as this wave's own best (stale reads only bound less)
+  auto bound_now = [&]() -> T {
+    T b = best;
+    if (shbest) {
+      const volatile double* sv = shbest + lane;
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        if (w < nshare) {
+          const T o = (T)sv[64 * w];
+          b = o < b ? o : b;
+        }
+    }
+    return b;
+  };
   auto needs = [&](int k) -> bool {
     if (!CULL) return valid;
-    return valid & needs_at(ht[k], pxf, pyf, pzf, fminf(ub, (float)best) + mrg);
+    return valid & needs_at(ht[k], pxf, pyf, pzf, fminf(ub, (float)bound_now()) + mrg);
   };
   // evaluations may run out of index order: ties keep the smaller k
 #if FSDF_WAVE_TIMES
@@ -1327,7 +1344,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     wt_count(0, 1);
     wt_count(5, __builtin_popcountll(__ballot(need)));
     T dk, hx, hy, hz;
-    hull_sdf<T, P64>(px, py, pz, k, m, ht, need, best, dk, hx, hy, hz, lw, stats);
+    hull_sdf<T, P64>(px, py, pz, k, m, ht, need, bound_now(), dk, hx, hy, hz, lw, stats);
 #if FSDF_WAVE_TIMES
     if (fsdf_wt_slow[threadIdx.x]) wt_slowk |= 1ull << (k & 63);
 #endif
@@ -1340,6 +1357,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     }
     const int ks = RBF ? m.hull_surface[k] : k;
     if (need && (dk < best || (dk == best && ks < bk))) { best = dk; bk = ks; gx = hx; gy = hy; gz = hz; }
+    if (shbest) ((volatile double*)shbest)[64 * part + lane] = (double)best;
   };
   uint64_t done[SLOTS];
 #pragma unroll
@@ -1590,9 +1608,16 @@ __global__ __launch_bounds__(kPassBlock) __attribute__((
     T best, gx, gy, gz;
     int bk;
     const F4* cws = out.chunk_ws ? (const F4*)out.chunk_ws + (base >> 6) : nullptr;
+    double* shb = nullptr;
+    if constexpr (HPART) {  // the chunk's shared per-lane bests, after the stages
+      shb = (double*)((char*)(ht + m.K + 1) + (kPassBlock / 64) * m.stage_bytes) + 64 * kParts * cw;
+      ((volatile double*)shb)[64 * part + lane] = __builtin_huge_val();
+      __syncthreads();
+    }
     scene_eval<T, SLOTS, CULL, RBF, ALIAS>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz, cws,
                                            HPART ? ((kParts == 4 ? 0x1111111111111111ull : 0x5555555555555555ull) << part)
-                                                 : ~0ull);
+                                                 : ~0ull,
+                                           shb, part, kParts);
     if constexpr (HPART) {
       // the chunk's waves' results meet in their stages; part 0 keeps the
       // lexicographic (d, k) minimum per point
@@ -1870,6 +1895,9 @@ __global__ void to_f32_kernel(const double* __restrict__ src, float* __restrict_
 // ---------------------------------------------------------------------------
 // Launchers
 // ---------------------------------------------------------------------------
+// the aliased pass's LDS plus the hull-partitioned pass's shared per-lane bests
+static size_t hpart_lds_bytes(const LocalModel& lm) { return pass_lds_bytes(lm, false, true) + kPassBlock * sizeof(double); }
+
 #ifndef FSDF_HPART_POINTS
 #define FSDF_HPART_POINTS 131072
 #endif
@@ -1881,7 +1909,8 @@ bool hpart_pass(const LocalModel& lm, int64_t n) {
     return e ? (int64_t)atoll(e) : (int64_t)FSDF_HPART_POINTS;
   }();
   return FSDF_RED_IN_STAGE && lm.planes64 && lm.S <= 64 && lm.R == 0 && n > 0 && n <= limit &&
-         (n + kPassBlock / kHpart - 1) / (kPassBlock / kHpart) <= kMaxBlocks;
+         (n + kPassBlock / kHpart - 1) / (kPassBlock / kHpart) <= kMaxBlocks &&
+         hpart_lds_bytes(lm) <= (size_t)kLdsPerCu * kPassBlock / 1024;  // (4 waves per SIMD)
 }
 
 int pass_blocks(int64_t n, const LocalModel& lm) {
@@ -1971,7 +2000,7 @@ static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void
   if constexpr (!RBF && FSDF_RED_IN_STAGE) {
     // one chunk per wave: the wrench rows alias the stage (pass_kernel ALIAS)
     if (hpart_pass(lm, n)) {
-      launch_lds(pass_kernel<T, 1, CULL, false, true, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
+      launch_lds(pass_kernel<T, 1, CULL, false, true, true>, nblocks, kPassBlock, hpart_lds_bytes(lm), s,
                  pts, n, m, out);
       return;
     }
@@ -1998,7 +2027,7 @@ static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm,
 #if FSDF_BENCH_ONLY
   const PassModel<T> m = pass_model<T>(lm, pm);
   if (hpart_pass(lm, n))
-    launch_lds(pass_kernel<T, 1, true, false, true, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
+    launch_lds(pass_kernel<T, 1, true, false, true, true>, nblocks, kPassBlock, hpart_lds_bytes(lm), s,
                (const T*)d_pts, n, m, out);
   else if (FSDF_RED_IN_STAGE && lm.planes64 && (int64_t)nblocks * kPassBlock >= n)
     launch_lds(pass_kernel<T, 1, true, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,

@@ -1198,12 +1198,12 @@ __device__ __forceinline__ void rbf_adjoint(T px, T py, T pz, const T* __restric
 // gradient. Wave-cooperative (ballots, LDS staging): call with the whole wave
 // active; `valid` marks lanes whose result is used.
 // ---------------------------------------------------------------------------
-template <typename T, int SLOTS, bool CULL, bool RBF, bool P64 = false>
+template <typename T, int SLOTS, bool CULL, bool RBF, bool P64 = false, int NSHARE = 1>
 __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const PassModel<T>& m,
                                            const HullRow* __restrict__ ht, float smax, T* __restrict__ lw,
                                            unsigned long long* __restrict__ stats, T& best, int& bk, T& gx, T& gy,
                                            T& gz, const F4* __restrict__ cws = nullptr, uint64_t partmask = ~0ull,
-                                           double* shbest = nullptr, int part = 0, int nshare = 1) {
+                                           double* shbest = nullptr, int part = 0) {
   // partmask (hull-partitioned pass, pass_kernel HPART): this wave evaluates
   // only the hulls whose bit (k & 63) is set; culling and the upper bound
   // still use every hull
@@ -1272,9 +1272,11 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
       atomicAdd(stats + 8, nc);
     }
     // per lane over the candidates: ub = min_k |p-c_k| and the best-first seed
+    // (hull-partitioned pass: over this wave's part only — its ub is still an
+    // upper bound of d*, and the chunk's waves share their bests anyway)
 #pragma unroll
     for (int s = 0; s < SLOTS; ++s) {
-      uint64_t cm = cand[s];
+      uint64_t cm = cand[s] & partmask;
       while (cm) {
         const int k = 64 * s + __builtin_ctzll(cm);
         cm &= cm - 1;
@@ -1284,7 +1286,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
         ub2 = fminf(ub2, dist2);
         // seed: the least lower bound (sphere or box)
         const float lb = fmaxf(__builtin_sqrtf(dist2) - sp[3], box_lower(ht[k], pxf, pyf, pzf));
-        if (((partmask >> (k & 63)) & 1) && lb < lb_min) { lb_min = lb; kseed = k; }
+        if (lb < lb_min) { lb_min = lb; kseed = k; }
       }
     }
   }
@@ -1321,14 +1323,13 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   // a pruning bound as this wave's own best (stale reads only bound less)
   auto bound_now = [&]() -> T {
     T b = best;
-    if (shbest) {
+    if constexpr (NSHARE > 1) {
       const volatile double* sv = shbest + lane;
 #pragma unroll
-      for (int w = 0; w < 4; ++w)
-        if (w < nshare) {
-          const T o = (T)sv[64 * w];
-          b = o < b ? o : b;
-        }
+      for (int w = 0; w < NSHARE; ++w) {
+        const T o = (T)sv[64 * w];
+        b = o < b ? o : b;
+      }
     }
     return b;
   };
@@ -1357,7 +1358,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     }
     const int ks = RBF ? m.hull_surface[k] : k;
     if (need && (dk < best || (dk == best && ks < bk))) { best = dk; bk = ks; gx = hx; gy = hy; gz = hz; }
-    if (shbest) ((volatile double*)shbest)[64 * part + lane] = (double)best;
+    if constexpr (NSHARE > 1) ((volatile double*)shbest)[64 * part + lane] = (double)best;
   };
   uint64_t done[SLOTS];
 #pragma unroll
@@ -1614,10 +1615,12 @@ __global__ __launch_bounds__(kPassBlock) __attribute__((
       ((volatile double*)shb)[64 * part + lane] = __builtin_huge_val();
       __syncthreads();
     }
-    scene_eval<T, SLOTS, CULL, RBF, ALIAS>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz, cws,
-                                           HPART ? ((kParts == 4 ? 0x1111111111111111ull : 0x5555555555555555ull) << part)
-                                                 : ~0ull,
-                                           shb, part, kParts);
+    scene_eval<T, SLOTS, CULL, RBF, ALIAS, kParts>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy,
+                                                   gz, cws,
+                                                   HPART ? ((kParts == 4 ? 0x1111111111111111ull : 0x5555555555555555ull)
+                                                            << part)
+                                                         : ~0ull,
+                                                   shb, part);
     if constexpr (HPART) {
       // the chunk's waves' results meet in their stages; part 0 keeps the
       // lexicographic (d, k) minimum per point

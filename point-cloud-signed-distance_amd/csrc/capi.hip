@@ -1327,7 +1327,11 @@ extern "C" int fsdf_profile_pass(fsdf_ctx* c, int32_t enable) {
   HIPCHECK(c, hipSetDevice(c->device));
   if (enable && c->prof_ev.empty()) {
     c->prof_ev.resize(3 * 4096, nullptr);
-    for (auto& e : c->prof_ev) HIPCHECK(c, hipEventCreate(&e));
+    // timing-only events: a default event record is a system-scope release
+    // (the whole L2 written back), which put ~10 us between the pass and the
+    // reduce of every profiled pass; fsdf_pass_times synchronizes the stream
+    // before reading them
+    for (auto& e : c->prof_ev) HIPCHECK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
   }
   c->profiling = enable != 0;
   c->prof_used = 0;

@@ -360,7 +360,7 @@ def main():
                 "bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": hbm_achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": "pass_kernel", "kernel_ms": kernel_avg_ms,
-                "whole_pass_ms": pass_avg_ms,
+                "pass_and_reduce_ms": pass_avg_ms,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "valu_issue_frac": issue,
                 "valu_effective": {"flop_per_eval": f_alg, "achieved_tflops": eff_tflops, "peak_tflops": peak_valu,

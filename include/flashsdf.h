@@ -291,13 +291,14 @@ int fsdf_get_permutation_device(fsdf_ctx* ctx, int64_t* d_perm_out);
 int fsdf_synchronize(fsdf_ctx* ctx);
 
 /* ---- measurement ------------------------------------------------------------
- * With profiling enabled, every residual pass records HIP events on the
- * context stream before the pass kernel (the dominant launch), after it, and
- * again after it (a whole-pass bracket kept for the pose/pass/reduce
- * accounting). fsdf_pass_times synchronizes, returns the summed pass-kernel
- * time, the summed whole-pass time of the passes recorded
- * since the last query and their count, and resets the record;
- * fsdf_pass_time returns the whole-pass sum only. */
+ * With profiling enabled, every residual pass stamps HIP events at the start
+ * and end of the pass kernel (the dominant launch) and at the end of the
+ * reduction that follows it, through the kernel dispatches themselves
+ * (hipExtLaunchKernel: no event packets between the kernels, so profiling
+ * leaves the step's timing alone). fsdf_pass_times synchronizes, returns the
+ * summed pass-kernel time, the summed pass + reduction time of the passes
+ * recorded since the last query and their count, and resets the record;
+ * fsdf_pass_time returns the pass + reduction sum only. */
 int fsdf_profile_pass(fsdf_ctx* ctx, int32_t enable);
 int fsdf_pass_times(fsdf_ctx* ctx, double* kernel_ms_out, double* pass_ms_out, int64_t* launches_out);
 int fsdf_pass_time(fsdf_ctx* ctx, double* total_ms_out, int64_t* launches_out);

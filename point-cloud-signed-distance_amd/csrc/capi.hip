@@ -836,22 +836,22 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
     out.order = c->order_nblocks == nblocks ? c->d_block_order : nullptr;
   }
   if (n > 0) {
+    // profiling: the pass kernel's start / end and the reduce's end, stamped
+    // by the dispatches themselves (no packets of their own between kernels)
     const bool prof = c->profiling && c->prof_used + 3 <= c->prof_ev.size();
-    if (prof) HIPCHECK(c, hipEventRecord(c->prof_ev[c->prof_used], c->stream));
-    HIPCHECK(c, fsdf::launch_pass(c->precision, c->cull != 0, c->lm, *P, d_pts, n, nblocks, out, c->stream));
-    if (prof) HIPCHECK(c, hipEventRecord(c->prof_ev[c->prof_used + 1], c->stream));
+    hipEvent_t* pe = prof ? &c->prof_ev[c->prof_used] : nullptr;
+    HIPCHECK(c, fsdf::launch_pass(c->precision, c->cull != 0, c->lm, *P, d_pts, n, nblocks, out, c->stream,
+                                  pe ? pe[0] : nullptr, pe ? pe[1] : nullptr));
     rc = release_posed(c, pbuf);
     if (rc) return rc;
-    if (prof) {
-      HIPCHECK(c, hipEventRecord(c->prof_ev[c->prof_used + 2], c->stream));
-      c->prof_used += 3;
-    }
+    if (prof) c->prof_used += 3;
     // the order is rebuilt on the first scheduled pass of a grid and then every
     // kOrderEvery passes (the heavy blocks of a cloud stay heavy from pass to
     // pass; the rebuild is a ~7 us single-workgroup sort on the reduce launch)
     const bool rebuild = out.cost && (c->order_nblocks != nblocks || ++c->order_age >= kOrderEvery);
     HIPCHECK(c, fsdf::launch_reduce(c->d_partials, nblocks, accum_len(c), d_accum, c->stream,
-                                    rebuild ? out.cost : nullptr, rebuild ? c->d_block_order : nullptr));
+                                    rebuild ? out.cost : nullptr, rebuild ? c->d_block_order : nullptr,
+                                    pe ? pe[2] : nullptr));
     if (rebuild) {
       c->order_nblocks = nblocks;
       c->order_age = 0;

@@ -138,9 +138,11 @@ struct PoseArgs {
 hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_poses,
                        const PosedModel& pm, hipStream_t s, const double* h_poses = nullptr);
 
+// ev_start / ev_stop (optional): timing events stamped by the pass kernel's
+// dispatch itself (hipExtLaunchKernel), not by packets of their own
 hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm,
                        const void* d_pts, int64_t n, int nblocks, const PassOutputs& out,
-                       hipStream_t s);
+                       hipStream_t s, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 
 // origin: 3 host doubles (passed by value); d_rays [n][3] f64 unit directions.
 hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const double* origin,
@@ -149,7 +151,8 @@ hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const 
 // With cost/order: one extra workgroup also rebuilds order[] (heaviest logical
 // blocks first) from this pass's costs, for the next pass of the same grid.
 hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum,
-                         hipStream_t s, const uint32_t* cost = nullptr, int32_t* order = nullptr);
+                         hipStream_t s, const uint32_t* cost = nullptr, int32_t* order = nullptr,
+                         hipEvent_t ev_stop = nullptr);
 
 hipError_t launch_to_f32(const double* src, float* dst, int64_t count, hipStream_t s);
 

@@ -31,6 +31,8 @@
 
 #include "fsdf_internal.h"
 
+#include <hip/hip_ext.h>
+
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1988,10 +1990,21 @@ size_t pass_lds_bytes(const LocalModel& lm, bool raycast, bool alias) {
   return red + rbf + stage;
 }
 
+// start/stop events of the next pass launch (launch_pass; this thread only):
+// hipExtLaunchKernel stamps them in the dispatch itself, where a separate
+// hipEventRecord is a stream packet of its own that held the next kernel
+// back by ~5-10 us (profiles/r03, step_trace)
+static thread_local hipEvent_t g_pass_ev0 = nullptr, g_pass_ev1 = nullptr;
+
 template <typename K, typename... Args>
 static void launch_lds(K kernel, int grid, int block, size_t lds, hipStream_t s, Args... args) {
   if (lds > 65536) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), lds, s, args...);
+  if (g_pass_ev0 || g_pass_ev1) {
+    hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(block), (uint32_t)lds, s, g_pass_ev0, g_pass_ev1, 0u, args...);
+    g_pass_ev0 = g_pass_ev1 = nullptr;
+  } else {
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), lds, s, args...);
+  }
 }
 
 template <typename T, bool CULL, bool RBF>
@@ -2050,7 +2063,10 @@ static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm,
 }
 
 hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const void* d_pts,
-                       int64_t n, int nblocks, const PassOutputs& out, hipStream_t s) {
+                       int64_t n, int nblocks, const PassOutputs& out, hipStream_t s, hipEvent_t ev_start,
+                       hipEvent_t ev_stop) {
+  g_pass_ev0 = ev_start;
+  g_pass_ev1 = ev_stop;
 #if FSDF_BENCH_ONLY
   if (precision != 64 || !cull || lm.R > 0 || lm.S > 64) return hipErrorNotSupported;
   launch_pass_p<double>(cull, lm, pm, d_pts, n, nblocks, out, s);
@@ -2098,9 +2114,13 @@ hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const 
 }
 
 hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum, hipStream_t s,
-                         const uint32_t* cost, int32_t* order) {
-  hipLaunchKernelGGL(reduce_tiles_kernel, dim3((len + 7) / 8), dim3(kTileBlock), 0, s, partials, nblocks, len,
-                     d_accum);
+                         const uint32_t* cost, int32_t* order, hipEvent_t ev_stop) {
+  if (ev_stop)
+    hipExtLaunchKernelGGL(reduce_tiles_kernel, dim3((len + 7) / 8), dim3(kTileBlock), 0u, s, nullptr, ev_stop, 0u,
+                          partials, nblocks, len, d_accum);
+  else
+    hipLaunchKernelGGL(reduce_tiles_kernel, dim3((len + 7) / 8), dim3(kTileBlock), 0, s, partials, nblocks, len,
+                       d_accum);
   if (cost) hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kBlock), 0, s, cost, nblocks, order);
   return hipGetLastError();
 }

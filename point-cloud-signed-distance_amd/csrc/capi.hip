@@ -566,7 +566,7 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
     else HIPCHECK(c, dalloc((char**)&c->pm.rbf_rows, (size_t)nrows * 4 * sizeof(float)));
     for (int i = 0; i < kPoseRing; ++i) {
       HIPCHECK(c, hipHostMalloc((void**)&c->h_rbf[i], (size_t)nrows * 4 * sizeof(double), hipHostMallocDefault));
-      if (!c->rbf_ev[i]) HIPCHECK(c, hipEventCreateWithFlags(&c->rbf_ev[i], hipEventDisableTiming));
+      if (!c->rbf_ev[i]) HIPCHECK(c, hipEventCreateWithFlags(&c->rbf_ev[i], hipEventDisableTiming | hipEventDisableSystemFence));
     }
   }
   HIPCHECK(c, hipMemcpy(c->d_verts_l, verts.data(), verts.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -585,7 +585,7 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
     if (c->h_poses[i]) (void)hipHostFree(c->h_poses[i]);
     c->h_poses[i] = nullptr;
     HIPCHECK(c, hipHostMalloc((void**)&c->h_poses[i], (size_t)S * 12 * sizeof(double), hipHostMallocDefault));
-    if (!c->pose_ev[i]) HIPCHECK(c, hipEventCreateWithFlags(&c->pose_ev[i], hipEventDisableTiming));
+    if (!c->pose_ev[i]) HIPCHECK(c, hipEventCreateWithFlags(&c->pose_ev[i], hipEventDisableTiming | hipEventDisableSystemFence));
   }
   c->lm.K = K;
   c->lm.F = F;
@@ -642,6 +642,7 @@ extern "C" int fsdf_set_rbf_params(fsdf_ctx* c, const double* params, int64_t n)
     if (!std::isfinite(params[i])) return fail(c, FSDF_ERR_ARG, "set_rbf_params: entry %lld not finite", (long long)i);
   HIPCHECK(c, hipSetDevice(c->device));
   // own ring: the slot is reused only after the copy that last read it ran
+  // (the ring events only mark a copy's completion: no system-scope fence)
   // (an asynchronous caller may queue several passes with different rows)
   const int sl = c->rbf_slot;
   c->rbf_slot = (sl + 1) % kPoseRing;

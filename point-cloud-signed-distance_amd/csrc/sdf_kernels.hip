@@ -422,7 +422,8 @@ constexpr int kMaxRbfAcc = kMaxRbfAccum;
 //   ph[0]: 10-ns units in hull staging | screen | fast path | closest-feature search
 //   ph[1]: culling | RBF | segmented reduction + stores | descent walk (within the search)
 //   ev[2]: lane-evaluations through the closest-feature search | those whose
-//          hull won the lane | lanes spared the search by the h_max bound | -
+//          hull won the lane | lanes spared the search by the h_max bound |
+//          10-ns units in the candidate need tests of phase C
 __shared__ unsigned long long fsdf_wave_ev[kPassBlock / 64][3];
 __shared__ bool fsdf_wt_slow[kPassBlock];  // per lane: the last hull_sdf ran its search
 __shared__ unsigned long long fsdf_wave_ph[kPassBlock / 64][2];
@@ -1397,8 +1398,16 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
       if (!cm) break;
       k = 64 * slot + __builtin_ctzll(cm);
       cm &= cm - 1;
+#if FSDF_WAVE_TIMES
+      const uint64_t tw_need = wt_now();
+      need = needs(k);
+      const bool any_need = __any(need);
+      wt_count(11, wt_now() - tw_need);
+      if (!any_need) continue;
+#else
       need = needs(k);
       if (!__any(need)) continue;
+#endif
     }
     evaluate(k, need);
   }

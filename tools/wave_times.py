@@ -56,7 +56,7 @@ def main():
     evf = fields(ev_raw)  # evals, rejects, slow, walk steps, seeds, need lanes, candidates, full scans
     phf = fields(ph) * 0.01  # us: stage, screen, fast, search, cull, rbf, emit, -
     e2 = buf[32 + 26 * 16384:32 + 26 * 16384 + min(nw, 4 * 16384)].astype(np.uint64)
-    ev2 = np.stack([(e2 >> np.uint64(16 * j)) & np.uint64(0xffff) for j in range(3)], 1).astype(np.int64)
+    ev2 = np.stack([(e2 >> np.uint64(16 * j)) & np.uint64(0xffff) for j in range(4)], 1).astype(np.int64)
     # slow lane-evaluations | of which the hull won the lane | lanes spared the search by h_max
     nw2 = min(nw, 16384)
     p2 = buf[32 + 30 * 16384:32 + 30 * 16384 + 2 * nw2].reshape(-1, 2).astype(np.uint64)
@@ -108,7 +108,7 @@ def main():
     ne = max(int(evf[:, 0].sum()), 1)
     res["per_eval_us"] = {n: round(float(phf[:, j].sum() / ne), 3) for j, n in enumerate(ph_names[:4])}
     res["event_totals"] = {n: int(evf[:, j].sum()) for j, n in enumerate(ev_names)}
-    e2n = ["slow_lane_evals", "slow_lane_evals_won", "lanes_spared_by_hmax"]
+    e2n = ["slow_lane_evals", "slow_lane_evals_won", "lanes_spared_by_hmax", "t_needs_phase_c_10ns"]
     res["search_lanes"] = {n: int(ev2[:, j].sum()) for j, n in enumerate(e2n)}
     for i, r in zip(heavy, res["heaviest_detail"]):
         r.update({n: int(ev2[i, j]) for j, n in enumerate(e2n)})

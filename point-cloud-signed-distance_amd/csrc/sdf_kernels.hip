@@ -409,6 +409,16 @@ __device__ __forceinline__ float load_hull_table(const PassModel<T>& m, HullRow*
 }
 
 constexpr int kMaxRbfAcc = kMaxRbfAccum;
+#ifndef FSDF_HPART
+#define FSDF_HPART 4
+#endif
+constexpr int kHpart = FSDF_HPART;  // waves per chunk in the hull-partitioned pass (2 or 4)
+static_assert(kHpart == 2 || kHpart == 4, "FSDF_HPART is 2 or 4");
+// workgroups of the hull-partitioned and the one-chunk-per-wave pass
+// (pass_kernel NB; 512-thread workgroups measured slower for both)
+constexpr int kHpartBlock = kPassBlock;
+constexpr int kAliasBlock = kPassBlock;
+
 // The one diagnostic build (-DFSDF_WAVE_TIMES=1, tools/wave_times.py): a
 // per-wave timeline with per-phase 100 MHz clocks and event counts; every hook
 // below compiles to nothing in the product library.
@@ -424,14 +434,15 @@ constexpr int kMaxRbfAcc = kMaxRbfAccum;
 //   ev[2]: lane-evaluations through the closest-feature search | those whose
 //          hull won the lane | lanes spared the search by the h_max bound |
 //          10-ns units in the candidate need tests of phase C
-__shared__ unsigned long long fsdf_wave_ev[kPassBlock / 64][3];
-__shared__ bool fsdf_wt_slow[kPassBlock];  // per lane: the last hull_sdf ran its search
-__shared__ unsigned long long fsdf_wave_ph[kPassBlock / 64][2];
+constexpr int kWtWaves = kPassBlock / 64;
+__shared__ unsigned long long fsdf_wave_ev[kWtWaves][3];
+__shared__ bool fsdf_wt_slow[64 * kWtWaves];  // per lane: the last hull_sdf ran its search
+__shared__ unsigned long long fsdf_wave_ph[kWtWaves][2];
 //   ph2[0]: 10-ns units in walk certificates | walk closest points | vertex-
 //           region lane-certificates | fan iterations (max over lanes, per step)
 //   ph2[1]: 10-ns units in the screen loop | screen fix-up | edge-region
 //           lane-certificates | interior-region lane-certificates
-__shared__ unsigned long long fsdf_wave_ph2[kPassBlock / 64][2];
+__shared__ unsigned long long fsdf_wave_ph2[kWtWaves][2];
 #endif
 __device__ __forceinline__ uint64_t wt_now() {
 #if FSDF_WAVE_TIMES
@@ -1206,7 +1217,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
                                            const HullRow* __restrict__ ht, float smax, T* __restrict__ lw,
                                            unsigned long long* __restrict__ stats, T& best, int& bk, T& gx, T& gy,
                                            T& gz, const F4* __restrict__ cws = nullptr, uint64_t partmask = ~0ull,
-                                           double* shbest = nullptr, int part = 0) {
+                                           double* shbest = nullptr) {
   // partmask (hull-partitioned pass, pass_kernel HPART): this wave evaluates
   // only the hulls whose bit (k & 63) is set; culling and the upper bound
   // still use every hull
@@ -1321,24 +1332,23 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   // by more than the fp32 rounding margin
   // hull k is needed by a lane unless |p-c_k| - r_k > min(ub, best) + mrg,
   // tested without a sqrt: |p-c_k|^2 <= (min(ub, best) + mrg + r_k)^2
-  // (HPART) the best distances the chunk's other waves have found so far, per
-  // lane, published in LDS: any of them is an upper bound of d* — as exact-safe
-  // a pruning bound as this wave's own best (stale reads only bound less)
+  // (HPART) the least best distance the chunk's waves have found so far, per
+  // lane, one LDS slot kept by ds_min_f64: an upper bound of d* — as exact-safe
+  // a pruning bound as this wave's own best (a stale read only bounds less).
+  // (One slot read per test: 2.6 % faster at 2^17 than a slot per wave, a
+  // cached copy refreshed per evaluation no faster; profiles/r03/experiments)
   auto bound_now = [&]() -> T {
     T b = best;
     if constexpr (NSHARE > 1) {
-      const volatile double* sv = shbest + lane;
-#pragma unroll
-      for (int w = 0; w < NSHARE; ++w) {
-        const T o = (T)sv[64 * w];
-        b = o < b ? o : b;
-      }
+      const T o = (T)((const volatile double*)shbest)[lane];
+      b = o < b ? o : b;
     }
     return b;
   };
   auto needs = [&](int k) -> bool {
     if (!CULL) return valid;
-    return valid & needs_at(ht[k], pxf, pyf, pzf, fminf(ub, (float)bound_now()) + mrg);
+    const T b = bound_now();
+    return valid & needs_at(ht[k], pxf, pyf, pzf, fminf(ub, (float)b) + mrg);
   };
   // evaluations may run out of index order: ties keep the smaller k
 #if FSDF_WAVE_TIMES
@@ -1361,7 +1371,8 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     }
     const int ks = RBF ? m.hull_surface[k] : k;
     if (need && (dk < best || (dk == best && ks < bk))) { best = dk; bk = ks; gx = hx; gy = hy; gz = hz; }
-    if constexpr (NSHARE > 1) ((volatile double*)shbest)[64 * part + lane] = (double)best;
+    if constexpr (NSHARE > 1)  // (one slot per lane: the minimum over the chunk's waves, ds_min_f64)
+      __hip_atomic_fetch_min(shbest + lane, (double)best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
   uint64_t done[SLOTS];
 #pragma unroll
@@ -1523,11 +1534,6 @@ __device__ __forceinline__ int64_t pidx(int t, int b, int nblocks) {
 // Residual pass.
 // ---------------------------------------------------------------------------
 extern __shared__ __attribute__((aligned(16))) char fsdf_lds[];
-#ifndef FSDF_HPART
-#define FSDF_HPART 4
-#endif
-constexpr int kHpart = FSDF_HPART;  // waves per chunk in the hull-partitioned pass (2 or 4)
-static_assert(kHpart == 2 || kHpart == 4, "FSDF_HPART is 2 or 4");
 
 // ALIAS (one chunk per wave: n <= grid * 256; hull-only, <= 64 surfaces; f64
 // models with LocalModel::planes64): the wave's wrench rows live in its own
@@ -1544,15 +1550,15 @@ static_assert(kHpart == 2 || kHpart == 4, "FSDF_HPART is 2 or 4");
 // chunk's waves is the full scene's — bit for bit. The heaviest chunks'
 // serial evaluations are spread over kHpart waves where a one-wave-per-chunk
 // grid would leave most wave slots idle.
-template <typename T, int SLOTS, bool CULL, bool RBF, bool ALIAS = false, bool HPART = false>
-// (occupancy target in waves per SIMD, whatever the workgroup size)
-__global__ __launch_bounds__(kPassBlock) __attribute__((
+template <typename T, int SLOTS, bool CULL, bool RBF, bool ALIAS = false, bool HPART = false, int NB = kPassBlock>
+// (occupancy target in waves per SIMD, whatever the workgroup size NB)
+__global__ __launch_bounds__(NB) __attribute__((
     amdgpu_waves_per_eu((SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)))) void pass_kernel(
     const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out) {
   static_assert(!ALIAS || (SLOTS == 1 && !RBF), "aliased wrench rows: hull-only, <= 64 surfaces");
   static_assert(!HPART || ALIAS, "the hull-partitioned pass is an aliased pass");
   constexpr int kParts = HPART ? kHpart : 1;
-  constexpr int kChunkStride = kPassBlock / kParts;  // points per logical block
+  constexpr int kChunkStride = NB / kParts;  // points per logical block
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   // (wave-uniform: readfirstlane keeps the hull mask and the loops scalar)
@@ -1568,7 +1574,7 @@ __global__ __launch_bounds__(kPassBlock) __attribute__((
   // lane `lane` (hull s*64 + lane)
   constexpr int kRedStride = SLOTS * 64 * 6 + 2;
   double* red = (double*)fsdf_lds;
-  HullRow* ht = (HullRow*)(fsdf_lds + (ALIAS ? 0 : ((kPassBlock / 64) * kRedStride + (RBF ? (kPassBlock / 64) * kMaxRbfAcc : 0)) * 8));
+  HullRow* ht = (HullRow*)(fsdf_lds + (ALIAS ? 0 : ((NB / 64) * kRedStride + (RBF ? (NB / 64) * kMaxRbfAcc : 0)) * 8));
   T* stage = (T*)((char*)(ht + m.K + 1) + wave * m.stage_bytes);
   auto red_of = [&](int w) -> double* {
     return ALIAS ? (double*)((char*)(ht + m.K + 1) + w * m.stage_bytes) : red + w * kRedStride;
@@ -1583,7 +1589,7 @@ __global__ __launch_bounds__(kPassBlock) __attribute__((
   if (!ALIAS) zero_rows();
   double cost_acc = 0.0;
   // RBF adjoint sums of this wave (lane 0 adds)
-  double* rbf_acc = red + (kPassBlock / 64) * kRedStride;
+  double* rbf_acc = red + (NB / 64) * kRedStride;
   double* rbf_wave = rbf_acc + wave * kMaxRbfAcc;
   const int stage_cap = m.stage_bytes / (4 * (int)sizeof(T));
   if (RBF)
@@ -1622,16 +1628,18 @@ __global__ __launch_bounds__(kPassBlock) __attribute__((
     const F4* cws = out.chunk_ws ? (const F4*)out.chunk_ws + (base >> 6) : nullptr;
     double* shb = nullptr;
     if constexpr (HPART) {  // the chunk's shared per-lane bests, after the stages
-      shb = (double*)((char*)(ht + m.K + 1) + (kPassBlock / 64) * m.stage_bytes) + 64 * kParts * cw;
-      ((volatile double*)shb)[64 * part + lane] = __builtin_huge_val();
+      shb = (double*)((char*)(ht + m.K + 1) + (NB / 64) * m.stage_bytes) + 64 * cw;
+      if (part == 0) ((volatile double*)shb)[lane] = __builtin_huge_val();
       __syncthreads();
     }
     scene_eval<T, SLOTS, CULL, RBF, ALIAS, kParts>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy,
                                                    gz, cws,
-                                                   HPART ? ((kParts == 4 ? 0x1111111111111111ull : 0x5555555555555555ull)
+                                                   HPART ? ((kParts == 8 ? 0x0101010101010101ull
+                                                                         : (kParts == 4 ? 0x1111111111111111ull
+                                                                                        : 0x5555555555555555ull))
                                                             << part)
                                                          : ~0ull,
-                                                   shb, part);
+                                                   shb);
     if constexpr (HPART) {
       // the chunk's waves' results meet in their stages; part 0 keeps the
       // lexicographic (d, k) minimum per point
@@ -1700,18 +1708,18 @@ __global__ __launch_bounds__(kPassBlock) __attribute__((
   __syncthreads();
   const int len6 = 1 + 6 * m.S;
   const int len = len6 + (RBF ? m.rbf_acc_off[m.R] : 0);
-  for (int t = threadIdx.x; t < len; t += kPassBlock) {
+  for (int t = threadIdx.x; t < len; t += NB) {
     double s;
     if (t < len6) {
       const int src = (t == 0) ? SLOTS * 64 * 6 : t - 1;
       s = red_of(0)[src];
 #pragma unroll
-      for (int w = 1; w < kPassBlock / 64; ++w) s += red_of(w)[src];
+      for (int w = 1; w < NB / 64; ++w) s += red_of(w)[src];
     } else {
       const int src = RBF ? t - len6 : 0;
       s = rbf_acc[src];
 #pragma unroll
-      for (int w = 1; w < kPassBlock / 64; ++w) s += rbf_acc[w * kMaxRbfAcc + src];
+      for (int w = 1; w < NB / 64; ++w) s += rbf_acc[w * kMaxRbfAcc + src];
     }
     out.partials[pidx(t, lb, gridDim.x)] = s;
   }
@@ -1910,7 +1918,10 @@ __global__ void to_f32_kernel(const double* __restrict__ src, float* __restrict_
 // Launchers
 // ---------------------------------------------------------------------------
 // the aliased pass's LDS plus the hull-partitioned pass's shared per-lane bests
-static size_t hpart_lds_bytes(const LocalModel& lm) { return pass_lds_bytes(lm, false, true) + kPassBlock * sizeof(double); }
+static size_t hpart_lds_bytes(const LocalModel& lm) {
+  return (size_t)(kHpartBlock / 64) * lm.stage_bytes + (size_t)(lm.K + 1) * sizeof(HullRow) +
+         (size_t)kHpartBlock / kHpart * sizeof(double);
+}
 
 #ifndef FSDF_HPART_POINTS
 #define FSDF_HPART_POINTS 131072
@@ -1923,12 +1934,20 @@ bool hpart_pass(const LocalModel& lm, int64_t n) {
     return e ? (int64_t)atoll(e) : (int64_t)FSDF_HPART_POINTS;
   }();
   return FSDF_RED_IN_STAGE && lm.planes64 && lm.S <= 64 && lm.R == 0 && n > 0 && n <= limit &&
-         (n + kPassBlock / kHpart - 1) / (kPassBlock / kHpart) <= kMaxBlocks &&
-         hpart_lds_bytes(lm) <= (size_t)kLdsPerCu * kPassBlock / 1024;  // (4 waves per SIMD)
+         (n + kHpartBlock / kHpart - 1) / (kHpartBlock / kHpart) <= kMaxBlocks &&
+         hpart_lds_bytes(lm) <= (size_t)kLdsPerCu * kHpartBlock / 1024;  // (4 waves per SIMD)
+}
+
+static bool alias_pass(const LocalModel& lm, int64_t n) {
+  return FSDF_RED_IN_STAGE && lm.planes64 && lm.S <= 64 && lm.R == 0 && n > 0 && (n + kAliasBlock - 1) / kAliasBlock <= kMaxBlocks;
+}
+static size_t alias_lds_bytes(const LocalModel& lm) {
+  return (size_t)(kAliasBlock / 64) * lm.stage_bytes + (size_t)(lm.K + 1) * sizeof(HullRow);
 }
 
 int pass_blocks(int64_t n, const LocalModel& lm) {
-  if (hpart_pass(lm, n)) return (int)((n + kPassBlock / kHpart - 1) / (kPassBlock / kHpart));
+  if (hpart_pass(lm, n)) return (int)((n + kHpartBlock / kHpart - 1) / (kHpartBlock / kHpart));
+  if (alias_pass(lm, n)) return (int)((n + kAliasBlock - 1) / kAliasBlock);
   int64_t b = (n + kPassBlock - 1) / kPassBlock;
   if (b < 1) b = 1;
   if (b > kMaxBlocks) b = kMaxBlocks;
@@ -2025,12 +2044,12 @@ static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void
   if constexpr (!RBF && FSDF_RED_IN_STAGE) {
     // one chunk per wave: the wrench rows alias the stage (pass_kernel ALIAS)
     if (hpart_pass(lm, n)) {
-      launch_lds(pass_kernel<T, 1, CULL, false, true, true>, nblocks, kPassBlock, hpart_lds_bytes(lm), s,
+      launch_lds(pass_kernel<T, 1, CULL, false, true, true, kHpartBlock>, nblocks, kHpartBlock, hpart_lds_bytes(lm), s,
                  pts, n, m, out);
       return;
     }
-    if (lm.S <= 64 && lm.planes64 && (int64_t)nblocks * kPassBlock >= n) {
-      launch_lds(pass_kernel<T, 1, CULL, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
+    if (alias_pass(lm, n) && (int64_t)nblocks * kAliasBlock >= n) {
+      launch_lds(pass_kernel<T, 1, CULL, false, true, false, kAliasBlock>, nblocks, kAliasBlock, alias_lds_bytes(lm), s,
                  pts, n, m, out);
       return;
     }
@@ -2052,10 +2071,10 @@ static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm,
 #if FSDF_BENCH_ONLY
   const PassModel<T> m = pass_model<T>(lm, pm);
   if (hpart_pass(lm, n))
-    launch_lds(pass_kernel<T, 1, true, false, true, true>, nblocks, kPassBlock, hpart_lds_bytes(lm), s,
+    launch_lds(pass_kernel<T, 1, true, false, true, true, kHpartBlock>, nblocks, kHpartBlock, hpart_lds_bytes(lm), s,
                (const T*)d_pts, n, m, out);
-  else if (FSDF_RED_IN_STAGE && lm.planes64 && (int64_t)nblocks * kPassBlock >= n)
-    launch_lds(pass_kernel<T, 1, true, false, true>, nblocks, kPassBlock, pass_lds_bytes(lm, false, true), s,
+  else if (alias_pass(lm, n) && (int64_t)nblocks * kAliasBlock >= n)
+    launch_lds(pass_kernel<T, 1, true, false, true, false, kAliasBlock>, nblocks, kAliasBlock, alias_lds_bytes(lm), s,
                (const T*)d_pts, n, m, out);
   else
     launch_lds(pass_kernel<T, 1, true, false>, nblocks, kPassBlock, pass_lds_bytes(lm, false), s, (const T*)d_pts,

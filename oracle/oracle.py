@@ -55,6 +55,12 @@ def load():
         lib.oracle_rbf_skin.argtypes = [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]
         lib.oracle_raycast.argtypes = [ctypes.POINTER(Posed), c_void_p, c_void_p, c_int64, c_void_p, c_int32]
         lib.oracle_max_threads.restype = c_int32
+        # fp32 instantiation (skin_impl.h with R = float): fp32 contexts bit for bit
+        lib.oracle_pose_model_f32.argtypes = [c_int32, c_int32, c_int32] + [c_void_p] * 11
+        lib.oracle_hull_sdf_f32.argtypes = [ctypes.POINTER(Posed), c_int32, c_void_p, c_void_p, c_void_p]
+        lib.oracle_skin_f32.argtypes = [ctypes.POINTER(Posed), c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                        c_int32]
+        lib.oracle_rbf_skin_f32.argtypes = [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]
         _lib = lib
     return _lib
 
@@ -136,18 +142,24 @@ class OracleModel:
                 surfaces.append(("rbf", len(s.surface_points) + len(s.skeleton_points)))
         return OracleModel(hulls, surfaces)
 
-    def pose(self, poses, rbf_rows=None):
-        """World-frame model arrays for `poses` ([S,12], one per surface)."""
+    def pose(self, poses, rbf_rows=None, precision: int = 64):
+        """World-frame model arrays for `poses` ([S,12], one per surface).
+        precision=32: the rows an fp32 context works on (computed in fp64 from
+        the fp64 poses, rounded once to fp32, edge records formed in fp32)."""
+        if precision not in (32, 64):
+            raise ValueError("precision is 32 or 64")
+        rt = np.float64 if precision == 64 else np.float32
         poses = np.ascontiguousarray(poses, np.float64).reshape(self.S, 12)
         hp = np.ascontiguousarray(poses[self.hull_surface]) if self.K else np.zeros((1, 12))
-        pw = np.empty((max(self.F, 1), 4))
-        fx = np.empty((max(self.F, 1), FX))
-        vw = np.empty((max(self.V, 1), 4))
-        hs = np.empty(max(self.K, 1))
-        load().oracle_pose_model(self.F, self.V, self.K, _p(self.verts_l), _p(self.faces), _p(self.planes_l),
-                                 _p(self.face_hull), _p(self.vert_hull), _p(self.vert_off), _p(hp), _p(pw),
-                                 _p(fx), _p(vw), _p(hs))
-        rr = np.ascontiguousarray(rbf_rows if rbf_rows is not None else np.zeros((1, 4)), np.float64)
+        pw = np.empty((max(self.F, 1), 4), rt)
+        fx = np.empty((max(self.F, 1), FX), rt)
+        vw = np.empty((max(self.V, 1), 4), rt)
+        hs = np.empty(max(self.K, 1), rt)
+        fn = load().oracle_pose_model if precision == 64 else load().oracle_pose_model_f32
+        fn(self.F, self.V, self.K, _p(self.verts_l), _p(self.faces), _p(self.planes_l),
+           _p(self.face_hull), _p(self.vert_hull), _p(self.vert_off), _p(hp), _p(pw),
+           _p(fx), _p(vw), _p(hs))
+        rr = np.ascontiguousarray(rbf_rows if rbf_rows is not None else np.zeros((1, 4)), rt)
         arrays = (pw, fx, vw, hs, rr)
         st = Posed(self.K, self.face_off.ctypes.data, self.vert_off.ctypes.data, self.nbr.ctypes.data,
                    pw.ctypes.data, fx.ctypes.data, vw.ctypes.data, hs.ctypes.data, self.S,
@@ -155,10 +167,23 @@ class OracleModel:
                    rr.ctypes.data, self.faces.ctypes.data)
         return st, arrays
 
-    def skin(self, poses, pts, threads: int = 0, rbf_rows=None, culled: bool = False):
+    def skin(self, poses, pts, threads: int = 0, rbf_rows=None, culled: bool = False, precision: int = 64):
         """Per-point (d*, k*, ∇d*). culled=True visits the hulls by a bounding-sphere
         lower bound and stops early (same results bit for bit; the CPU baseline's
-        culled leg)."""
+        culled leg). precision=32 restates an fp32 context (points and RBF rows
+        rounded to fp32 as fsdf_set_points / fsdf_set_rbf_params do; results
+        returned as float64 holding fp32 values, like the C-ABI's outputs)."""
+        if precision == 32:
+            if culled:
+                raise ValueError("the culled leg is fp64 only")
+            p32 = np.ascontiguousarray(np.asarray(pts, np.float64).reshape(-1, 3).astype(np.float32))
+            st, _keep = self.pose(poses, rbf_rows, precision=32)
+            n = len(p32)
+            d = np.empty(n, np.float32)
+            k = np.empty(n, np.int32)
+            g = np.empty((n, 3), np.float32)
+            load().oracle_skin_f32(ctypes.byref(st), _p(p32), n, _p(d), _p(k), _p(g), threads)
+            return d.astype(np.float64), k, g.astype(np.float64)
         pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
         st, _keep = self.pose(poses, rbf_rows)
         n = len(pts)

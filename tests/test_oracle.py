@@ -176,3 +176,33 @@ def test_oracle_culled_equals_brute_force(m64, oracle_mod, scene):
     b = om.skin(poses, pts, rbf_rows=rows, culled=True)
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("name", ["c1_irb140", "m64_2k", "table_quat", "c3_beanbag", "c5_scene"])
+def test_oracle_fp32_instantiation(name, oracle_mod):
+    """The fp32 restatement (skin_impl.h with R = float, what fp32 contexts are
+    checked against bit for bit on the GPU): its world rows are the fp64 rows
+    rounded once to fp32, and its per-point results stay within fp32 resolution
+    of the fp64 goldens (|Δd*| < 2e-5, |Δ∇d*| small where k* agrees, k* equal
+    except at near-ties)."""
+    from flash import Models
+    manip = {"c1_irb140": Models.irb140, "m64_2k": Models.arm_grid, "table_quat": Models.table,
+             "c3_beanbag": Models.beanbag, "c5_scene": lambda: Models.irb_and_squishable()[0]}[name]()
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    om = oracle_mod.OracleModel.from_manipulator(manip)
+    rows = z["rbf_rows"] if "rbf_rows" in z.files else None
+    if om.K:
+        st64, (pw, fx, vw, hs, _) = om.pose(z["poses"], rows)
+        st32, (pw32, fx32, vw32, hs32, _) = om.pose(z["poses"], rows, precision=32)
+        assert pw32.dtype == np.float32 and np.array_equal(pw32, pw.astype(np.float32))
+        assert np.array_equal(vw32, vw.astype(np.float32))
+        assert np.allclose(fx32, fx, rtol=0, atol=1e-5 * max(1.0, np.abs(fx).max()))
+    d, k, g = om.skin(z["poses"], z["points"], rbf_rows=rows, precision=32)
+    same = k == z["kstar"]
+    assert same.mean() > 0.995
+    assert np.abs(d - z["d"]).max() < 2e-5 * max(1.0, np.abs(z["d"]).max())
+    assert np.median(np.abs(g - z["grad"])[same]) < 1e-4
+    # determinism and the fp32 grid: every value is an fp32 number
+    assert np.array_equal(d.astype(np.float32).astype(np.float64), d)
+    d2, k2, g2 = om.skin(z["poses"], z["points"], rbf_rows=rows, precision=32, threads=1)
+    assert np.array_equal(d2, d) and np.array_equal(k2, k) and np.array_equal(g2, g)

@@ -44,27 +44,43 @@ class ShardedCostFunctor:
     """CostFunctor over this rank's shard; value/gradient are global (all-reduced)."""
 
     def __init__(self, manipulator: Manipulator, local_points, rank: int = 0, world: int = 1, device: int = 0,
-                 precision: int = 64, group=None, deformation_cost_weight=default_deformation_cost_weight):
+                 precision: int = 64, group=None, deformation_cost_weight=default_deformation_cost_weight,
+                 engine=None):
+        """engine: an already-built context-like object to drive instead of
+        manipulator.engine(device, precision) — with engine.device_type == "cpu"
+        the accumulator lives in host memory and no HIP stream is used (the CPU
+        gloo tests drive this class's sharding / all-reduce / read-back / chain
+        rule through a stand-in engine; the product engine is the HIP context)."""
+        import contextlib
         import torch
         self.torch = torch
         self.manipulator = manipulator
         self.group = group
         self.weight = deformation_cost_weight
         self.state = ManipulatorState(manipulator)
-        self.ctx = manipulator.engine(device, precision)
-        self.dev = torch.device("cuda", device)
+        self.ctx = engine if engine is not None else manipulator.engine(device, precision)
+        on_host = getattr(self.ctx, "device_type", "cuda") == "cpu"
+        self.dev = torch.device("cpu") if on_host else torch.device("cuda", device)
         pts = torch.as_tensor(np.ascontiguousarray(local_points, np.float64).reshape(-1, 3), device=self.dev)
+        self._pts = pts  # the context reads the resident copy (set_points_device does not own it)
         self.ctx.set_points_device(pts.data_ptr(), pts.shape[0])
         self.accum = torch.zeros(self.ctx.accum_len, dtype=torch.float64, device=self.dev)
         # pinned read-back of the all-reduced accumulator (a pageable .cpu()
         # goes through the runtime's staging buffer: ~10 us per iteration on
         # the single-GPU path, profiles/r02/experiments/r02pin)
-        self.h_accum = torch.empty(self.ctx.accum_len, dtype=torch.float64, pin_memory=True)
-        self.stream = torch.cuda.current_stream(self.dev)
-        self.ctx.set_stream(self.stream.cuda_stream)
+        self.h_accum = torch.empty(self.ctx.accum_len, dtype=torch.float64, pin_memory=not on_host)
+        if on_host:
+            self.stream = None
+            self._on_stream = contextlib.nullcontext
+            self._sync = lambda: None
+        else:
+            self.stream = torch.cuda.current_stream(self.dev)
+            self.ctx.set_stream(self.stream.cuda_stream)
+            self._on_stream = lambda: torch.cuda.stream(self.stream)
+            self._sync = self.stream.synchronize
         # native iterations (fsdf_eval_state_device + fsdf_state_gradient: FK,
         # RBF solve, poses, pass; chain rule after the all-reduce)
-        self._native = native_capable(manipulator)
+        self._native = native_capable(manipulator) and getattr(self.ctx, "native_iterations", True)
 
     def _ensure_native(self):
         if getattr(self.ctx, "_mechanism_of", None) != (self.manipulator, self.weight):
@@ -94,7 +110,7 @@ class ShardedCostFunctor:
         unflatten(self.state, x)
         normalize(self.state)
         poses, self._solves = prepare_pass(self.ctx, self.manipulator, self.state.q, self.state.deformation_data)
-        with torch.cuda.stream(self.stream):
+        with self._on_stream():
             self.ctx.eval_device(poses, self.accum.data_ptr(), k.data_ptr(), d.data_ptr(), g.data_ptr())
             allreduce_accum(self.accum, self.group)
             return k[:n].cpu().numpy(), d[:n].cpu().numpy(), g[:n].cpu().numpy()
@@ -104,9 +120,9 @@ class ShardedCostFunctor:
         # the pass runs on self.stream (given to the context); the all-reduce
         # and the copy must be ordered after it whatever the caller's current
         # stream is
-        with self.torch.cuda.stream(self.stream):
+        with self._on_stream():
             self.h_accum.copy_(self.launch(x), non_blocking=True)
-            self.stream.synchronize()
+            self._sync()
         acc = self.h_accum.numpy()
         if self._native:
             return self.ctx.state_gradient(x, acc)

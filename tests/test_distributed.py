@@ -1,5 +1,8 @@
 """The N>1 path on CPU: world_size-2 gloo ranks shard the cloud, compute their
-local accumulators and all-reduce them; the result equals the 1-rank pass."""
+local accumulators and all-reduce them; the result equals the 1-rank pass.
+ShardedCostFunctor itself (sharding, in-place all-reduce, read-back, chain
+rule) runs on CPU too, driving a stand-in engine whose passes are the oracle's
+(the HIP engine is exercised by tests/test_gpu_distributed.py)."""
 import os
 import socket
 
@@ -75,3 +78,108 @@ def test_gloo_world2_allreduce_equals_single_rank():
         assert np.allclose(acc, full, rtol=1e-11, atol=1e-12)
         assert np.allclose(g, chain_gradient(m, qe, full, 10), rtol=1e-10, atol=1e-12)
     assert np.array_equal(res[0][1], res[1][1])  # every rank holds the same sum
+
+
+class OracleEngine:
+    """Stand-in for the HIP context with the calls ShardedCostFunctor makes:
+    host memory (device_type "cpu"), passes computed by the CPU oracle,
+    accumulator and per-point outputs written through the raw pointers like
+    fsdf_eval_device. Test infrastructure only."""
+    device_type = "cpu"
+    native_iterations = False
+
+    def __init__(self, manip):
+        import oracle
+        self.om = oracle.OracleModel.from_manipulator(manip)
+        self.accum_len = self.om.accum_len
+        self.rows = None
+        self.n = 0
+
+    @staticmethod
+    def _view(ptr, count, dtype):
+        import ctypes
+        buf = (ctypes.c_char * (count * np.dtype(dtype).itemsize)).from_address(ptr)
+        return np.frombuffer(buf, dtype=dtype, count=count)
+
+    def set_points_device(self, ptr, n):
+        self.n = n
+        self.pts = self._view(ptr, 3 * n, np.float64).reshape(n, 3).copy()
+
+    def set_rbf_params(self, rows):
+        self.rows = np.asarray(rows, np.float64).copy()
+
+    def eval_device(self, poses, accum_ptr, k_ptr=None, d_ptr=None, g_ptr=None):
+        self._view(accum_ptr, self.accum_len, np.float64)[:] = self.om.cost_accum(poses, self.pts, rbf_rows=self.rows)
+        if k_ptr:
+            d, k, g = self.om.skin(poses, self.pts, rbf_rows=self.rows)
+            self._view(k_ptr, self.n, np.int32)[:] = k
+            self._view(d_ptr, self.n, np.float64)[:] = d
+            self._view(g_ptr, 3 * self.n, np.float64)[:] = g.ravel()
+
+
+def _scene(name):
+    import flash
+    from flash import Models, synthetic
+    if name == "irb140":
+        m = Models.irb140()
+        qt, qe = synthetic.perturbed_configuration(m, 40)
+        return m, synthetic.depth_cloud(m, qt, 3001, seed=41), qe
+    m = Models.beanbag()  # RBF skin: the chain through the weight solve
+    r = np.random.Generator(np.random.PCG64(43))
+    x = np.zeros(flash.num_states(m))
+    nq = m.mechanism.num_positions
+    x[:nq] = m.mechanism.zero_configuration()
+    x[4:7] = 0.05 * r.random(3)
+    x[nq:] = 0.2 * (r.random(len(x) - nq) - 0.5)
+    pts = r.normal(size=(1501, 3)) * 0.3
+    return m, pts, x
+
+
+def _functor_worker(rank, world, port, q, name):
+    import sys
+    from conftest import ROOT
+    for p in (os.path.join(ROOT, "point-cloud-signed-distance_amd"), os.path.join(ROOT, "oracle")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    from flash.distributed import ShardedCostFunctor, shard_range
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m, pts, x = _scene(name)
+        a, b = shard_range(len(pts), rank, world)
+        f = ShardedCostFunctor(m, pts[a:b], rank, world, engine=OracleEngine(m))
+        c, g = f.value_and_gradient(x)
+        k, d, _ = f.per_point(x)
+        q.put((rank, c, g, a, k, d))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["irb140", "beanbag_rbf"])
+def test_gloo_world2_sharded_cost_functor(name):
+    """ShardedCostFunctor on 2 gloo ranks == the same class on one rank (the
+    whole cloud): cost and ∂c/∂x to 1e-10, every rank the same values, and the
+    per-point outputs of the shards concatenate to the whole cloud's."""
+    import multiprocessing as mp
+    from flash.distributed import ShardedCostFunctor
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_functor_worker, args=(r, 2, port, q, name)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m, pts, x = _scene(name)
+    one = ShardedCostFunctor(m, pts, engine=OracleEngine(m))
+    c1, g1 = one.value_and_gradient(x)
+    k1, d1, _ = one.per_point(x)
+    for _, c, g, _, _, _ in res:
+        assert c == pytest.approx(c1, rel=1e-10)
+        assert np.allclose(g, g1, rtol=1e-9, atol=1e-10 * max(1.0, np.abs(g1).max()))
+    assert res[0][1] == res[1][1] and np.array_equal(res[0][2], res[1][2])
+    assert np.array_equal(np.concatenate([r[4] for r in res]), k1)
+    assert np.array_equal(np.concatenate([r[5] for r in res]), d1)
+    assert np.abs(g1).max() > 0

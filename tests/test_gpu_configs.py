@@ -149,3 +149,6 @@ def test_c3_beanbag_full_size_fp32(oracle_mod):
     assert np.abs(d - d64).max() < 1e-4 * max(1.0, float(np.abs(d64).max()))
     assert cost == pytest.approx(cost64, rel=1e-4)
     assert np.array_equal(d64[sel], od)  # the fp64 context is bit-exact with the oracle
+    # ... and the fp32 context with the oracle's fp32 instantiation (oracle/skin_impl.h)
+    od32, ok32, og32 = om.skin(_c3_poses(m, x), pts[sel], rbf_rows=rows, precision=32)
+    assert np.array_equal(k[sel], ok32) and np.array_equal(d[sel], od32) and np.array_equal(g[sel], og32)

@@ -310,7 +310,7 @@ def test_resident_order_outputs(m64, oracle_mod, ctx_factory):
 
 
 def test_hull_partitioned_pass_matches_one_wave_per_chunk(m64, ctx_factory):
-    """Clouds of <= 131,072 points run the hull-partitioned pass (pass_kernel
+    """Clouds of <= 196,608 points (FSDF_HPART_POINTS) run the hull-partitioned pass (pass_kernel
     HPART: 4 waves share a chunk, hull k goes to wave k % 4, lexicographic
     (d, k) merge); one more point runs the one-wave-per-chunk pass. Per-point
     outputs do not depend on the block structure: the shared points must agree
@@ -319,7 +319,7 @@ def test_hull_partitioned_pass_matches_one_wave_per_chunk(m64, ctx_factory):
     import flash
     qt, qe = synthetic.perturbed_configuration(m64, 303)
     poses = flash.hull_poses(m64, qe)
-    n = 131072
+    n = 196608
     pts = synthetic.depth_cloud(m64, qt, n + 1, seed=304, order="shuffled")
     out = {}
     for cull in (True, False):

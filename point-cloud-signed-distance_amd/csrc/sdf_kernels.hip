@@ -1550,20 +1550,22 @@ extern __shared__ __attribute__((aligned(16))) char fsdf_lds[];
 // chunk's waves is the full scene's — bit for bit. The heaviest chunks'
 // serial evaluations are spread over kHpart waves where a one-wave-per-chunk
 // grid would leave most wave slots idle.
-template <typename T, int SLOTS, bool CULL, bool RBF, bool ALIAS = false, bool HPART = false, int NB = kPassBlock>
-// (occupancy target in waves per SIMD, whatever the workgroup size NB)
+template <typename T, int SLOTS, bool CULL, bool RBF, bool ALIAS = false, bool HPART = false, int NB = kPassBlock,
+          int NPART = kHpart>
+// (occupancy target in waves per SIMD, whatever the workgroup size NB; NPART:
+// waves per chunk of the hull-partitioned pass, 4 or 2 — hpart_parts)
 __global__ __launch_bounds__(NB) __attribute__((
     amdgpu_waves_per_eu((SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)))) void pass_kernel(
     const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out) {
   static_assert(!ALIAS || (SLOTS == 1 && !RBF), "aliased wrench rows: hull-only, <= 64 surfaces");
   static_assert(!HPART || ALIAS, "the hull-partitioned pass is an aliased pass");
-  constexpr int kParts = HPART ? kHpart : 1;
+  constexpr int kParts = HPART ? NPART : 1;
   constexpr int kChunkStride = NB / kParts;  // points per logical block
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   // (wave-uniform: readfirstlane keeps the hull mask and the loops scalar)
-  const int part = HPART ? __builtin_amdgcn_readfirstlane(wave % kHpart) : 0;  // (HPART) this wave's hull residue
-  const int cw = HPART ? __builtin_amdgcn_readfirstlane(wave / kHpart) : wave;  // the block's chunk this wave works on
+  const int part = HPART ? __builtin_amdgcn_readfirstlane(wave % kParts) : 0;  // (HPART) this wave's hull residue
+  const int cw = HPART ? __builtin_amdgcn_readfirstlane(wave / kParts) : wave;  // the block's chunk this wave works on
   // All LDS is one dynamic region (16-byte aligned carve, see pass_lds_bytes):
   //   red     [4 waves][kRedStride] f64  per-hull wrench sums + cost (not ALIAS)
   //   rbf_acc [4 waves][kMaxRbfAcc] f64  (RBF variants only)
@@ -1920,25 +1922,40 @@ __global__ void to_f32_kernel(const double* __restrict__ src, float* __restrict_
 // Launchers
 // ---------------------------------------------------------------------------
 // the aliased pass's LDS plus the hull-partitioned pass's shared per-lane bests
-static size_t hpart_lds_bytes(const LocalModel& lm) {
+// (one 64-double slot row per chunk of the workgroup)
+static size_t hpart_lds_bytes(const LocalModel& lm, int parts) {
   return (size_t)(kHpartBlock / 64) * lm.stage_bytes + (size_t)(lm.K + 1) * sizeof(HullRow) +
-         (size_t)kHpartBlock / kHpart * sizeof(double);
+         (size_t)kHpartBlock / parts * sizeof(double);
 }
 
 #ifndef FSDF_HPART_POINTS
 #define FSDF_HPART_POINTS 196608  // crossover measured between 196,608 and 262,144
 #endif
-// the hull-partitioned pass (pass_kernel HPART) for clouds of at most
-// FSDF_HPART_POINTS points (environment override: FSDF_HPART_POINTS)
-bool hpart_pass(const LocalModel& lm, int64_t n) {
-  static const int64_t limit = [] {
+#ifndef FSDF_HPART2_POINTS
+#define FSDF_HPART2_POINTS 0  // 2 waves per chunk up to this size: off until measured
+#endif
+// Waves per chunk of the hull-partitioned pass (pass_kernel HPART) for a cloud
+// of n points, 0 = the one-wave-per-chunk pass: kHpart (4) up to
+// FSDF_HPART_POINTS points, 2 up to FSDF_HPART2_POINTS (environment overrides
+// of the same names, read once per process; 0 disables a tier).
+int hpart_parts(const LocalModel& lm, int64_t n) {
+  static const int64_t limit4 = [] {
     const char* e = getenv("FSDF_HPART_POINTS");
     return e ? (int64_t)atoll(e) : (int64_t)FSDF_HPART_POINTS;
   }();
-  return FSDF_RED_IN_STAGE && lm.planes64 && lm.S <= 64 && lm.R == 0 && n > 0 && n <= limit &&
-         (n + kHpartBlock / kHpart - 1) / (kHpartBlock / kHpart) <= kMaxBlocks &&
-         hpart_lds_bytes(lm) <= (size_t)kLdsPerCu * kHpartBlock / 1024;  // (4 waves per SIMD)
+  static const int64_t limit2 = [] {
+    const char* e = getenv("FSDF_HPART2_POINTS");
+    return e ? (int64_t)atoll(e) : (int64_t)FSDF_HPART2_POINTS;
+  }();
+  if (!(FSDF_RED_IN_STAGE && lm.planes64 && lm.S <= 64 && lm.R == 0 && n > 0)) return 0;
+  const int parts = n <= limit4 ? kHpart : (n <= limit2 ? 2 : 0);
+  if (!parts) return 0;
+  const int64_t per = kHpartBlock / parts;  // points per workgroup
+  if ((n + per - 1) / per > kMaxBlocks) return 0;
+  if (hpart_lds_bytes(lm, parts) > (size_t)kLdsPerCu * kHpartBlock / 1024) return 0;  // (4 waves per SIMD)
+  return parts;
 }
+bool hpart_pass(const LocalModel& lm, int64_t n) { return hpart_parts(lm, n) > 0; }
 
 static bool alias_pass(const LocalModel& lm, int64_t n) {
   return FSDF_RED_IN_STAGE && lm.planes64 && lm.S <= 64 && lm.R == 0 && n > 0 && (n + kAliasBlock - 1) / kAliasBlock <= kMaxBlocks;
@@ -1948,7 +1965,7 @@ static size_t alias_lds_bytes(const LocalModel& lm) {
 }
 
 int pass_blocks(int64_t n, const LocalModel& lm) {
-  if (hpart_pass(lm, n)) return (int)((n + kHpartBlock / kHpart - 1) / (kHpartBlock / kHpart));
+  if (const int parts = hpart_parts(lm, n)) return (int)((n + kHpartBlock / parts - 1) / (kHpartBlock / parts));
   if (alias_pass(lm, n)) return (int)((n + kAliasBlock - 1) / kAliasBlock);
   int64_t b = (n + kPassBlock - 1) / kPassBlock;
   if (b < 1) b = 1;
@@ -2045,9 +2062,13 @@ static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void
   const size_t lds = pass_lds_bytes(lm, false);
   if constexpr (!RBF && FSDF_RED_IN_STAGE) {
     // one chunk per wave: the wrench rows alias the stage (pass_kernel ALIAS)
-    if (hpart_pass(lm, n)) {
-      launch_lds(pass_kernel<T, 1, CULL, false, true, true, kHpartBlock>, nblocks, kHpartBlock, hpart_lds_bytes(lm), s,
-                 pts, n, m, out);
+    if (const int parts = hpart_parts(lm, n)) {
+      if (parts == kHpart)
+        launch_lds(pass_kernel<T, 1, CULL, false, true, true, kHpartBlock, kHpart>, nblocks, kHpartBlock,
+                   hpart_lds_bytes(lm, parts), s, pts, n, m, out);
+      else
+        launch_lds(pass_kernel<T, 1, CULL, false, true, true, kHpartBlock, 2>, nblocks, kHpartBlock,
+                   hpart_lds_bytes(lm, parts), s, pts, n, m, out);
       return;
     }
     if (alias_pass(lm, n) && (int64_t)nblocks * kAliasBlock >= n) {
@@ -2072,9 +2093,13 @@ static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm,
                           int nblocks, const PassOutputs& out, hipStream_t s) {
 #if FSDF_BENCH_ONLY
   const PassModel<T> m = pass_model<T>(lm, pm);
-  if (hpart_pass(lm, n))
-    launch_lds(pass_kernel<T, 1, true, false, true, true, kHpartBlock>, nblocks, kHpartBlock, hpart_lds_bytes(lm), s,
-               (const T*)d_pts, n, m, out);
+  const int parts = hpart_parts(lm, n);
+  if (parts == kHpart)
+    launch_lds(pass_kernel<T, 1, true, false, true, true, kHpartBlock, kHpart>, nblocks, kHpartBlock,
+               hpart_lds_bytes(lm, parts), s, (const T*)d_pts, n, m, out);
+  else if (parts == 2)
+    launch_lds(pass_kernel<T, 1, true, false, true, true, kHpartBlock, 2>, nblocks, kHpartBlock,
+               hpart_lds_bytes(lm, parts), s, (const T*)d_pts, n, m, out);
   else if (alias_pass(lm, n) && (int64_t)nblocks * kAliasBlock >= n)
     launch_lds(pass_kernel<T, 1, true, false, true, false, kAliasBlock>, nblocks, kAliasBlock, alias_lds_bytes(lm), s,
                (const T*)d_pts, n, m, out);

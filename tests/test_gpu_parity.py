@@ -309,17 +309,18 @@ def test_resident_order_outputs(m64, oracle_mod, ctx_factory):
     assert np.array_equal(k0, kc) and np.array_equal(d0, dc)
 
 
-def test_hull_partitioned_pass_matches_one_wave_per_chunk(m64, ctx_factory):
-    """Clouds of <= 196,608 points (FSDF_HPART_POINTS) run the hull-partitioned pass (pass_kernel
-    HPART: 4 waves share a chunk, hull k goes to wave k % 4, lexicographic
-    (d, k) merge); one more point runs the one-wave-per-chunk pass. Per-point
-    outputs do not depend on the block structure: the shared points must agree
-    bit for bit, sums to rounding."""
+@pytest.mark.parametrize("n", [196608, 393216])
+def test_hull_partitioned_pass_matches_one_wave_per_chunk(m64, ctx_factory, n):
+    """Clouds of <= 196,608 points (FSDF_HPART_POINTS) run the hull-partitioned
+    pass with 4 waves per chunk, <= 393,216 (FSDF_HPART2_POINTS) with 2 (pass_kernel
+    HPART: hull k goes to wave k % parts, lexicographic (d, k) merge); one point
+    more runs the next tier (2 waves per chunk, then one wave per chunk).
+    Per-point outputs do not depend on the block structure: the shared points
+    must agree bit for bit, sums to rounding."""
     from flash import synthetic
     import flash
     qt, qe = synthetic.perturbed_configuration(m64, 303)
     poses = flash.hull_poses(m64, qe)
-    n = 196608
     pts = synthetic.depth_cloud(m64, qt, n + 1, seed=304, order="shuffled")
     out = {}
     for cull in (True, False):

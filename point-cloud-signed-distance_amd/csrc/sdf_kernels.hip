@@ -1932,7 +1932,7 @@ static size_t hpart_lds_bytes(const LocalModel& lm, int parts) {
 #define FSDF_HPART_POINTS 196608  // crossover measured between 196,608 and 262,144
 #endif
 #ifndef FSDF_HPART2_POINTS
-#define FSDF_HPART2_POINTS 0  // 2 waves per chunk up to this size: off until measured
+#define FSDF_HPART2_POINTS 393216  // 2 waves per chunk up to this size (crossover below 524,288)
 #endif
 // Waves per chunk of the hull-partitioned pass (pass_kernel HPART) for a cloud
 // of n points, 0 = the one-wave-per-chunk pass: kHpart (4) up to

@@ -107,3 +107,24 @@ def skin_cloud(manip: Manipulator, x, n: int, seed: int = 0, near: float = 0.85,
         pts[:k] -= d[:, None] * g
     pts[:k] += r.normal(scale=sigma, size=(k, 3))
     return pts
+
+
+def c5_cloud(manip: Manipulator, x, n: int, real_xyz: np.ndarray, seed: int = 0, sigma: float = 0.002,
+             frac_real: float = 0.5) -> np.ndarray:
+    """BASELINE config 5's cloud: the reference's recorded
+    Kinect cloud of the squishable (examples/data/squishable_unsquished_xyzrgb.txt,
+    25,571 points, read by examples/squishable.ipynb cell 4 / src/depthdata.jl:19-30)
+    tiled to `frac_real`·n points — copy j > 0 jittered by N(0, sigma) — plus
+    generator G (depth_cloud) on the scene's hulls at the configuration x[:nq]
+    for the rest, shuffled together. `real_xyz` is the [N,3] position array
+    (tests/golden/squishable_unsquished.npz)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    real = np.asarray(real_xyz, np.float64)
+    n_real = int(round(frac_real * n))
+    reps = -(-n_real // len(real))
+    tiled = np.tile(real, (reps, 1))[:n_real].copy()
+    tiled[len(real):] += rng.normal(0.0, sigma, size=(n_real - min(n_real, len(real)), 3))
+    nq = manip.mechanism.num_positions
+    arm = depth_cloud(manip, np.asarray(x[:nq], np.float64), n - n_real, seed=seed + 1, order="generated")
+    pts = np.concatenate([tiled, arm])
+    return np.ascontiguousarray(pts[rng.permutation(len(pts))])

@@ -198,20 +198,28 @@ def test_async_rbf_rows_not_torn():
 
 
 def test_c5_precision_sweep_vs_oracle():
-    """BASELINE config 5's fp32-vs-fp64 sweep (tools/precision_sweep.py) at
-    2^16 points of the deformed irb_and_squishable scene, both precisions
-    against the fp64 CPU oracle. Tolerances: f64 k*/d* exact (north-star bar:
-    k* exact, 1e-6 rel); f32 |Δd*| < 5e-5 m, k* flips on < 0.5 % of the points
-    and only at near-ties (|Δd*| < 5e-5 there), cost within 1e-4 rel, ∂c/∂x
-    within 1e-2 rel of the f64 gradient."""
+    """BASELINE config 5 as SURVEY.md §8d defines it: 2^20 points — the
+    reference's recorded squishable cloud (25,571 points) tiled and jittered to
+    half of them, generator G on the scene's hulls for the rest — on the
+    deformed irb_and_squishable scene (tools/precision_sweep.py), both
+    precisions against the fp64 CPU oracle on ALL points. Tolerances: f64
+    k*/d* exact (north-star bar: k* exact, 1e-6 rel); f32 bit-exact against
+    the fp32 oracle on a 131,072-point sample; f32 vs f64: |Δd*| < 5e-5 m, k*
+    flips on < 0.5 % of the points and only at near-ties (|Δd*| < 5e-5
+    there), cost within 1e-4 rel, ∂c/∂x within 1e-2 rel of the f64 gradient.
+    Reference: examples/irb_and_squishable.ipynb:329-331 (poses),
+    src/depthdata.jl:19-30 (the cloud's format)."""
     import sys
     from conftest import ROOT
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import precision_sweep
-    r = precision_sweep.sweep(1 << 16)
+    r = precision_sweep.sweep(1 << 20)
+    assert r["points"] == 1 << 20
     f64, f32 = r["f64"], r["f32"]
     assert f64["max_abs_dd"] == 0.0 and f64["kstar_mismatch"] == 0
     assert f64["cost_rel_err"] < 1e-9
+    ex = f32["f32_exact_sample"]
+    assert ex["points"] == 1 << 17 and ex["kstar_equal"] and ex["d_equal"] and ex["grad_equal"], ex
     assert f32["max_abs_dd"] < 5e-5
     assert f32["kstar_mismatch_frac"] < 5e-3
     assert f32.get("max_abs_dd_at_mismatch", 0.0) < 5e-5

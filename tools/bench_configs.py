@@ -5,7 +5,8 @@ is bench.py's; these are the companion numbers DESIGN.md §7 reports).
   C2  IRB140 rigid, 2^20 synthetic points, f64
   C3  deformable beanbag (RBF, 25 states), 2^20 points, f32 (and f64)
   C4  IRB140, 10*2^20/8 = 1,310,720 points = one GPU's shard of the 8-GPU config, f64
-  C5  irb_and_squishable (7 hulls + squishable RBF + table, 63 states), 2^20 points, f32 vs f64
+  C5  irb_and_squishable (7 hulls + squishable RBF + table, 63 states), 2^20 points (the reference's
+      recorded squishable cloud tiled + G, flash.synthetic.c5_cloud), f32 vs f64
   M64 the metric model, for reference
 Each: one residual pass incl. the RBF parameter upload; mean pass-kernel time
 (HIP events) and whole-pass wall time over R passes; set_points once (sorted).
@@ -78,8 +79,9 @@ def main():
     for prec in (32, 64):
         rows.append(run("C3 beanbag", bb, x, pts, prec, a.reps))
     sc, x0 = Models.irb_and_squishable()
-    pts = np.concatenate([rbf_cloud(sc, x0, 1 << 19, 7),
-                          synthetic.depth_cloud(sc, x0[:sc.mechanism.num_positions], 1 << 19, seed=8)])
+    # the reference's recorded cloud tiled/jittered + G on the scene's hulls
+    real = np.load(os.path.join(ROOT, "tests", "golden", "squishable_unsquished.npz"))["xyz"]
+    pts = synthetic.c5_cloud(sc, x0, 1 << 20, real, seed=7)
     for prec in (32, 64):
         rows.append(run("C5 irb_and_squishable", sc, x0, pts, prec, a.reps))
     m64 = Models.arm_grid()

@@ -3,13 +3,18 @@
 
 Scene: irb_and_squishable (7 IRB140 hulls + the squishable RBF skin + the
 table box, 63 states; examples/irb_and_squishable.ipynb cells 3-6) with a
-random deformation of the squishable's surface points, 2^20 points (half near
-the RBF skin, half generator G on the arm). For each context precision the GPU
-pass is compared with the fp64 CPU oracle on the same posed scene:
+random deformation of the squishable's surface points; 2^20 points as SURVEY.md
+§8d defines C5: the reference's recorded cloud (squishable_unsquished_xyzrgb.txt,
+25,571 points, fixture tests/golden/squishable_unsquished.npz) tiled and
+jittered to half the points, generator G on the scene's hulls for the rest
+(flash.synthetic.c5_cloud). For each context precision the GPU pass is
+compared with the fp64 CPU oracle on the same posed scene:
 
   max / p99 |Δd*|, k* mismatch rate (and max |Δd*| at the mismatches: a flip
   is harmless only at a near-tie), max |Δ∇d*| where k* agrees,
-  relative error of the cost and of ∂c/∂x (63 states, host chain rule).
+  relative error of the cost and of ∂c/∂x (63 states, host chain rule);
+  and the fp32 context bit for bit against the oracle's fp32 instantiation on
+  a sample (`f32_exact_sample`).
 
     python tools/precision_sweep.py [--points N] [--json out.json]
 """
@@ -26,21 +31,22 @@ for p in (os.path.join(ROOT, "point-cloud-signed-distance_amd"), os.path.join(RO
     sys.path.insert(0, p)
 
 
+REAL_CLOUD = os.path.join(ROOT, "tests", "golden", "squishable_unsquished.npz")
+
+
 def scene(n, seed=31):
-    import flash
+    import flash  # noqa: F401
     from flash import Models, synthetic
-    from bench_configs import rbf_cloud
     m, x = Models.irb_and_squishable()
     nq = m.mechanism.num_positions
     r = np.random.Generator(np.random.PCG64(seed))
     x = x.copy()
     x[nq:] = 0.02 * (r.random(len(x) - nq) - 0.5)  # deformed squishable
-    pts = np.concatenate([rbf_cloud(m, x, n // 2, seed + 1),
-                          synthetic.depth_cloud(m, x[:nq], n - n // 2, seed=seed + 2, order="shuffled")])
-    return m, x, pts
+    real = np.load(REAL_CLOUD)["xyz"]
+    return m, x, synthetic.c5_cloud(m, x, n, real, seed=seed + 1)
 
 
-def sweep(n, seed=31):
+def sweep(n, seed=31, exact_sample=1 << 17):
     import flash  # noqa: F401
     import oracle
     from flash import rbf as host_rbf
@@ -54,7 +60,8 @@ def sweep(n, seed=31):
     om = oracle.OracleModel.from_manipulator(m)
     od, ok, og = om.skin(poses, pts, rbf_rows=rows, culled=True)
     oacc = om.cost_accum(poses, pts, rbf_rows=rows)
-    out = {"scene": "irb_and_squishable (7 hulls + squishable RBF + table), deformed", "points": len(pts),
+    out = {"scene": "irb_and_squishable (7 hulls + squishable RBF + table), deformed; reference cloud tiled + G",
+           "points": len(pts),
            "states": len(x), "oracle_cost": float(oacc[0])}
     ref_grad = None
     for prec in (64, 32):
@@ -75,6 +82,14 @@ def sweep(n, seed=31):
         if mis.any():
             # a flip is harmless only at a near-tie: |Δd*| there bounds the gap
             row["max_abs_dd_at_mismatch"] = float(dd[mis].max())
+        if prec == 32 and exact_sample:
+            # the fp32 context against the oracle's fp32 instantiation, bit for bit
+            idx = np.sort(np.random.Generator(np.random.PCG64(seed + 7)).choice(len(pts), min(exact_sample, len(pts)),
+                                                                                 replace=False))
+            fd, fk, fg = om.skin(poses, pts[idx], rbf_rows=rows, precision=32)
+            row["f32_exact_sample"] = {"points": int(len(idx)), "kstar_equal": bool(np.array_equal(k[idx], fk)),
+                                       "d_equal": bool(np.array_equal(d[idx], fd)),
+                                       "grad_equal": bool(np.array_equal(gr[idx], fg))}
         out[f"f{prec}"] = row
     return out
 

@@ -206,7 +206,8 @@ def main():
     ctx.set_output_order(not args.caller_order)
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
-    accum = torch.zeros(ctx.accum_len, dtype=torch.float64, device=dev)
+    accums = [torch.zeros(ctx.accum_len, dtype=torch.float64, device=dev) for _ in range(2)]
+    accum = accums[0]
 
     def run_cloud(pts_host):
         """Upload the cloud (timed per frame), then W untimed + K timed steps
@@ -230,12 +231,27 @@ def main():
                     torch.empty((max(n_, 1), 3), dtype=torch.float64, device=dev))
             outs = tuple(b_.data_ptr() for b_ in bufs)
 
+        # W > 1: two accumulators and an asynchronous all-reduce — step i+1's
+        # pass runs while step i's collective is in flight (flash/distributed.py);
+        # a buffer is reused only after its previous collective completed
+        pending = [None, None]
+
         def step(i):
-            ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs)
-            allreduce_accum(accum)
+            s_ = i & 1
+            if pending[s_] is not None:
+                pending[s_].wait()
+            ctx.eval_device(poses[s_], accums[s_].data_ptr(), *outs)
+            pending[s_] = allreduce_accum(accums[s_], async_op=True)
+
+        def drain():
+            for s_ in (0, 1):
+                if pending[s_] is not None:
+                    pending[s_].wait()
+                    pending[s_] = None
 
         for i in range(args.warmup):
             step(i)
+        drain()
         torch.cuda.synchronize()
         ctx.profile_pass(True)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -246,6 +262,7 @@ def main():
         ev0.record(stream)
         for i in range(args.steps):
             step(i)
+        drain()
         ev1.record(stream)
         if world > 1:
             dist.barrier()
@@ -259,15 +276,30 @@ def main():
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         # sanity: the last pass is finite and non-trivial
-        acc = accum.cpu().numpy()
+        acc = accums[(args.steps - 1) & 1].cpu().numpy()
         assert np.isfinite(acc).all() and acc[0] > 0
         return float(t[0]), float(t[1]), float(t[2]), float(t[3])
 
     n = len(pts)
     elapsed, pass_avg_ms, kernel_avg_ms, set_points_ms = run_cloud(pts)
 
-    allreduce_ms = None
+    allreduce_ms = dependent_ms = None
     if world > 1:
+        # a dependent iteration (track!: x_{k+1} needs the all-reduced accumulator
+        # of x_k): pass, collective, host read-back, every step — the latency the
+        # overlap above cannot hide
+        outs0 = (0, 0, 0)
+        for _ in range(3):
+            ctx.eval_device(poses[0], accum.data_ptr(), *outs0)
+            allreduce_accum(accum)
+            accum[0].item()
+        dist.barrier()
+        t_dep = time.perf_counter()
+        for i in range(args.steps):
+            ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs0)
+            allreduce_accum(accum)
+            accum[0].item()
+        dependent_ms = (time.perf_counter() - t_dep) / args.steps * 1e3
         # the all-reduce alone, host-synchronised per call (latency-bound: ~3 KB)
         for _ in range(3):
             allreduce_accum(accum)
@@ -312,10 +344,14 @@ def main():
         default_run = (world == 1 and args.config == "m64" and n == 1 << 20 and args.precision == 64
                        and not args.no_cull and not args.no_sort and not args.no_per_point
                        and args.order == "shuffled" and not args.caller_order)
+        ran = ctx.pass_kernel_name()
+        pmc_kernel = None
         if os.path.exists(pmc) and default_run:
             with open(pmc) as f:
                 rec = json.load(f)
-            if rec.get("workload") == "bench.py default":
+            pmc_kernel = rec.get("kernel", "").replace("fsdf::", "")
+            # counters of another kernel variant (an older profile) are not this run's: refuse them
+            if rec.get("workload") == "bench.py default" and pmc_kernel == ran:
                 traffic, traffic_src = rec.get("traffic_bytes_per_launch"), rec.get("source")
                 executed = rec.get("executed")
                 if executed and executed.get("valu_insts_per_launch"):
@@ -348,6 +384,11 @@ def main():
                                 f"{ctx.accum_len}-f64 all-reduce per pass"),
                 "backend": backend,
                 "allreduce_ms": allreduce_ms,
+                "allreduce_overlap": ("asynchronous all-reduce, two accumulators: step i+1's pass overlaps step "
+                                      "i's collective" if world > 1 else None),
+                "dependent_step_ms": dependent_ms,
+                "dependent_step_note": ("pass + all-reduce + host read-back per step, no overlap (a track! "
+                                        "iteration's latency; no per-point outputs)" if world > 1 else None),
                 "set_points_ms_per_frame": set_points_ms,
                 "frame_ms_at_30_iterations": frame_ms,
                 "frame_note": "set_points (H2D-resident copy + Hilbert sort) once + 30 residual passes",
@@ -359,16 +400,18 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": hbm_achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": "pass_kernel", "kernel_ms": kernel_avg_ms,
+                "kernel": ran, "kernel_ms": kernel_avg_ms,
                 "pass_and_reduce_ms": pass_avg_ms,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "valu_issue_frac": issue,
-                "valu_effective": {"flop_per_eval": f_alg, "achieved_tflops": eff_tflops, "peak_tflops": peak_valu,
-                                   "ratio": eff_tflops / peak_valu,
-                                   "note": "brute-force F_alg (every plane of every hull, SURVEY.md §8d) per "
-                                           "launch / kernel time; culling skips most of it, so it can exceed 1"},
                 "executed_pmc": executed,
+                "pmc_kernel": pmc_kernel,
             },
+            # not a roofline fraction: the brute-force work the culling skips, per kernel time
+            "valu_effective": {"flop_per_eval": f_alg, "achieved_tflops": eff_tflops, "peak_tflops": peak_valu,
+                               "ratio": eff_tflops / peak_valu,
+                               "note": "brute-force F_alg (every plane of every hull, SURVEY.md §8d) per launch / "
+                                       "kernel time; culling skips most of it, so the ratio exceeds 1"},
         }
         if weak is not None:
             out["weak"] = weak

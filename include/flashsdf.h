@@ -192,8 +192,10 @@ int fsdf_set_deformations(fsdf_ctx* ctx, int32_t n_deform, double weight);
  * the poses and the pass into the DEVICE accumulator d_accum (asynchronous on
  * the context's stream); after the caller's all-reduce (RCCL) and read-back,
  * fsdf_state_gradient(x, accum) returns cost and gradient as
- * fsdf_value_and_gradient does, on the FK / weight solve of that pass: x must
- * be the x of the last fsdf_eval_state_device (FSDF_ERR_STATE otherwise). */
+ * fsdf_value_and_gradient does, on the FK / weight solve of that pass. x may
+ * be an earlier pass's x (pipelined passes: the next pass is enqueued before
+ * the previous all-reduce completes): the host FK and weight solve are then
+ * redone for x — the same arithmetic, the same bits. */
 int fsdf_eval_state_device(fsdf_ctx* ctx, const double* x, double* d_accum);
 int fsdf_state_gradient(fsdf_ctx* ctx, const double* x, const double* accum, double* cost_out, double* grad_out);
 
@@ -302,6 +304,28 @@ int fsdf_synchronize(fsdf_ctx* ctx);
 int fsdf_profile_pass(fsdf_ctx* ctx, int32_t enable);
 int fsdf_pass_times(fsdf_ctx* ctx, double* kernel_ms_out, double* pass_ms_out, int64_t* launches_out);
 int fsdf_pass_time(fsdf_ctx* ctx, double* total_ms_out, int64_t* launches_out);
+
+/* The pass-kernel variant the context's last residual pass dispatched, as
+ * rocprofv3 names it without the namespace, e.g.
+ * "pass_kernel<double, 1, true, false, true, false, 256, 4>"; "" before any
+ * pass. (bench.py attaches PMC counters to its roofline only when the
+ * profiled kernel is this one.) */
+const char* fsdf_pass_kernel_name(const fsdf_ctx* ctx);
+
+/* ---- hull-partitioned pass tiers ---------------------------------------------
+ * Small clouds leave wave slots idle while a chunk's serial hull evaluations
+ * set the pass time; up to a tier's point count the pass instead runs 4 (or
+ * 2) waves per 64-point chunk, each evaluating every 4th (2nd) hull, merged by
+ * the first-index (d, k) minimum — bit-identical per point. The tiers apply to
+ * f64 hull-only scenes of <= 64 surfaces. Defaults depend on the model (hull
+ * count); fsdf_set_partition overrides them for this context:
+ * -1 = the model's default, 0 = tier off, else the largest cloud (points per
+ * device) the tier runs. fsdf_get_partition reports the limits in effect and
+ * the waves per chunk (4, 2, 0 = one) a pass over n points would run.
+ * Replaces the reference's nothing: a scheduling knob of this build. */
+int fsdf_set_partition(fsdf_ctx* ctx, int64_t four_way_max_points, int64_t two_way_max_points);
+int fsdf_get_partition(fsdf_ctx* ctx, int64_t n, int64_t* four_way_max_out, int64_t* two_way_max_out,
+                       int32_t* parts_out);
 
 /* Kernel work counters (diagnostics). enable=1 zeroes and starts counting in
  * every following pass; enable=0 stops and writes the counters:

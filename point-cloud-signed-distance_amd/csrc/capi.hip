@@ -53,6 +53,7 @@ struct fsdf_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   std::string err;
+  std::string pass_kernel;  // the pass-kernel variant of the last pass (fsdf_pass_kernel_name)
 
   // local model
   fsdf::LocalModel lm;
@@ -206,7 +207,11 @@ static void free_model(fsdf_ctx* c) {
   c->pm_next = 0;
   dfree(c->d_poses);
   dfree(c->d_accum);
+  // (the partition tiers are a context setting: they survive a model change)
+  const int64_t h4 = c->lm.hpart4_points, h2 = c->lm.hpart2_points;
   c->lm = fsdf::LocalModel();
+  c->lm.hpart4_points = h4;
+  c->lm.hpart2_points = h2;
 }
 
 extern "C" int fsdf_create(fsdf_ctx** out, const fsdf_opts* opts) {
@@ -718,7 +723,9 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
     if (rc) return rc;
   }
   if (n > 0) {  // per-chunk bounding spheres of the resident order (pose-independent)
-    const int64_t nc = (n + 63) / 64;
+    // (padded to whole 4-chunk pass workgroups: every wave of a hull-partitioned
+    // pass reads its chunk's row, also past the cloud's end)
+    const int64_t nc = ((n + 63) / 64 + 3) & ~(int64_t)3;
     if (c->chunk_ws_cap < nc) {
       HIPCHECK(c, hipStreamSynchronize(c->stream));
       dfree(c->d_chunk_ws);
@@ -726,7 +733,7 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
       HIPCHECK(c, hipMalloc(&c->d_chunk_ws, (size_t)nc * 4 * sizeof(float)));
       c->chunk_ws_cap = nc;
     }
-    HIPCHECK(c, fsdf::launch_chunk_spheres(c->precision, c->d_pts, n, c->d_chunk_ws, c->stream));
+    HIPCHECK(c, fsdf::launch_chunk_spheres(c->precision, c->d_pts, n, nc, c->d_chunk_ws, c->stream));
   }
   // the caller may reuse its buffer once this returns
   HIPCHECK(c, hipStreamSynchronize(c->stream));
@@ -843,6 +850,7 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
     hipEvent_t* pe = prof ? &c->prof_ev[c->prof_used] : nullptr;
     HIPCHECK(c, fsdf::launch_pass(c->precision, c->cull != 0, c->lm, *P, d_pts, n, nblocks, out, c->stream,
                                   pe ? pe[0] : nullptr, pe ? pe[1] : nullptr));
+    c->pass_kernel = fsdf::last_pass_kernel();
     rc = release_posed(c, pbuf);
     if (rc) return rc;
     if (prof) c->prof_used += 3;
@@ -868,6 +876,30 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
 // per-point outputs of resident-cloud passes: scattered to caller order through
 // the sort permutation, or written in resident order (coalesced)
 static const int32_t* out_perm(const fsdf_ctx* c) { return c->out_order == FSDF_ORDER_RESIDENT ? nullptr : c->d_perm; }
+
+extern "C" int fsdf_set_partition(fsdf_ctx* c, int64_t four_way_max_points, int64_t two_way_max_points) {
+  if (!c) return FSDF_ERR_ARG;
+  if (four_way_max_points < -1 || two_way_max_points < -1)
+    return fail(c, FSDF_ERR_ARG, "set_partition: limits are -1 (model default), 0 (off) or a point count");
+  c->lm.hpart4_points = four_way_max_points;
+  c->lm.hpart2_points = two_way_max_points;
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_get_partition(fsdf_ctx* c, int64_t n, int64_t* four_way_max_out, int64_t* two_way_max_out,
+                                  int32_t* parts_out) {
+  if (!c) return FSDF_ERR_ARG;
+  int64_t f4, f2;
+  fsdf::hpart_default_limits(c->lm, &f4, &f2);
+  if (c->lm.hpart4_points >= 0) f4 = c->lm.hpart4_points;
+  if (c->lm.hpart2_points >= 0) f2 = c->lm.hpart2_points;
+  if (four_way_max_out) *four_way_max_out = f4;
+  if (two_way_max_out) *two_way_max_out = f2;
+  if (parts_out) *parts_out = c->lm.K > 0 ? fsdf::hpart_parts(c->lm, n) : 0;
+  return FSDF_OK;
+}
+
+extern "C" const char* fsdf_pass_kernel_name(const fsdf_ctx* c) { return c ? c->pass_kernel.c_str() : ""; }
 
 extern "C" int fsdf_set_output_order(fsdf_ctx* c, int32_t order) {
   if (!c) return FSDF_ERR_ARG;
@@ -1082,7 +1114,10 @@ extern "C" int fsdf_set_deformations(fsdf_ctx* c, int32_t n_deform, double weigh
 // and its device-split form fsdf_eval_state_device + fsdf_state_gradient):
 // prepare = FK, RBF centres + weight solve + rows upload, surface poses;
 // finish = RBF adjoint, chain rule, regularizer from an accumulator.
-static int iteration_prepare(fsdf_ctx* c, const double* x, const char* who) {
+// upload = false: the host part only (FK, RBF centres + weight solve, surface
+// poses into c->mech) — fsdf_state_gradient re-prepares an earlier x so the
+// chain rule runs on that pass's solve (pipelined passes, flash/distributed.py)
+static int iteration_prepare(fsdf_ctx* c, const double* x, const char* who, bool upload = true) {
   auto& M = c->mech;
   if (M.nb == 0) return fail(c, FSDF_ERR_STATE, "%s: no mechanism (call fsdf_set_mechanism)", who);
   if ((int)M.surface_body.size() != c->lm.S || (int)M.poses.size() != 12 * c->lm.S)
@@ -1128,8 +1163,10 @@ static int iteration_prepare(fsdf_ctx* c, const double* x, const char* who) {
       }
       M.rows.insert(M.rows.end(), D.u.begin() + D.n, D.u.end());
     }
-    rc = fsdf_set_rbf_params(c, M.rows.data(), (int64_t)M.rows.size());
-    if (rc) return rc;
+    if (upload) {
+      rc = fsdf_set_rbf_params(c, M.rows.data(), (int64_t)M.rows.size());
+      if (rc) return rc;
+    }
   }
   // surface poses T_world_body · T_body_geometry (identity for surfaces without a body)
   const int S = c->lm.S;
@@ -1281,9 +1318,13 @@ extern "C" int fsdf_state_gradient(fsdf_ctx* c, const double* x, const double* a
   auto& M = c->mech;
   const size_t nx = (size_t)M.nq + 3 * (size_t)M.n_deform;
   // the chain rule runs on the FK / weight solve of the pass that produced
-  // accum: x must be that pass's x (fsdf_eval_state_device)
-  if (M.nb == 0 || M.x_prepared.size() != nx || memcmp(M.x_prepared.data(), x, nx * sizeof(double)) != 0)
-    return fail(c, FSDF_ERR_STATE, "state_gradient: x is not the x of the last fsdf_eval_state_device");
+  // accum; for an x other than the last prepared one (a pipelined earlier
+  // pass) that host part is redone — the same arithmetic, the same bits
+  if (M.nb == 0) return fail(c, FSDF_ERR_STATE, "state_gradient: no mechanism (call fsdf_set_mechanism)");
+  if (M.x_prepared.size() != nx || memcmp(M.x_prepared.data(), x, nx * sizeof(double)) != 0) {
+    const int rc = iteration_prepare(c, x, "state_gradient", false);
+    if (rc) return rc;
+  }
   return iteration_finish(c, x, accum, cost_out, grad_out, "state_gradient");
 }
 

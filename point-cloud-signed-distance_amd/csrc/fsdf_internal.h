@@ -91,7 +91,20 @@ struct LocalModel {
   const int32_t* face_rows = nullptr;  // [F][4]
   int stage_bytes = 0;                 // per-wave LDS stage, context precision (multiple of 16)
   int planes64 = 0;                    // f64: stage the fp64 planes too (FSDF_STAGE_PLANES64, if they fit)
+  // hull-partitioned pass tiers (pass_kernel HPART, hpart_parts): clouds of
+  // up to hpart4_points run 4 waves per chunk, up to hpart2_points 2; -1 =
+  // the model's default (hpart_default_limits), 0 = tier off (fsdf_set_partition)
+  int64_t hpart4_points = -1, hpart2_points = -1;
 };
+
+// the model-dependent defaults of the two tiers (sdf_kernels.hip)
+void hpart_default_limits(const LocalModel& lm, int64_t* four, int64_t* two);
+// waves per chunk a pass over n points runs (4, 2; 0 = one wave per chunk)
+int hpart_parts(const LocalModel& lm, int64_t n);
+// the pass-kernel variant the last launch_pass on this thread dispatched
+// ("pass_kernel<T, SLOTS, CULL, RBF, ALIAS, HPART, NB, NPART>", as rocprofv3
+// prints it without the namespace); "" before any
+const char* last_pass_kernel();
 
 struct PosedModel {
   void* planes_w = nullptr;   // T
@@ -158,7 +171,8 @@ hipError_t launch_to_f32(const double* src, float* dst, int64_t count, hipStream
 
 // per-chunk (64 points) bounding spheres of a resident cloud of the context
 // precision -> d_out [ceil(n/64)][4] f32 (the pass kernel's wave culling input)
-hipError_t launch_chunk_spheres(int precision, const void* d_pts, int64_t n, float* d_out, hipStream_t s);
+hipError_t launch_chunk_spheres(int precision, const void* d_pts, int64_t n, int64_t nchunks, float* d_out,
+                                hipStream_t s);
 
 int pass_blocks(int64_t n, const LocalModel& lm);
 bool hpart_pass(const LocalModel& lm, int64_t n);

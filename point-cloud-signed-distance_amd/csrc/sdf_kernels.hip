@@ -34,6 +34,7 @@
 #include <hip/hip_ext.h>
 
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -417,6 +418,12 @@ static_assert(kHpart == 2 || kHpart == 4, "FSDF_HPART is 2 or 4");
 // workgroups of the hull-partitioned and the one-chunk-per-wave pass
 // (pass_kernel NB; 512-thread workgroups measured slower for both)
 constexpr int kHpartBlock = kPassBlock;
+// hpart_default_limits: models with at least kHpartFullHulls hulls use the
+// M64-measured tiers, smaller ones kHpartSmall4 / kHpartSmall2 (measured on
+// IRB140, C2)
+constexpr int kHpartFullHulls = 32;
+constexpr int64_t kHpartSmall4 = 196608;
+constexpr int64_t kHpartSmall2 = 393216;
 constexpr int kAliasBlock = kPassBlock;
 
 // The one diagnostic build (-DFSDF_WAVE_TIMES=1, tools/wave_times.py): a
@@ -1132,12 +1139,15 @@ __device__ __forceinline__ WaveSphere wave_sphere(float pxf, float pyf, float pz
 }
 
 // Per-chunk bounding spheres of a resident cloud (one wave per 64 points),
-// read by the pass kernel instead of recomputing them every pass.
+// read by the pass kernel instead of recomputing them every pass. `nchunks`
+// may exceed ceil(n/64) (padding to whole pass workgroups): a chunk past the
+// cloud's end gets the zero-radius sphere of the last point, so a
+// hull-partitioned workgroup's empty second chunk reads a defined row.
 template <typename T>
-__global__ __launch_bounds__(kBlock) void chunk_sphere_kernel(const T* __restrict__ pts, int64_t n,
+__global__ __launch_bounds__(kBlock) void chunk_sphere_kernel(const T* __restrict__ pts, int64_t n, int64_t nchunks,
                                                               F4* __restrict__ out) {
   const int64_t base = ((int64_t)blockIdx.x * kBlock + threadIdx.x) & ~(int64_t)63;
-  if (base >= n) return;  // wave-uniform
+  if (base >= 64 * nchunks) return;  // wave-uniform
   const int64_t i = base + (threadIdx.x & 63);
   const bool valid = i < n;
   const int64_t ii = valid ? i : n - 1;
@@ -1928,26 +1938,30 @@ static size_t hpart_lds_bytes(const LocalModel& lm, int parts) {
          (size_t)kHpartBlock / parts * sizeof(double);
 }
 
-#ifndef FSDF_HPART_POINTS
-#define FSDF_HPART_POINTS 196608  // crossover measured between 196,608 and 262,144
-#endif
-#ifndef FSDF_HPART2_POINTS
-#define FSDF_HPART2_POINTS 393216  // 2 waves per chunk up to this size (crossover below 524,288)
-#endif
 // Waves per chunk of the hull-partitioned pass (pass_kernel HPART) for a cloud
-// of n points, 0 = the one-wave-per-chunk pass: kHpart (4) up to
-// FSDF_HPART_POINTS points, 2 up to FSDF_HPART2_POINTS (environment overrides
-// of the same names, read once per process; 0 disables a tier).
+// of n points, 0 = the one-wave-per-chunk pass: kHpart (4) up to the model's
+// hpart4 limit, 2 up to its hpart2 limit (LocalModel; fsdf_set_partition
+// overrides them per context, 0 disables a tier).
+void hpart_default_limits(const LocalModel& lm, int64_t* four, int64_t* two) {
+  // Measured crossovers (same-box A/B): M64 (64 hulls) 4-way up
+  // to 196,608 points, 2-way up to 393,216; IRB140 (7 hulls) — the partition
+  // splits a chunk's few candidate hulls over the waves, see the C2 sweep
+  // (profiles/r04/hpart_sweep_c2.json) — HPART_SMALL_* below.
+  if (lm.K >= kHpartFullHulls) {
+    *four = 196608;
+    *two = 393216;
+  } else {
+    *four = kHpartSmall4;
+    *two = kHpartSmall2;
+  }
+}
+
 int hpart_parts(const LocalModel& lm, int64_t n) {
-  static const int64_t limit4 = [] {
-    const char* e = getenv("FSDF_HPART_POINTS");
-    return e ? (int64_t)atoll(e) : (int64_t)FSDF_HPART_POINTS;
-  }();
-  static const int64_t limit2 = [] {
-    const char* e = getenv("FSDF_HPART2_POINTS");
-    return e ? (int64_t)atoll(e) : (int64_t)FSDF_HPART2_POINTS;
-  }();
   if (!(FSDF_RED_IN_STAGE && lm.planes64 && lm.S <= 64 && lm.R == 0 && n > 0)) return 0;
+  int64_t limit4, limit2;
+  hpart_default_limits(lm, &limit4, &limit2);
+  if (lm.hpart4_points >= 0) limit4 = lm.hpart4_points;
+  if (lm.hpart2_points >= 0) limit2 = lm.hpart2_points;
   const int parts = n <= limit4 ? kHpart : (n <= limit2 ? 2 : 0);
   if (!parts) return 0;
   const int64_t per = kHpartBlock / parts;  // points per workgroup
@@ -2054,6 +2068,24 @@ static void launch_lds(K kernel, int grid, int block, size_t lds, hipStream_t s,
   }
 }
 
+static thread_local char g_pass_name[96] = "";
+const char* last_pass_kernel() { return g_pass_name; }
+
+template <typename T> constexpr const char* type_name();
+template <> constexpr const char* type_name<double>() { return "double"; }
+template <> constexpr const char* type_name<float>() { return "float"; }
+
+// launch one pass_kernel variant and record its name (last_pass_kernel)
+template <typename T, int SLOTS, bool CULL, bool RBF, bool ALIAS = false, bool HPART = false, int NB = kPassBlock,
+          int NPART = kHpart>
+static void launch_pass_variant(int grid, size_t lds, hipStream_t s, const T* pts, int64_t n, const PassModel<T>& m,
+                                const PassOutputs& out) {
+  auto b = [](bool v) { return v ? "true" : "false"; };
+  snprintf(g_pass_name, sizeof g_pass_name, "pass_kernel<%s, %d, %s, %s, %s, %s, %d, %d>", type_name<T>(), SLOTS,
+           b(CULL), b(RBF), b(ALIAS), b(HPART), NB, NPART);
+  launch_lds(pass_kernel<T, SLOTS, CULL, RBF, ALIAS, HPART, NB, NPART>, grid, NB, lds, s, pts, n, m, out);
+}
+
 template <typename T, bool CULL, bool RBF>
 static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void* d_pts, int64_t n, int nblocks,
                           const PassOutputs& out, hipStream_t s) {
@@ -2064,22 +2096,21 @@ static void launch_pass_t(const LocalModel& lm, const PosedModel& pm, const void
     // one chunk per wave: the wrench rows alias the stage (pass_kernel ALIAS)
     if (const int parts = hpart_parts(lm, n)) {
       if (parts == kHpart)
-        launch_lds(pass_kernel<T, 1, CULL, false, true, true, kHpartBlock, kHpart>, nblocks, kHpartBlock,
-                   hpart_lds_bytes(lm, parts), s, pts, n, m, out);
+        launch_pass_variant<T, 1, CULL, false, true, true, kHpartBlock, kHpart>(nblocks, hpart_lds_bytes(lm, parts), s,
+                                                                                pts, n, m, out);
       else
-        launch_lds(pass_kernel<T, 1, CULL, false, true, true, kHpartBlock, 2>, nblocks, kHpartBlock,
-                   hpart_lds_bytes(lm, parts), s, pts, n, m, out);
+        launch_pass_variant<T, 1, CULL, false, true, true, kHpartBlock, 2>(nblocks, hpart_lds_bytes(lm, parts), s, pts,
+                                                                           n, m, out);
       return;
     }
     if (alias_pass(lm, n) && (int64_t)nblocks * kAliasBlock >= n) {
-      launch_lds(pass_kernel<T, 1, CULL, false, true, false, kAliasBlock>, nblocks, kAliasBlock, alias_lds_bytes(lm), s,
-                 pts, n, m, out);
+      launch_pass_variant<T, 1, CULL, false, true, false, kAliasBlock>(nblocks, alias_lds_bytes(lm), s, pts, n, m, out);
       return;
     }
   }
-  if (lm.S <= 64) launch_lds(pass_kernel<T, 1, CULL, RBF>, nblocks, kPassBlock, lds, s, pts, n, m, out);
-  else if (lm.S <= 128) launch_lds(pass_kernel<T, 2, CULL, RBF>, nblocks, kPassBlock, lds, s, pts, n, m, out);
-  else launch_lds(pass_kernel<T, 4, CULL, RBF>, nblocks, kPassBlock, lds, s, pts, n, m, out);
+  if (lm.S <= 64) launch_pass_variant<T, 1, CULL, RBF>(nblocks, lds, s, pts, n, m, out);
+  else if (lm.S <= 128) launch_pass_variant<T, 2, CULL, RBF>(nblocks, lds, s, pts, n, m, out);
+  else launch_pass_variant<T, 4, CULL, RBF>(nblocks, lds, s, pts, n, m, out);
 }
 
 // FSDF_BENCH_ONLY=1: A/B timing builds instantiate only the bench variant
@@ -2094,18 +2125,17 @@ static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm,
 #if FSDF_BENCH_ONLY
   const PassModel<T> m = pass_model<T>(lm, pm);
   const int parts = hpart_parts(lm, n);
+  const T* pts = (const T*)d_pts;
   if (parts == kHpart)
-    launch_lds(pass_kernel<T, 1, true, false, true, true, kHpartBlock, kHpart>, nblocks, kHpartBlock,
-               hpart_lds_bytes(lm, parts), s, (const T*)d_pts, n, m, out);
+    launch_pass_variant<T, 1, true, false, true, true, kHpartBlock, kHpart>(nblocks, hpart_lds_bytes(lm, parts), s,
+                                                                            pts, n, m, out);
   else if (parts == 2)
-    launch_lds(pass_kernel<T, 1, true, false, true, true, kHpartBlock, 2>, nblocks, kHpartBlock,
-               hpart_lds_bytes(lm, parts), s, (const T*)d_pts, n, m, out);
+    launch_pass_variant<T, 1, true, false, true, true, kHpartBlock, 2>(nblocks, hpart_lds_bytes(lm, parts), s, pts, n,
+                                                                       m, out);
   else if (alias_pass(lm, n) && (int64_t)nblocks * kAliasBlock >= n)
-    launch_lds(pass_kernel<T, 1, true, false, true, false, kAliasBlock>, nblocks, kAliasBlock, alias_lds_bytes(lm), s,
-               (const T*)d_pts, n, m, out);
+    launch_pass_variant<T, 1, true, false, true, false, kAliasBlock>(nblocks, alias_lds_bytes(lm), s, pts, n, m, out);
   else
-    launch_lds(pass_kernel<T, 1, true, false>, nblocks, kPassBlock, pass_lds_bytes(lm, false), s, (const T*)d_pts,
-               n, m, out);
+    launch_pass_variant<T, 1, true, false>(nblocks, pass_lds_bytes(lm, false), s, pts, n, m, out);
 #else
   if (lm.R > 0) {
     if (cull) launch_pass_t<T, true, true>(lm, pm, d_pts, n, nblocks, out, s);
@@ -2120,6 +2150,12 @@ static void launch_pass_p(bool cull, const LocalModel& lm, const PosedModel& pm,
 hipError_t launch_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const void* d_pts,
                        int64_t n, int nblocks, const PassOutputs& out, hipStream_t s, hipEvent_t ev_start,
                        hipEvent_t ev_stop) {
+  // the events belong to this call only: cleared on every exit (a refused or
+  // failed launch must not leave them for the next launch_lds on this thread)
+  struct ClearEvents {
+    ~ClearEvents() { g_pass_ev0 = g_pass_ev1 = nullptr; }
+  } clear_events;
+  g_pass_name[0] = 0;
   g_pass_ev0 = ev_start;
   g_pass_ev1 = ev_stop;
 #if FSDF_BENCH_ONLY
@@ -2180,14 +2216,15 @@ hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d
   return hipGetLastError();
 }
 
-hipError_t launch_chunk_spheres(int precision, const void* d_pts, int64_t n, float* d_out, hipStream_t s) {
+hipError_t launch_chunk_spheres(int precision, const void* d_pts, int64_t n, int64_t nchunks, float* d_out,
+                                hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
+  const unsigned grid = (unsigned)((64 * nchunks + kBlock - 1) / kBlock);
   if (precision == 64)
-    hipLaunchKernelGGL(chunk_sphere_kernel<double>, dim3(grid), dim3(kBlock), 0, s, (const double*)d_pts, n,
+    hipLaunchKernelGGL(chunk_sphere_kernel<double>, dim3(grid), dim3(kBlock), 0, s, (const double*)d_pts, n, nchunks,
                        (F4*)d_out);
   else
-    hipLaunchKernelGGL(chunk_sphere_kernel<float>, dim3(grid), dim3(kBlock), 0, s, (const float*)d_pts, n,
+    hipLaunchKernelGGL(chunk_sphere_kernel<float>, dim3(grid), dim3(kBlock), 0, s, (const float*)d_pts, n, nchunks,
                        (F4*)d_out);
   return hipGetLastError();
 }

@@ -76,6 +76,9 @@ _PROTOS = {
     "fsdf_pass_time": (c_int32, [c_void_p, POINTER(c_double), POINTER(c_int64)]),
     "fsdf_pass_times": (c_int32, [c_void_p, POINTER(c_double), POINTER(c_double), POINTER(c_int64)]),
     "fsdf_kernel_stats": (c_int32, [c_void_p, c_int32, c_void_p]),
+    "fsdf_pass_kernel_name": (ctypes.c_char_p, [c_void_p]),
+    "fsdf_set_partition": (c_int32, [c_void_p, c_int64, c_int64]),
+    "fsdf_get_partition": (c_int32, [c_void_p, c_int64, POINTER(c_int64), POINTER(c_int64), POINTER(c_int32)]),
     "fsdf_tree_transforms": (c_int32, [c_int32] + [c_void_p] * 13),
     "fsdf_config_gradient": (c_int32, [c_int32] + [c_void_p] * 7 + [c_int32] + [c_void_p] * 5),
     "fsdf_set_mechanism": (c_int32, [c_void_p, c_int32] + [c_void_p] * 8 + [c_int32] + [c_void_p] * 3),
@@ -308,6 +311,23 @@ class Context:
         check(self._lib.fsdf_pass_times(self._ctx, ctypes.byref(k), ctypes.byref(p), ctypes.byref(n)), self._ctx,
               "pass_times")
         return k.value, p.value, n.value
+
+    def pass_kernel_name(self) -> str:
+        """The pass-kernel variant of the last residual pass ('' before any)."""
+        return self._lib.fsdf_pass_kernel_name(self._ctx).decode()
+
+    def set_partition(self, four_way_max_points: int = -1, two_way_max_points: int = -1):
+        """Hull-partitioned pass tiers for this context: -1 = the model's
+        default, 0 = off, else the largest cloud the tier runs."""
+        check(self._lib.fsdf_set_partition(self._ctx, int(four_way_max_points), int(two_way_max_points)), self._ctx,
+              "set_partition")
+
+    def get_partition(self, n: int = 0):
+        """(4-way limit, 2-way limit, waves per chunk a pass over n points runs)."""
+        a, b, p = c_int64(0), c_int64(0), c_int32(0)
+        check(self._lib.fsdf_get_partition(self._ctx, int(n), ctypes.byref(a), ctypes.byref(b), ctypes.byref(p)),
+              self._ctx, "get_partition")
+        return a.value, b.value, p.value
 
     def set_mechanism(self, mechanism, surface_body, frame_R, frame_t):
         """Register the mechanism tree and each surface's body / frame for

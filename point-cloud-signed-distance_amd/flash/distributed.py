@@ -10,6 +10,16 @@ is per point, so the cloud shards trivially:
     RCCL (torch.distributed backend "nccl") between GPUs, gloo on CPU tests.
 The accumulator never leaves the device on the GPU path: fsdf_eval_device
 writes it into a torch tensor that is all-reduced in place.
+
+Overlap. The all-reduce is issued asynchronously (torch's RCCL stream waits
+on the pass through an event; the compute stream does not wait for the
+collective), and the functor keeps two accumulators, so the pass of the next
+configuration runs while the previous one's all-reduce is in flight
+(`value_and_gradient_many`, and bench.py's N > 1 step loop). A dependent
+iteration (the NaiveSolver: x_{k+1} needs ∂c/∂x at x_k) cannot hide it —
+there the host waits on the collective's completion only, not on a whole
+stream synchronize. Results are bit-identical with and without the overlap:
+every pass and every all-reduce sees the same inputs.
 """
 from __future__ import annotations
 
@@ -27,12 +37,16 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     return start, min(start + per, n)
 
 
-def allreduce_accum(accum, group=None):
-    """Sum the per-rank accumulators in place (torch tensor, any device)."""
+def allreduce_accum(accum, group=None, async_op=False):
+    """Sum the per-rank accumulators in place (torch tensor, any device).
+    async_op=True returns the collective's work handle (None on one rank):
+    `.wait()` orders the caller's current stream (RCCL) or the host (gloo)
+    after it."""
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(accum, op=dist.ReduceOp.SUM, group=group)
-    return accum
+        work = dist.all_reduce(accum, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+        return work if async_op else accum
+    return None if async_op else accum
 
 
 def chain_gradient(manip: Manipulator, x: np.ndarray, accum: np.ndarray, weight, solves=()) -> np.ndarray:
@@ -64,7 +78,10 @@ class ShardedCostFunctor:
         pts = torch.as_tensor(np.ascontiguousarray(local_points, np.float64).reshape(-1, 3), device=self.dev)
         self._pts = pts  # the context reads the resident copy (set_points_device does not own it)
         self.ctx.set_points_device(pts.data_ptr(), pts.shape[0])
-        self.accum = torch.zeros(self.ctx.accum_len, dtype=torch.float64, device=self.dev)
+        # two accumulators: the next pass may run while the previous all-reduce is in flight
+        self.accums = [torch.zeros(self.ctx.accum_len, dtype=torch.float64, device=self.dev) for _ in range(2)]
+        self.accum = self.accums[0]
+        self._slot = 0
         # pinned read-back of the all-reduced accumulator (a pageable .cpu()
         # goes through the runtime's staging buffer: ~10 us per iteration on
         # the single-GPU path, profiles/r02/experiments/r02pin)
@@ -86,18 +103,48 @@ class ShardedCostFunctor:
         if getattr(self.ctx, "_mechanism_of", None) != (self.manipulator, self.weight):
             register_native(self.manipulator, self.ctx, self.weight)
 
-    def launch(self, x):
-        """Enqueue one residual pass + all-reduce (asynchronous)."""
+    def launch(self, x, slot=None):
+        """Enqueue one residual pass into accumulator `slot` (default: the
+        other one than last time) and its all-reduce, asynchronously. Returns
+        (slot, work); `finish` turns it into the host accumulator."""
+        if slot is None:
+            slot = self._slot ^ 1
+        self._slot = slot
+        acc = self.accums[slot]
+        with self._on_stream():
+            if self._native:
+                self._ensure_native()
+                self.ctx.eval_state_device(np.asarray(x, np.float64), acc.data_ptr())
+            else:
+                unflatten(self.state, x)
+                normalize(self.state)
+                poses, self._solves = prepare_pass(self.ctx, self.manipulator, self.state.q,
+                                                   self.state.deformation_data)
+                self.ctx.eval_device(poses, acc.data_ptr())
+            work = allreduce_accum(acc, self.group, async_op=True)
+        self.accum = acc
+        return slot, work
+
+    def finish(self, pending, out=None):
+        """Wait for a launched pass's all-reduce and copy its accumulator to
+        host memory (`out`, default the pinned buffer); the host blocks on
+        this copy only."""
+        slot, work = pending
+        out = self.h_accum if out is None else out
+        with self._on_stream():
+            if work is not None:
+                work.wait()  # RCCL: the stream waits for the collective; gloo: the host does
+            out.copy_(self.accums[slot], non_blocking=True)
+            self._sync()
+        return out.numpy()
+
+    def _gradient(self, x, acc, solves):
         if self._native:
-            self._ensure_native()
-            self.ctx.eval_state_device(np.asarray(x, np.float64), self.accum.data_ptr())
-        else:
-            unflatten(self.state, x)
-            normalize(self.state)
-            poses, self._solves = prepare_pass(self.ctx, self.manipulator, self.state.q, self.state.deformation_data)
-            self.ctx.eval_device(poses, self.accum.data_ptr())
-        allreduce_accum(self.accum, self.group)
-        return self.accum
+            return self.ctx.state_gradient(x, acc)  # (re-prepares x's FK / solve if a later pass was enqueued)
+        unflatten(self.state, x)  # the state of THIS x (a pipelined later launch moved it)
+        normalize(self.state)
+        c = float(acc[0]) + _regularizer(self.state, self.weight)
+        return c, chain_gradient(self.manipulator, x, acc, self.weight, solves)
 
     def per_point(self, x):
         """(k*, d*, ∇d*) of this rank's shard at x, like CostFunctor.per_point (device
@@ -117,14 +164,24 @@ class ShardedCostFunctor:
 
     def value_and_gradient(self, x):
         x = np.asarray(x, np.float64)
-        # the pass runs on self.stream (given to the context); the all-reduce
-        # and the copy must be ordered after it whatever the caller's current
-        # stream is
-        with self._on_stream():
-            self.h_accum.copy_(self.launch(x), non_blocking=True)
-            self._sync()
-        acc = self.h_accum.numpy()
-        if self._native:
-            return self.ctx.state_gradient(x, acc)
-        c = float(acc[0]) + _regularizer(self.state, self.weight)
-        return c, chain_gradient(self.manipulator, x, acc, self.weight, self._solves)
+        acc = self.finish(self.launch(x))
+        return self._gradient(x, acc, getattr(self, "_solves", ()))
+
+    def value_and_gradient_many(self, xs):
+        """[(c, ∂c/∂x)] at independent configurations, pipelined: the pass at
+        xs[i+1] is enqueued before the host waits for the all-reduce of xs[i],
+        so the collective's latency hides behind the next pass. Bit-identical
+        to [value_and_gradient(x) for x in xs]."""
+        xs = [np.asarray(x, np.float64) for x in xs]
+        out = []
+        pending, solves = None, ()
+        for x in xs:
+            nxt = self.launch(x)  # the other accumulator than `pending`'s
+            nxt_solves = getattr(self, "_solves", ())
+            if pending is not None:
+                xp, pp = pending
+                out.append(self._gradient(xp, self.finish(pp, self.torch.empty_like(self.h_accum)), solves))
+            pending, solves = (x, nxt), nxt_solves
+        if pending is not None:
+            out.append(self._gradient(pending[0], self.finish(pending[1]), solves))
+        return out

@@ -183,3 +183,43 @@ def test_gloo_world2_sharded_cost_functor(name):
     assert np.array_equal(np.concatenate([r[4] for r in res]), k1)
     assert np.array_equal(np.concatenate([r[5] for r in res]), d1)
     assert np.abs(g1).max() > 0
+
+
+def _pipelined_worker(rank, world, port, q, name):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from flash.distributed import ShardedCostFunctor, shard_range
+        m, pts, x = _scene(name)
+        a, b = shard_range(len(pts), rank, world)
+        f = ShardedCostFunctor(m, pts[a:b], rank, world, engine=OracleEngine(m))
+        xs = [x + 1e-3 * i for i in range(4)]
+        seq = [f.value_and_gradient(xi) for xi in xs]
+        pip = f.value_and_gradient_many(xs)
+        q.put((rank, seq, pip))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["irb140", "beanbag_rbf"])
+def test_gloo_world2_pipelined_allreduce_same_bits(name):
+    """value_and_gradient_many (the pass of x_{i+1} enqueued before the
+    all-reduce of x_i is waited for; two accumulators, async collective) gives
+    the same bits as one value_and_gradient per configuration, on 2 gloo ranks."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, 2, port, q, name)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, seq, pip in res:
+        assert len(seq) == len(pip) == 4
+        for (c1, g1), (c2, g2) in zip(seq, pip):
+            assert c1 == c2 and np.array_equal(g1, g2)
+        assert len({c for c, _ in seq}) == 4  # the configurations differ

@@ -103,8 +103,10 @@ def test_fused_rbf_needs_declared_centres():
 
 def test_state_split_and_validation():
     """fsdf_eval_state_device + fsdf_state_gradient (the sharded path's halves)
-    equal fsdf_value_and_gradient; the chain rule refuses an x other than the
-    pass's; deformation rows beyond fsdf_set_deformations are refused."""
+    equal fsdf_value_and_gradient, also pipelined (two passes in flight, the
+    chain rule of the first after the second was enqueued: its host FK / RBF
+    solve is redone, bit for bit); deformation rows beyond
+    fsdf_set_deformations are refused."""
     import os
     import torch
     from conftest import GOLDEN
@@ -123,8 +125,17 @@ def test_state_split_and_validation():
     c2, g2 = ctx.state_gradient(x, acc.cpu().numpy())
     ctx.set_stream(None)
     assert c2 == c1 and np.array_equal(g2, g1)
-    with pytest.raises(FlashNativeError):
-        ctx.state_gradient(x + 1e-3, acc.cpu().numpy())
+    x2 = x + 1e-3
+    c4, g4 = cf.value_and_gradient(x2)
+    acc2 = torch.zeros_like(acc)
+    ctx.set_stream(torch.cuda.current_stream(0).cuda_stream)
+    ctx.eval_state_device(x, acc.data_ptr())
+    ctx.eval_state_device(x2, acc2.data_ptr())
+    c5, g5 = ctx.state_gradient(x, acc.cpu().numpy())
+    c6, g6 = ctx.state_gradient(x2, acc2.cpu().numpy())
+    ctx.set_stream(None)
+    assert c5 == c1 and np.array_equal(g5, g1)
+    assert c6 == c4 and np.array_equal(g6, g4)
     ctx.set_deformations(1, 10.0)  # the squishable's 13 deformable points need 13 rows
     with pytest.raises(FlashNativeError):
         ctx.value_and_gradient(x[:m.mechanism.num_positions + 3])

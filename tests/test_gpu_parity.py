@@ -309,28 +309,45 @@ def test_resident_order_outputs(m64, oracle_mod, ctx_factory):
     assert np.array_equal(k0, kc) and np.array_equal(d0, dc)
 
 
-@pytest.mark.parametrize("n", [196608, 393216])
-def test_hull_partitioned_pass_matches_one_wave_per_chunk(m64, ctx_factory, n):
-    """Clouds of <= 196,608 points (FSDF_HPART_POINTS) run the hull-partitioned
-    pass with 4 waves per chunk, <= 393,216 (FSDF_HPART2_POINTS) with 2 (pass_kernel
-    HPART: hull k goes to wave k % parts, lexicographic (d, k) merge); one point
-    more runs the next tier (2 waves per chunk, then one wave per chunk).
-    Per-point outputs do not depend on the block structure: the shared points
-    must agree bit for bit, sums to rounding."""
+@pytest.mark.parametrize("model", ["m64", "irb"])
+@pytest.mark.parametrize("tier", [4, 2])
+def test_hull_partitioned_pass_matches_one_wave_per_chunk(m64, irb, ctx_factory, model, tier):
+    """Clouds up to the model's 4-way limit run the hull-partitioned pass with
+    4 waves per chunk, up to its 2-way limit with 2 (pass_kernel HPART: hull k
+    goes to wave k % parts, lexicographic (d, k) merge; limits per model,
+    fsdf_get_partition); one point more runs the next tier (2 waves per chunk,
+    then one wave per chunk). Per-point outputs do not depend on the block
+    structure: the shared points agree bit for bit, sums to rounding. The
+    same cloud with the tiers forced off (fsdf_set_partition) agrees too."""
     from flash import synthetic
     import flash
-    qt, qe = synthetic.perturbed_configuration(m64, 303)
-    poses = flash.hull_poses(m64, qe)
-    pts = synthetic.depth_cloud(m64, qt, n + 1, seed=304, order="shuffled")
+    m = {"m64": m64, "irb": irb}[model]
+    probe = ctx_factory(m)
+    lim4, lim2, _ = probe.get_partition(0)
+    n = lim4 if tier == 4 else lim2
+    if n <= 0:
+        pytest.skip(f"{model}: the {tier}-way tier is off by default")
+    assert probe.get_partition(n)[2] == tier
+    assert probe.get_partition(n + 1)[2] == (2 if tier == 4 and lim2 > n else 0)
+    qt, qe = synthetic.perturbed_configuration(m, 303)
+    poses = flash.hull_poses(m, qe)
+    pts = synthetic.depth_cloud(m, qt, n + 1, seed=304, order="shuffled")
     out = {}
     for cull in (True, False):
-        for m in (n, n + 1):
-            ctx = ctx_factory(m64, cull=cull)
-            ctx.set_points(pts[:m])
-            out[cull, m] = ctx.eval(poses, per_point=True)
+        for mm in (n, n + 1):
+            ctx = ctx_factory(m, cull=cull)
+            ctx.set_points(pts[:mm])
+            out[cull, mm] = ctx.eval(poses, per_point=True)
+            assert ctx.pass_kernel_name().endswith(f"true, true, 256, {tier}>") == (mm == n), ctx.pass_kernel_name()
+    forced = ctx_factory(m)
+    forced.set_partition(0, 0)
+    forced.set_points(pts[:n])
+    _, _, (kf, df, gf) = forced.eval(poses, per_point=True)
+    assert forced.pass_kernel_name().endswith("true, false, 256, 4>")  # ALIAS, not HPART
     for cull in (True, False):
         (c1, a1, (k1, d1, g1)), (c0, a0, (k0, d0, g0)) = out[cull, n], out[cull, n + 1]
         assert np.array_equal(k1, k0[:n]) and np.array_equal(d1, d0[:n]) and np.array_equal(g1, g0[:n])
+        assert np.array_equal(k1, kf) and np.array_equal(d1, df) and np.array_equal(g1, gf)
         assert c1 == pytest.approx(np.dot(d1, d1), rel=1e-10)
     # culled and brute force share the partitioned block structure: identical sums
     assert np.array_equal(out[True, n][1], out[False, n][1])

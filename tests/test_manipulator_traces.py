@@ -129,9 +129,8 @@ def test_clip_is_componentwise():
 # ----------------------------------------------- this repo's landscape (oracle)
 
 
-@pytest.fixture(scope="module")
-def landscape(oracle_mod):
-    """(cost(x), value_and_gradient(x)) of the notebook scene on the C oracle:
+def oracle_landscape(oracle_mod):
+    """(cost(x), value_and_gradient(x), N) of the notebook scene on the C oracle:
     the sensed cloud raycast at x_true, cost undivided (the callback's c)."""
     import test_notebook_pins as P
     from flash import Models
@@ -154,6 +153,11 @@ def landscape(oracle_mod):
         a, solves = acc(x)
         return float(a[0]), gradient_from_accum(m, np.asarray(x, np.float64), a, solves, 10.0)
     return cost, value_and_gradient, len(pts)
+
+
+@pytest.fixture(scope="module")
+def landscape(oracle_mod):
+    return oracle_landscape(oracle_mod)
 
 
 def run_notebook_trial(value_and_gradient, x0, solver_kw):

@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Hull-partitioned pass tiers against cloud size, per model (run on the GPU box).
+
+For every size and every forced tier — 4 waves per chunk, 2, one wave per
+chunk (fsdf_set_partition) — the bench's step (pose + pass + reduce on the
+resident, Hilbert-sorted cloud, per-point outputs written; two alternating
+configurations) is timed, interleaved over rounds on one context, and the pass
+kernel's own HIP-event time recorded; then the model's default tier and what
+it picks. One JSON line per (size, tier); min over rounds.
+
+    python tools/hpart_sweep.py --model irb140 --sizes 65536,131072,196608,262144,393216,524288
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "point-cloud-signed-distance_amd"))
+
+TIERS = {"4-way": (1 << 40, 0), "2-way": (0, 1 << 40), "one-wave": (0, 0), "default": (-1, -1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="irb140", choices=("irb140", "arm_grid"))
+    ap.add_argument("--sizes", default="65536,131072,196608,262144,393216,524288")
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--seed", type=int, default=1234)
+    a = ap.parse_args()
+    import torch
+    import flash
+    from flash import Models, synthetic
+    dev = torch.device("cuda", 0)
+    m = getattr(Models, a.model)()
+    qt, qe = synthetic.perturbed_configuration(m, a.seed)
+    poses = [flash.hull_poses(m, qe), flash.hull_poses(m, qe + 1e-3)]
+    ctx = m.engine(device=0, precision=64, cull=True, sort_points=True)
+    ctx.set_output_order(True)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+    accum = torch.zeros(ctx.accum_len, dtype=torch.float64, device=dev)
+    for n in (int(s) for s in a.sizes.split(",")):
+        pts = synthetic.depth_cloud(m, qt, n, seed=a.seed + 17, order="shuffled")
+        d_pts = torch.as_tensor(pts, device=dev)
+        ctx.set_points_device(d_pts.data_ptr(), n)
+        bufs = (torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.float64, device=dev),
+                torch.empty((n, 3), dtype=torch.float64, device=dev))
+        outs = tuple(b.data_ptr() for b in bufs)
+        best = {}
+        for _ in range(a.rounds):
+            for tier, lim in TIERS.items():
+                ctx.set_partition(*lim)
+                for i in range(5):
+                    ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs)
+                torch.cuda.synchronize()
+                ctx.profile_pass(True)
+                t0 = time.perf_counter()
+                for i in range(a.steps):
+                    ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs)
+                torch.cuda.synchronize()
+                step = (time.perf_counter() - t0) / a.steps * 1e3
+                kms, pms, launches = ctx.pass_times()
+                ctx.profile_pass(False)
+                row = best.setdefault(tier, {"step_ms": 1e9, "pass_kernel_ms": 1e9})
+                row["step_ms"] = min(row["step_ms"], step)
+                row["pass_kernel_ms"] = min(row["pass_kernel_ms"], kms / launches)
+                row["kernel"] = ctx.pass_kernel_name()
+        ctx.set_partition(-1, -1)
+        lim4, lim2, parts = ctx.get_partition(n)
+        for tier, row in best.items():
+            print(json.dumps({"model": a.model, "hulls": ctx.K, "points": n, "tier": tier, **row,
+                              "default_limits": [lim4, lim2], "default_parts": parts}), flush=True)
+        del d_pts, bufs
+
+
+if __name__ == "__main__":
+    main()

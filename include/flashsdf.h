@@ -327,6 +327,21 @@ int fsdf_set_partition(fsdf_ctx* ctx, int64_t four_way_max_points, int64_t two_w
 int fsdf_get_partition(fsdf_ctx* ctx, int64_t n, int64_t* four_way_max_out, int64_t* two_way_max_out,
                        int32_t* parts_out);
 
+/* ---- planned pass --------------------------------------------------------------
+ * Resident-cloud passes of f64 hull-only scenes with <= 64 surfaces (the
+ * metric's M64, IRB140) run a planned grid: every 64-point chunk writes its
+ * own partial row (so the accumulator sums chunks in index order, bit-identical
+ * whatever the plan), records its duration, and from the cloud's first pass on
+ * (rebuilt every 16 passes) the heaviest chunks — `four_way_share` of them —
+ * are split over 4 waves (hull-partitioned), the next `two_way_share` over 2,
+ * the rest run one wave each grouped by similar cost, heaviest workgroups
+ * first. enable = 0 runs the unplanned one-block-per-4-chunks grid instead
+ * (A/B). Defaults: enabled, 1/32 and 1/16; at least as many chunks go 4 ways
+ * as the device has idle wave slots for (a strong-scaling shard smaller than
+ * the machine splits its heaviest third). A new cloud's first pass runs the
+ * tier shape of fsdf_set_partition. */
+int fsdf_set_plan(fsdf_ctx* ctx, int32_t enable, double four_way_share, double two_way_share);
+
 /* Kernel work counters (diagnostics). enable=1 zeroes and starts counting in
  * every following pass; enable=0 stops and writes the counters:
  *   [0] wave-iterations (64 points each)  [1] hull evaluations (per wave)

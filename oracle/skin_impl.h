@@ -296,6 +296,9 @@ void RF(oracle_hull_sdf)(const RF(oracle_posed) * m, int32_t k, const R* p, R* d
   /* stage B: descent walk (<= 24 steps), each step to a face the failed
    * certificate names, accepted only if strictly closer */
   int cf = fs, cr = rA, todo = 1;
+#ifdef ORACLE_WALK_HOOK /* tools/walk_study.c: descent-walk lengths (not defined in liboracle.so) */
+  int walked = 0;
+#endif
   for (int step = 0; step < 24; ++step) {
     int n1, n2;
     if (RF(cert_step)(m, p, cf, cr, scale, &n1, &n2)) { todo = 0; break; }
@@ -311,7 +314,13 @@ void RF(oracle_hull_sdf)(const RF(oracle_posed) * m, int32_t k, const R* p, R* d
       }
     }
     if (!moved) break;
+#ifdef ORACLE_WALK_HOOK
+    ++walked;
+#endif
   }
+#ifdef ORACLE_WALK_HOOK
+  ORACLE_WALK_HOOK(walked, todo);
+#endif
   if (todo) {
     /* stage C: continues from the walk's point; only a strictly closer face replaces it */
     R b2 = best2, b[3] = {q[0], q[1], q[2]};

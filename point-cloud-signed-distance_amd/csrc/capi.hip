@@ -115,6 +115,19 @@ struct fsdf_ctx {
   int32_t* d_block_order = nullptr;  // [kMaxBlocks]
   int order_nblocks = 0;             // grid the order was built for (0: none yet)
   int order_age = 0;                 // passes since the order was rebuilt
+  // planned pass (fsdf::planned_pass_kernel): per-chunk partial rows, chunk
+  // durations and the workgroup plan built from them (fsdf_set_plan)
+  fsdf::ChunkOutputs co;             // device arrays, [co_cap] chunks
+  int64_t co_cap = 0;
+  int32_t* d_plan = nullptr;         // [plan_cap][4]
+  int32_t* d_plan_order = nullptr;   // [co_cap] plan_kernel scratch
+  int64_t plan_cap = 0;
+  int plan_grid = 0;                 // workgroups of the current plan (0: none — the default shape)
+  int64_t plan_nc = -1;              // chunks the plan was built for
+  int plan_age = 0;                  // planned passes since the plan was rebuilt
+  int plan_enable = 1;
+  double plan_f4 = 1.0 / 32, plan_f2 = 1.0 / 16;  // shares of the chunks split over 4 / 2 waves
+  int wave_slots = 0;                // device wave slots at the pass's occupancy (0: not queried yet)
   double* d_accum = nullptr;
   int32_t* d_kstar = nullptr;
   double* d_d = nullptr;
@@ -209,6 +222,7 @@ static void free_model(fsdf_ctx* c) {
   dfree(c->d_accum);
   // (the partition tiers are a context setting: they survive a model change)
   const int64_t h4 = c->lm.hpart4_points, h2 = c->lm.hpart2_points;
+  c->plan_nc = -1;
   c->lm = fsdf::LocalModel();
   c->lm.hpart4_points = h4;
   c->lm.hpart2_points = h2;
@@ -272,6 +286,13 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   dfree(c->d_stats);
   dfree(c->d_block_cost);
   dfree(c->d_block_order);
+  dfree(c->co.hdr);
+  dfree(c->co.ent);
+  dfree(c->co.csum);
+  dfree(c->co.dense);
+  dfree(c->co.dur);
+  dfree(c->d_plan);
+  dfree(c->d_plan_order);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (int i = 0; i < kPoseRing; ++i) {
     if (c->pose_ev[i]) (void)hipEventDestroy(c->pose_ev[i]);
@@ -738,6 +759,7 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
   // the caller may reuse its buffer once this returns
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   c->n = n;
+  c->plan_nc = -1;  // a new cloud: its first planned pass runs the default shape and measures
   return FSDF_OK;
 }
 
@@ -814,6 +836,87 @@ static int release_posed(fsdf_ctx* c, int buf) {
 #endif
 static constexpr int kOrderEvery = FSDF_ORDER_EVERY;
 
+static int ensure_chunk_outputs(fsdf_ctx* c, int64_t nc) {
+  if (c->co_cap >= nc) return FSDF_OK;
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  dfree(c->co.hdr);
+  dfree(c->co.ent);
+  dfree(c->co.csum);
+  dfree(c->co.dense);
+  dfree(c->co.dur);
+  dfree(c->d_plan_order);
+  c->co_cap = 0;
+  c->plan_nc = -1;
+  HIPCHECK(c, hipMalloc(&c->co.hdr, (size_t)nc * 4 * sizeof(int32_t)));
+  HIPCHECK(c, hipMalloc(&c->co.ent, (size_t)nc * 24 * sizeof(double)));
+  HIPCHECK(c, hipMalloc(&c->co.csum, (size_t)nc * sizeof(double)));
+  HIPCHECK(c, hipMalloc(&c->co.dense, (size_t)nc * 64 * 6 * sizeof(double)));
+  HIPCHECK(c, hipMalloc(&c->co.dur, (size_t)nc * sizeof(uint32_t)));
+  HIPCHECK(c, hipMalloc(&c->d_plan_order, (size_t)nc * sizeof(int32_t)));
+  c->co_cap = nc;
+  return FSDF_OK;
+}
+
+// the plan's composition for nc chunks: n4 chunks over 4 waves, n2 over 2,
+// the rest one wave each. The heaviest `plan_f4` / `plan_f2` shares are split,
+// and at least as many chunks over 4 waves as the device's idle wave slots
+// allow (slots - nc, 3 extra waves per split chunk): a strong-scaling shard
+// that leaves slots free splits its heavy third, a full machine only its tail.
+static void plan_shape(fsdf_ctx* c, int64_t nc, int* n4, int* n2) {
+  if (c->wave_slots == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0)
+      cus = 256;
+    c->wave_slots = cus * 4 * 4;  // 4 SIMDs x 4 waves (the pass's register budget)
+  }
+  const int64_t spare = std::max<int64_t>(0, (int64_t)c->wave_slots - nc);
+  const int64_t a = std::min<int64_t>(nc, std::max<int64_t>(llround(c->plan_f4 * (double)nc), spare / 3));
+  *n4 = (int)a;
+  *n2 = (int)std::min<int64_t>(nc - a, llround(c->plan_f2 * (double)nc));
+}
+
+// The planned pass of a resident cloud: per-chunk partial rows, the
+// two-level chunk reduction, and a plan rebuilt from this pass's chunk
+// durations on the first pass of a cloud and then every kOrderEvery passes.
+static int run_planned(fsdf_ctx* c, const fsdf::PosedModel& P, const void* d_pts, int64_t n, double* d_accum,
+                       fsdf::PassOutputs& out, hipEvent_t* pe) {
+  const int64_t nc = (n + 63) / 64;
+  int rc = ensure_chunk_outputs(c, nc);
+  if (rc) return rc;
+  rc = ensure_partials(c, (int)((nc + fsdf::kChunkGroup - 1) / fsdf::kChunkGroup));
+  if (rc) return rc;
+  out.partials = c->d_partials;
+  out.cost = nullptr;
+  out.order = nullptr;
+  fsdf::ChunkOutputs co = c->co;
+  const bool planned = c->plan_nc == nc && c->plan_grid > 0;
+  co.plan = planned ? c->d_plan : nullptr;
+  const int dparts = fsdf::hpart_parts(c->lm, n);
+  co.dparts = dparts ? dparts : 1;
+  const int grid = planned ? c->plan_grid : (int)((nc * co.dparts + 3) / 4);
+  HIPCHECK(c, fsdf::launch_planned_pass(c->precision, c->cull != 0, c->lm, P, d_pts, n, grid, out, co, c->stream,
+                                        pe ? pe[0] : nullptr, pe ? pe[1] : nullptr));
+  c->pass_kernel = fsdf::last_pass_kernel();
+  HIPCHECK(c, fsdf::launch_reduce_chunks(co, nc, c->lm.S, c->d_partials, d_accum, c->stream, pe ? pe[2] : nullptr));
+  if (!planned || ++c->plan_age >= kOrderEvery) {
+    int n4, n2;
+    plan_shape(c, nc, &n4, &n2);
+    const int64_t g = n4 + (n2 + 1) / 2 + (nc - n4 - n2 + 3) / 4;
+    if (c->plan_cap < g) {
+      HIPCHECK(c, hipStreamSynchronize(c->stream));
+      dfree(c->d_plan);
+      c->plan_cap = 0;
+      HIPCHECK(c, hipMalloc(&c->d_plan, (size_t)g * 4 * sizeof(int32_t)));
+      c->plan_cap = g;
+    }
+    HIPCHECK(c, fsdf::launch_plan(c->co.dur, nc, n4, n2, c->d_plan_order, c->d_plan, c->stream));
+    c->plan_grid = (int)g;
+    c->plan_nc = nc;
+    c->plan_age = 0;
+  }
+  return FSDF_OK;
+}
+
 // schedule: resident-cloud passes (repeated over the same cloud) launch their
 // workgroups heaviest-first by the previous pass's durations
 static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t n, double* d_accum,
@@ -835,6 +938,14 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
   out.perm = d_perm;
   out.stats = c->stats_on ? c->d_stats : nullptr;
   out.chunk_ws = FSDF_CHUNK_WS && d_pts == c->d_pts && n == c->n ? c->d_chunk_ws : nullptr;  // resident cloud only
+  if (schedule && n > 0 && c->plan_enable && c->precision == 64 && fsdf::planned_pass(c->lm, n)) {
+    const bool prof = c->profiling && c->prof_used + 3 <= c->prof_ev.size();
+    hipEvent_t* pe = prof ? &c->prof_ev[c->prof_used] : nullptr;
+    rc = run_planned(c, *P, d_pts, n, d_accum, out, pe);
+    if (rc) return rc;
+    if (prof) c->prof_used += 3;
+    return release_posed(c, pbuf);
+  }
   if (schedule && n > 0) {
     if (!c->d_block_cost) {
       HIPCHECK(c, hipMalloc(&c->d_block_cost, fsdf::kMaxBlocks * sizeof(uint32_t)));
@@ -900,6 +1011,17 @@ extern "C" int fsdf_get_partition(fsdf_ctx* c, int64_t n, int64_t* four_way_max_
 }
 
 extern "C" const char* fsdf_pass_kernel_name(const fsdf_ctx* c) { return c ? c->pass_kernel.c_str() : ""; }
+
+extern "C" int fsdf_set_plan(fsdf_ctx* c, int32_t enable, double four_way_share, double two_way_share) {
+  if (!c) return FSDF_ERR_ARG;
+  if (!(four_way_share >= 0.0 && four_way_share <= 1.0 && two_way_share >= 0.0 && two_way_share <= 1.0))
+    return fail(c, FSDF_ERR_ARG, "set_plan: shares must lie in [0, 1]");
+  c->plan_enable = enable != 0;
+  c->plan_f4 = four_way_share;
+  c->plan_f2 = two_way_share;
+  c->plan_nc = -1;  // rebuilt on the next pass
+  return FSDF_OK;
+}
 
 extern "C" int fsdf_set_output_order(fsdf_ctx* c, int32_t order) {
   if (!c) return FSDF_ERR_ARG;

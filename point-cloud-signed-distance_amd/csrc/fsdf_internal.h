@@ -139,6 +139,33 @@ struct PassOutputs {
   const float* chunk_ws = nullptr;
 };
 
+// Planned pass (sdf_kernels.hip planned_pass_kernel): per-chunk partial rows
+// of a resident cloud (nc = ceil(n/64) chunks) and the workgroup plan.
+struct ChunkOutputs {
+  int32_t* hdr = nullptr;      // [nc][4] surfaces of entries 0..3 (-1: none); [c][0] == -2: dense row
+  double* ent = nullptr;       // [nc][4][6] (F, M) of each entry
+  double* csum = nullptr;      // [nc] Σ d² over the chunk's points
+  double* dense = nullptr;     // [nc][64][6] (F, M) per surface (chunks with > 4 surfaces)
+  uint32_t* dur = nullptr;     // [nc] serial-equivalent chunk durations (100 MHz ticks)
+  const int32_t* plan = nullptr;  // [grid][4] workgroup plan (chunk | parts << 24, chunk, chunk, chunk), or null
+  int dparts = 1;              // waves per chunk without a plan (4, 2 or 1)
+};
+constexpr int kPlanPartsShift = 24;
+constexpr int kChunkGroup = 16;          // chunks per level-1 reduce wave
+constexpr int64_t kMaxPlanChunks = 1 << 16;  // planned passes: clouds of <= 4,194,304 points per device
+
+// a resident pass over n points of this model can run planned
+bool planned_pass(const LocalModel& lm, int64_t n);
+hipError_t launch_planned_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const void* d_pts,
+                               int64_t n, int grid, const PassOutputs& out, const ChunkOutputs& co, hipStream_t s,
+                               hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+// level 1 (per group of kChunkGroup chunks into `partials` line tiles) + level 2
+// (reduce_tiles over the groups) -> d_accum [1 + 6S]
+hipError_t launch_reduce_chunks(const ChunkOutputs& co, int64_t nc, int S, double* partials, double* d_accum,
+                                hipStream_t s, hipEvent_t ev_stop = nullptr);
+// the plan of the next passes from the chunk durations of this one
+hipError_t launch_plan(const uint32_t* dur, int64_t nc, int n4, int n2, int32_t* order, int32_t* plan, hipStream_t s);
+
 // Surfaces whose poses ride in the pose kernel's arguments (12·64 doubles =
 // 6 KiB of kernarg; larger scenes upload them with a copy).
 constexpr int kPoseArgMax = 64;

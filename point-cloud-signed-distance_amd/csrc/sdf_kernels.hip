@@ -1347,11 +1347,18 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   // a pruning bound as this wave's own best (a stale read only bounds less).
   // (One slot read per test: 2.6 % faster at 2^17 than a slot per wave, a
   // cached copy refreshed per evaluation no faster; profiles/r03/experiments)
+  // (NSHARE == 0: shared iff shbest is given — the planned pass decides per
+  // workgroup at run time)
   auto bound_now = [&]() -> T {
     T b = best;
     if constexpr (NSHARE > 1) {
       const T o = (T)((const volatile double*)shbest)[lane];
       b = o < b ? o : b;
+    } else if constexpr (NSHARE == 0) {
+      if (shbest) {
+        const T o = (T)((const volatile double*)shbest)[lane];
+        b = o < b ? o : b;
+      }
     }
     return b;
   };
@@ -1383,6 +1390,8 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
     if (need && (dk < best || (dk == best && ks < bk))) { best = dk; bk = ks; gx = hx; gy = hy; gz = hz; }
     if constexpr (NSHARE > 1)  // (one slot per lane: the minimum over the chunk's waves, ds_min_f64)
       __hip_atomic_fetch_min(shbest + lane, (double)best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else if constexpr (NSHARE == 0)
+      if (shbest) __hip_atomic_fetch_min(shbest + lane, (double)best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
   uint64_t done[SLOTS];
 #pragma unroll
@@ -1443,7 +1452,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
 // segmented by k* (ballot loop + DPP wave sums) into the LDS rows owned by
 // lane k, then the per-point outputs. Whole wave active.
 template <typename T, int SLOTS, bool RBF>
-__device__ __forceinline__ void emit_chunk(T px, T py, T pz, bool valid, T best, int bk, T gx, T gy, T gz, int64_t i,
+__device__ __forceinline__ uint64_t emit_chunk(T px, T py, T pz, bool valid, T best, int bk, T gx, T gy, T gz, int64_t i,
                                            int64_t base, int64_t n, const PassModel<T>& m, const PassOutputs& out,
                                            double* __restrict__ acc_row, double& cost_acc,
                                            double* __restrict__ rbf_wave, T* __restrict__ stage, int stage_cap) {
@@ -1463,11 +1472,13 @@ __device__ __forceinline__ void emit_chunk(T px, T py, T pz, bool valid, T best,
   }
   const uint64_t tw = wt_now();
   uint64_t pending = __ballot(valid);
+  uint64_t touched = 0;  // surfaces (k & 63) of this chunk's points
   while (pending) {
     const int leader = __builtin_ctzll(pending);
     const int kk = __builtin_amdgcn_readfirstlane(__shfl(bk, leader, 64));
     const bool sel = valid && (bk == kk);
     pending &= ~__ballot(sel);
+    touched |= 1ull << (kk & 63);
     if (RBF && m.surface_kind[kk] != 0) {
       // RBF skin: adjoint sums instead of a rigid wrench
       int r = 0;
@@ -1530,6 +1541,7 @@ __device__ __forceinline__ void emit_chunk(T px, T py, T pz, bool valid, T best,
     }
   }
   wt_add(6, tw);
+  return touched;
 }
 
 // Per-block partial sums in line tiles: entry t of logical block b at
@@ -1742,6 +1754,264 @@ __global__ __launch_bounds__(NB) __attribute__((
     out.stats[33 + 16 * kMaxBlocks + 2 * lb] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// Planned pass: resident clouds of hull-only scenes with <= 64 surfaces whose
+// fp64 planes are staged (the aliased layout, pass_kernel ALIAS / HPART).
+//
+// Launch slot b runs plan[b], one of three workgroup shapes — 4 chunks of 64
+// points one wave each; 2 chunks over 2 waves each; 1 chunk over all 4 waves
+// (hull-partitioned: wave j evaluates the hulls k = j mod parts, bests shared
+// through one ds_min_f64 slot per lane, merged by the first-index (d, k) rule,
+// exactly as pass_kernel HPART) — chosen per chunk from the chunks' measured
+// durations (plan_kernel: the heaviest chunks split over 4 or 2 waves, the
+// rest grouped by similar cost, heaviest workgroups first). The pass is bound
+// by its heaviest chunks' serial hull evaluations (~100 us at 2^20 points
+// against ~70 us of average wave work); a per-chunk split only
+// where it pays leaves the rest of the grid one wave per chunk. Without a
+// plan (a new cloud's first pass) slot b runs `dparts` waves per chunk in
+// index order — the size tiers of hpart_parts.
+//
+// Every chunk writes its OWN partial row — the chunk's Σ d², and its wrench
+// sums (F, M) per nearest surface as up to 4 (k, F, M) entries, or a dense
+// [64][6] row when more than 4 surfaces meet in the chunk — so the
+// accumulator (reduce_chunks_kernel over fixed groups of kChunkGroup chunks,
+// then reduce_tiles_kernel) sums the chunks in index order whatever the plan:
+// bit-identical across plans, schedules and passes. No block combine, no
+// barrier after the prologue for one-wave chunks.
+// ---------------------------------------------------------------------------
+constexpr int kPlanChunkMask = (1 << kPlanPartsShift) - 1;
+
+template <typename T, bool CULL>
+__global__ __launch_bounds__(kPassBlock) __attribute__((amdgpu_waves_per_eu(kPassWavesPerSimd))) void planned_pass_kernel(
+    const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out, ChunkOutputs co) {
+  static_assert(kPassBlock == 256, "the planned pass runs 4-wave workgroups");
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  HullRow* ht = (HullRow*)fsdf_lds;
+  char* stages = (char*)(ht + m.K + 1);
+  T* stage = (T*)(stages + wave * m.stage_bytes);
+  double* shb_all = (double*)(stages + 4 * m.stage_bytes);  // [4][64] shared per-lane bests
+  uint64_t* t0_lds = (uint64_t*)(shb_all + 4 * 64);         // [4] chunk start times
+  // this wave's (waves per chunk, chunk): re-read after the scene evaluation
+  // rather than kept live through it (scalar registers are spilled to vector
+  // lanes at this kernel's register budget)
+  auto slot_of = [&](int& parts_, int& cid_) {
+    if (co.plan) {
+      const I4 e = ((const I4*)co.plan)[blockIdx.x];
+      parts_ = (e[0] >> kPlanPartsShift) & 7;
+      const int sl = wave / parts_;
+      cid_ = sl == 0 ? (e[0] & kPlanChunkMask) : (sl == 1 ? e[1] : (sl == 2 ? e[2] : e[3]));
+    } else {
+      parts_ = co.dparts;
+      cid_ = (int)blockIdx.x * (4 / parts_) + wave / parts_;
+    }
+    parts_ = __builtin_amdgcn_readfirstlane(parts_);
+    cid_ = __builtin_amdgcn_readfirstlane(cid_);
+  };
+  int parts, cid;
+  slot_of(parts, cid);
+  const float smax = load_hull_table(m, ht);  // (the workgroup's one barrier for one-wave chunks)
+  bool has = cid >= 0 && (int64_t)cid * 64 < n;
+  if (!has && parts == 1) return;  // wave-uniform; no barrier follows for one-wave chunks
+  if (lane == 0) t0_lds[wave] = __builtin_amdgcn_s_memrealtime();
+  const int part = __builtin_amdgcn_readfirstlane(wave % parts);
+  int64_t base = (int64_t)cid * 64;
+  const bool valid = has && base + lane < n;
+  const int64_t ii = valid ? base + lane : (has ? n - 1 : 0);
+  const T px = pts[3 * ii + 0], py = pts[3 * ii + 1], pz = pts[3 * ii + 2];
+  double* shb = parts > 1 ? shb_all + 64 * (wave / parts) : nullptr;
+  if (parts > 1) {
+    if (part == 0) ((volatile double*)shb)[lane] = __builtin_huge_val();
+    __syncthreads();
+  }
+  T best = tinf<T>(), gx = (T)0, gy = (T)0, gz = (T)0;
+  int bk = 0x7fffffff;
+  if (has) {
+    const uint64_t pm = parts == 4 ? (0x1111111111111111ull << part)
+                                   : (parts == 2 ? (0x5555555555555555ull << part) : ~0ull);
+    const F4* cws = out.chunk_ws ? (const F4*)out.chunk_ws + cid : nullptr;
+    scene_eval<T, 1, CULL, false, true, 0>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz,
+                                           cws, pm, shb);
+  }
+  if (parts > 1) {
+    // the chunk's waves' results meet in their stages; part 0 keeps the
+    // lexicographic (d, k) minimum per point (pass_kernel HPART's merge)
+    T* rs = stage;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    rs[4 * lane + 0] = best; rs[4 * lane + 1] = gx; rs[4 * lane + 2] = gy; rs[4 * lane + 3] = gz;
+    ((int*)(rs + 256))[lane] = bk;
+    __syncthreads();
+    if (part == 0) {
+      for (int w = 1; w < parts; ++w) {
+        const T* ro = (const T*)(stages + (wave + w) * m.stage_bytes);
+        const T d2 = ro[4 * lane];
+        const int k2 = ((const int*)(ro + 256))[lane];
+        if (d2 < best || (d2 == best && k2 < bk)) {
+          best = d2; bk = k2; gx = ro[4 * lane + 1]; gy = ro[4 * lane + 2]; gz = ro[4 * lane + 3];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (!has || part != 0) return;  // (no barrier follows)
+  slot_of(parts, cid);
+  base = (int64_t)cid * 64;
+  const int64_t i = base + lane;
+  if (!valid) bk = 0;
+  // this wave's wrench rows (lane k owns surface k) live in its free stage
+  double* acc_row = (double*)stage + lane * 6;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+  for (int j = 0; j < 6; ++j) acc_row[j] = 0.0;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  T* tstage = (T*)((char*)stage + (64 * 6 + 2) * 8);  // gradient transpose after the rows
+  double cost_chunk = 0.0;
+  const uint64_t touched = emit_chunk<T, 1, false>(px, py, pz, valid, best, bk, gx, gy, gz, i, base, n, m, out,
+                                                   acc_row, cost_chunk, nullptr, tstage,
+                                                   m.stage_bytes / (4 * (int)sizeof(T)));
+  cost_chunk = wave_sum(cost_chunk);
+  // the chunk's partial row: sparse entries in ascending k, or dense
+  const int cnt = __builtin_popcountll(touched);
+  if (cnt <= 4) {
+    if ((touched >> lane) & 1) {
+      const int sl = __builtin_popcountll(touched & ((1ull << lane) - 1));
+      double* e = co.ent + ((int64_t)cid * 4 + sl) * 6;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) e[j] = acc_row[j];
+    }
+    if (lane == 0) {
+      I4 h = I4{-1, -1, -1, -1};
+      uint64_t t = touched;
+      for (int sl = 0; sl < 4 && t; ++sl) {
+        h[sl] = __builtin_ctzll(t);
+        t &= t - 1;
+      }
+      ((I4*)co.hdr)[cid] = h;
+      co.csum[cid] = cost_chunk;
+    }
+  } else {
+    if (lane < m.S) {
+      double* r = co.dense + ((int64_t)cid * 64 + lane) * 6;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) r[j] = acc_row[j];
+    }
+    if (lane == 0) {
+      ((I4*)co.hdr)[cid] = I4{-2, -1, -1, -1};
+      co.csum[cid] = cost_chunk;
+    }
+  }
+  if (co.dur && lane == 0) {
+    // serial-equivalent duration: a split chunk's wall time scaled by the
+    // parallelism its split bought (measured ~2.5x at 4 waves, ~1.6x at 2)
+    const uint64_t dt = __builtin_amdgcn_s_memrealtime() - t0_lds[wave];
+    const uint64_t est = parts == 4 ? (dt * 5) / 2 : (parts == 2 ? (dt * 8) / 5 : dt);
+    co.dur[cid] = (uint32_t)(est < 0xffffffffull ? est : 0xffffffffull);
+  }
+}
+
+// Level 1 of the planned pass's reduction: one wave per kChunkGroup
+// consecutive chunks, lane k summing surface k's (F, M) over the group's
+// chunks in index order (entries in slot order); the group's 1 + 6S sums go
+// to the line-tile partials (column g) that reduce_tiles_kernel sums over the
+// groups in order. Deterministic and independent of the plan.
+__global__ __launch_bounds__(64) void reduce_chunks_kernel(const I4* __restrict__ hdr, const double* __restrict__ ent,
+                                                           const double* __restrict__ csum,
+                                                           const double* __restrict__ dense, int nc, int S,
+                                                           double* __restrict__ partials, int ngroups) {
+  const int g = blockIdx.x, lane = threadIdx.x;
+  double a[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  double cs = 0.0;
+  const int c0 = g * kChunkGroup, c1 = min(nc, c0 + kChunkGroup);
+  for (int c = c0; c < c1; ++c) {
+    const I4 h = hdr[c];
+    cs += csum[c];
+    if (h[0] == -2) {
+      if (lane < S) {
+        const double* r = dense + ((int64_t)c * 64 + lane) * 6;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) a[j] += r[j];
+      }
+    } else {
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) {
+        if (h[sl] < 0) break;
+        const double* e = ent + ((int64_t)c * 4 + sl) * 6;
+        double v[6];
+#pragma unroll
+        for (int j = 0; j < 6; ++j) v[j] = e[j];
+        if (lane == h[sl]) {
+#pragma unroll
+          for (int j = 0; j < 6; ++j) a[j] += v[j];
+        }
+      }
+    }
+  }
+  if (lane == 0) partials[pidx(0, g, ngroups)] = cs;
+  if (lane < S) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) partials[pidx(1 + 6 * lane + j, g, ngroups)] = a[j];
+  }
+}
+
+// The plan for the next passes (one workgroup, kPlanBlock threads): a counting
+// sort of the chunks' serial-equivalent durations into kPlanBuckets buckets,
+// heaviest first; the first n4 chunks of that order get a workgroup each (4
+// waves), the next n2 one per 2 waves (pairs of similar cost), the rest one
+// wave each in groups of 4 consecutive (similar cost: little idle inside a
+// workgroup). Workgroups are listed in that order — heaviest first, longest-
+// processing-time-first list scheduling. `order` is [nc] scratch.
+constexpr int kPlanBlock = 1024;
+constexpr int kPlanBuckets = 256;
+__global__ __launch_bounds__(kPlanBlock) void plan_kernel(const uint32_t* __restrict__ dur, int nc, int n4, int n2,
+                                                          int32_t* __restrict__ order, I4* __restrict__ plan) {
+  __shared__ unsigned hist[kPlanBuckets];
+  __shared__ unsigned wmax[kPlanBlock / 64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  unsigned mx = 0;
+  for (int c = t; c < nc; c += kPlanBlock) mx = max(mx, dur[c]);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, off, 64));
+  if (lane == 0) wmax[w] = mx;
+  for (int b = t; b < kPlanBuckets; b += kPlanBlock) hist[b] = 0;
+  __syncthreads();
+  mx = 0;
+  for (int j = 0; j < kPlanBlock / 64; ++j) mx = max(mx, wmax[j]);
+  const float sc = (float)(kPlanBuckets - 1) / (float)(mx ? mx : 1u);
+  auto bucket = [&](int c) { return kPlanBuckets - 1 - min(kPlanBuckets - 1, (int)((float)dur[c] * sc)); };
+  for (int c = t; c < nc; c += kPlanBlock) atomicAdd(&hist[bucket(c)], 1u);
+  __syncthreads();
+  if (t == 0) {  // exclusive scan (256 buckets, once per plan)
+    unsigned acc = 0;
+    for (int b = 0; b < kPlanBuckets; ++b) {
+      const unsigned h = hist[b];
+      hist[b] = acc;
+      acc += h;
+    }
+  }
+  __syncthreads();
+  for (int c = t; c < nc; c += kPlanBlock) order[atomicAdd(&hist[bucket(c)], 1u)] = c;
+  __threadfence();
+  __syncthreads();
+  const int n1 = nc - n4 - n2;
+  const int g2 = n2 / 2 + (n2 & 1), g1 = (n1 + 3) / 4;
+  for (int b = t; b < n4 + g2 + g1; b += kPlanBlock) {
+    I4 e = I4{-1, -1, -1, -1};
+    if (b < n4) {
+      e[0] = order[b] | (4 << kPlanPartsShift);
+    } else if (b < n4 + g2) {
+      const int p0 = n4 + 2 * (b - n4);
+      e[0] = order[p0] | (2 << kPlanPartsShift);
+      if (p0 + 1 < n4 + n2) e[1] = order[p0 + 1];
+    } else {
+      const int p0 = n4 + n2 + 4 * (b - n4 - g2);
+      e[0] = order[p0] | (1 << kPlanPartsShift);
+      for (int j = 1; j < 4; ++j)
+        if (p0 + j < nc) e[j] = order[p0 + j];
+    }
+    plan[b] = e;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2213,6 +2483,62 @@ hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d
     hipLaunchKernelGGL(reduce_tiles_kernel, dim3((len + 7) / 8), dim3(kTileBlock), 0, s, partials, nblocks, len,
                        d_accum);
   if (cost) hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kBlock), 0, s, cost, nblocks, order);
+  return hipGetLastError();
+}
+
+// the planned pass's LDS: the hull-partitioned layout + 4 chunk start times
+static size_t planned_lds_bytes(const LocalModel& lm) { return hpart_lds_bytes(lm, 1) + 4 * sizeof(uint64_t); }
+
+bool planned_pass(const LocalModel& lm, int64_t n) {
+  return FSDF_RED_IN_STAGE && lm.planes64 && lm.S <= 64 && lm.R == 0 && n > 0 && (n + 63) / 64 <= kMaxPlanChunks &&
+         planned_lds_bytes(lm) <= (size_t)kLdsPerCu / 4;
+}
+
+template <typename T>
+static void launch_planned_t(bool cull, const LocalModel& lm, const PosedModel& pm, const void* d_pts, int64_t n,
+                             int grid, const PassOutputs& out, const ChunkOutputs& co, hipStream_t s) {
+  const PassModel<T> m = pass_model<T>(lm, pm);
+  auto b = [](bool v) { return v ? "true" : "false"; };
+  snprintf(g_pass_name, sizeof g_pass_name, "planned_pass_kernel<%s, %s>", type_name<T>(), b(cull));
+  if (cull)
+    launch_lds(planned_pass_kernel<T, true>, grid, kPassBlock, planned_lds_bytes(lm), s, (const T*)d_pts, n, m, out,
+               co);
+  else
+    launch_lds(planned_pass_kernel<T, false>, grid, kPassBlock, planned_lds_bytes(lm), s, (const T*)d_pts, n, m, out,
+               co);
+}
+
+hipError_t launch_planned_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const void* d_pts,
+                               int64_t n, int grid, const PassOutputs& out, const ChunkOutputs& co, hipStream_t s,
+                               hipEvent_t ev_start, hipEvent_t ev_stop) {
+  struct ClearEvents {
+    ~ClearEvents() { g_pass_ev0 = g_pass_ev1 = nullptr; }
+  } clear_events;
+  g_pass_name[0] = 0;
+  if (precision != 64) return hipErrorNotSupported;  // (planes64: f64 contexts only)
+  g_pass_ev0 = ev_start;
+  g_pass_ev1 = ev_stop;
+  launch_planned_t<double>(cull, lm, pm, d_pts, n, grid, out, co, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce_chunks(const ChunkOutputs& co, int64_t nc, int S, double* partials, double* d_accum,
+                                hipStream_t s, hipEvent_t ev_stop) {
+  const int ngroups = (int)((nc + kChunkGroup - 1) / kChunkGroup);
+  hipLaunchKernelGGL(reduce_chunks_kernel, dim3(ngroups), dim3(64), 0, s, (const I4*)co.hdr, co.ent, co.csum,
+                     co.dense, (int)nc, S, partials, ngroups);
+  const int len = 1 + 6 * S;
+  if (ev_stop)
+    hipExtLaunchKernelGGL(reduce_tiles_kernel, dim3((len + 7) / 8), dim3(kTileBlock), 0u, s, nullptr, ev_stop, 0u,
+                          partials, ngroups, len, d_accum);
+  else
+    hipLaunchKernelGGL(reduce_tiles_kernel, dim3((len + 7) / 8), dim3(kTileBlock), 0, s, partials, ngroups, len,
+                       d_accum);
+  return hipGetLastError();
+}
+
+hipError_t launch_plan(const uint32_t* dur, int64_t nc, int n4, int n2, int32_t* order, int32_t* plan, hipStream_t s) {
+  hipLaunchKernelGGL(plan_kernel, dim3(1), dim3(kPlanBlock), 0, s, dur, (int)nc, n4, n2, order, (I4*)plan);
   return hipGetLastError();
 }
 

@@ -311,14 +311,17 @@ def test_resident_order_outputs(m64, oracle_mod, ctx_factory):
 
 @pytest.mark.parametrize("model", ["m64", "irb"])
 @pytest.mark.parametrize("tier", [4, 2])
-def test_hull_partitioned_pass_matches_one_wave_per_chunk(m64, irb, ctx_factory, model, tier):
+@pytest.mark.parametrize("planned", [False, True])
+def test_hull_partitioned_pass_matches_one_wave_per_chunk(m64, irb, ctx_factory, model, tier, planned):
     """Clouds up to the model's 4-way limit run the hull-partitioned pass with
-    4 waves per chunk, up to its 2-way limit with 2 (pass_kernel HPART: hull k
-    goes to wave k % parts, lexicographic (d, k) merge; limits per model,
-    fsdf_get_partition); one point more runs the next tier (2 waves per chunk,
-    then one wave per chunk). Per-point outputs do not depend on the block
-    structure: the shared points agree bit for bit, sums to rounding. The
-    same cloud with the tiers forced off (fsdf_set_partition) agrees too."""
+    4 waves per chunk, up to its 2-way limit with 2 (pass_kernel HPART, or the
+    planned pass's default shape: hull k goes to wave k % parts, lexicographic
+    (d, k) merge; limits per model, fsdf_get_partition); one point more runs
+    the next tier (2 waves per chunk, then one wave per chunk). Per-point
+    outputs do not depend on the block structure: the shared points agree bit
+    for bit, sums to rounding. The same cloud with the tiers forced off
+    (fsdf_set_partition) agrees too. planned: the product default
+    (fsdf_set_plan), whose first pass on a cloud runs the tier's shape."""
     from flash import synthetic
     import flash
     m = {"m64": m64, "irb": irb}[model]
@@ -336,18 +339,67 @@ def test_hull_partitioned_pass_matches_one_wave_per_chunk(m64, irb, ctx_factory,
     for cull in (True, False):
         for mm in (n, n + 1):
             ctx = ctx_factory(m, cull=cull)
+            ctx.set_plan(planned)
             ctx.set_points(pts[:mm])
             out[cull, mm] = ctx.eval(poses, per_point=True)
-            assert ctx.pass_kernel_name().endswith(f"true, true, 256, {tier}>") == (mm == n), ctx.pass_kernel_name()
+            name = ctx.pass_kernel_name()
+            if planned:
+                assert name.startswith("planned_pass_kernel<double"), name
+            else:
+                assert name.endswith(f"true, true, 256, {tier}>") == (mm == n), name
     forced = ctx_factory(m)
+    forced.set_plan(planned)
     forced.set_partition(0, 0)
     forced.set_points(pts[:n])
     _, _, (kf, df, gf) = forced.eval(poses, per_point=True)
-    assert forced.pass_kernel_name().endswith("true, false, 256, 4>")  # ALIAS, not HPART
+    if not planned:
+        assert forced.pass_kernel_name().endswith("true, false, 256, 4>")  # ALIAS, not HPART
     for cull in (True, False):
         (c1, a1, (k1, d1, g1)), (c0, a0, (k0, d0, g0)) = out[cull, n], out[cull, n + 1]
         assert np.array_equal(k1, k0[:n]) and np.array_equal(d1, d0[:n]) and np.array_equal(g1, g0[:n])
         assert np.array_equal(k1, kf) and np.array_equal(d1, df) and np.array_equal(g1, gf)
         assert c1 == pytest.approx(np.dot(d1, d1), rel=1e-10)
-    # culled and brute force share the partitioned block structure: identical sums
+    # culled and brute force share the partitioned block structure (planned:
+    # per-chunk rows summed in chunk order): identical sums
     assert np.array_equal(out[True, n][1], out[False, n][1])
+
+
+@pytest.mark.parametrize("sort_points", [True, False])
+def test_planned_pass_bits_independent_of_plan(m64, oracle_mod, ctx_factory, sort_points):
+    """The planned pass (fsdf_set_plan; per-chunk partial rows summed in chunk
+    order) gives the same bits whatever the plan: four plan compositions — all
+    chunks one wave, the default shares, a quarter split 4 ways and half 2 ways,
+    every chunk 4 ways — agree bit for bit in per-point outputs AND the
+    accumulator, on the first (default-shape) pass and on planned passes. Per
+    point they equal the unplanned grid's; sums to rounding, and the oracle.
+    Unsorted shuffled input puts > 4 nearest surfaces in most chunks (the dense
+    row path); sorted input mostly 1-2 (the sparse entries)."""
+    import flash
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(m64, 911)
+    pts = synthetic.depth_cloud(m64, qt, 262144 + 4321, seed=912, order="shuffled")
+    poses = flash.hull_poses(m64, qe)
+    res = []
+    for shares in ((0.0, 0.0), (1.0 / 32, 1.0 / 16), (0.25, 0.5), (1.0, 0.0)):
+        ctx = ctx_factory(m64, sort_points=sort_points)
+        ctx.set_plan(True, *shares)
+        ctx.set_points(pts)
+        runs = [ctx.eval(poses, per_point=True) for _ in range(3)]  # default shape, then planned
+        assert ctx.pass_kernel_name().startswith("planned_pass_kernel")
+        res.append(runs)
+    c0, a0, p0 = res[0][0]
+    for runs in res:
+        for c, a, pp in runs:
+            assert c == c0 and np.array_equal(a, a0)
+            for x, y in zip(pp, p0):
+                assert np.array_equal(x, y)
+    legacy = ctx_factory(m64, sort_points=sort_points)
+    legacy.set_plan(False)
+    legacy.set_points(pts)
+    cl, al, pl = legacy.eval(poses, per_point=True)
+    assert not legacy.pass_kernel_name().startswith("planned")
+    for x, y in zip(pl, p0):
+        assert np.array_equal(x, y)
+    assert np.allclose(al, a0, rtol=1e-11, atol=1e-12 * np.abs(a0).max())
+    om = oracle_mod.OracleModel.from_manipulator(m64)
+    _check_against(om.skin(poses, pts), p0[1], p0[0], p0[2], a0, om.cost_accum(poses, pts))

@@ -19,8 +19,8 @@
 #   sweep           bench.py at 2^16 .. 2^20 points           -> size_sweep.jsonl
 #   configs         tools/bench_configs.py (BASELINE configs C2-C5, M64)
 #   rehearse        bench.py N=2 on one GPU (gloo, both ranks on device 0)
-#   hsweep:MODEL:SIZES  hull-partition tiers against cloud size (tools/hpart_sweep.py; MODEL irb140 | arm_grid,
-#                   SIZES comma-separated)                    -> hpart_sweep_MODEL.jsonl
+#   hsweep:MODEL:SIZES[:EXTRA]  partition tiers / planned pass against cloud size (tools/hpart_sweep.py; MODEL
+#                   irb140 | arm_grid, SIZES and EXTRA arguments comma-separated) -> hpart_sweep_MODEL*.jsonl
 #   c5sweep         BASELINE C5 precision sweep on the reference cloud (tools/precision_sweep.py) -> c5_sweep.json
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -114,13 +114,15 @@ for step in "$@"; do
       cut -c1-600 $O/rehearse_n2.json
       unset FSDF_BENCH_BACKEND FSDF_BENCH_DEVICE ;;
     hsweep:*)
-      R=${step#hsweep:}; M=${R%%:*}; S=${R#*:}
-      timeout -k 10 600 python tools/hpart_sweep.py --model $M --sizes $S > $O/hpart_sweep_$M.jsonl 2> $O/hpart_sweep_$M.err \
-        || { echo HSWEEP FAILED; tail $O/hpart_sweep_$M.err; exit 1; }
+      # hsweep:MODEL:SIZES[:EXTRA] — EXTRA: more tools/hpart_sweep.py arguments, commas = spaces
+      R=${step#hsweep:}; M=${R%%:*}; R=${R#*:}; S=${R%%:*}; X=""; [ "$R" != "$S" ] && X=${R#*:}; X=${X//,/ }
+      N=$M$(echo "$X" | tr -c 'a-zA-Z0-9.' '_')
+      timeout -k 10 600 python tools/hpart_sweep.py --model $M --sizes $S $X >> $O/hpart_sweep_$N.jsonl \
+        2>> $O/hpart_sweep_$N.err || { echo HSWEEP FAILED; tail $O/hpart_sweep_$N.err; exit 1; }
       python3 -c "
 import json
-for l in open('$O/hpart_sweep_$M.jsonl'):
-    d = json.loads(l); print(d['points'], d['tier'], round(d['step_ms'], 4), round(d['pass_kernel_ms'], 4), d['default_parts'])" ;;
+for l in open('$O/hpart_sweep_$N.jsonl'):
+    d = json.loads(l); print(d['points'], d['tier'], d['shares'], round(d['step_ms'], 4), round(d['pass_kernel_ms'], 4), d['default_parts'])" ;;
     c5sweep)
       timeout -k 10 300 python tools/precision_sweep.py --json $O/c5_sweep.json > $O/c5_sweep.log 2>&1 \
         || { echo C5 SWEEP FAILED; tail $O/c5_sweep.log; exit 1; }

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Hull-partitioned pass tiers against cloud size, per model (run on the GPU box).
 
-For every size and every forced tier — 4 waves per chunk, 2, one wave per
-chunk (fsdf_set_partition) — the bench's step (pose + pass + reduce on the
+For every size and every mode — the unplanned grid (fsdf_set_plan off) at a
+forced tier (4 waves per chunk, 2, one wave per chunk; fsdf_set_partition) or
+at the model's default tier, and the planned pass (the product default) — the
+bench's step (pose + pass + reduce on the
 resident, Hilbert-sorted cloud, per-point outputs written; two alternating
 configurations) is timed, interleaved over rounds on one context, and the pass
 kernel's own HIP-event time recorded; then the model's default tier and what
@@ -21,7 +23,11 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "point-cloud-signed-distance_amd"))
 
-TIERS = {"4-way": (1 << 40, 0), "2-way": (0, 1 << 40), "one-wave": (0, 0), "default": (-1, -1)}
+# tier: (4-way limit, 2-way limit, planned pass) — the first three run the
+# unplanned grid (fsdf_set_plan off) at a forced tier; "planned" is the
+# product default (per-chunk plan from measured durations, fsdf_set_plan)
+TIERS = {"4-way": (1 << 40, 0, False), "2-way": (0, 1 << 40, False), "one-wave": (0, 0, False),
+         "unplanned": (-1, -1, False), "planned": (-1, -1, True)}
 
 
 def main():
@@ -31,6 +37,9 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--tiers", default="", help="comma-separated subset of " + ",".join(TIERS))
+    ap.add_argument("--four-share", type=float, default=1.0 / 32)
+    ap.add_argument("--two-share", type=float, default=1.0 / 16)
     a = ap.parse_args()
     import torch
     import flash
@@ -53,8 +62,11 @@ def main():
         outs = tuple(b.data_ptr() for b in bufs)
         best = {}
         for _ in range(a.rounds):
-            for tier, lim in TIERS.items():
-                ctx.set_partition(*lim)
+            for tier, (l4, l2, plan) in TIERS.items():
+                if a.tiers and tier not in a.tiers.split(","):
+                    continue
+                ctx.set_partition(l4, l2)
+                ctx.set_plan(plan, a.four_share, a.two_share)
                 for i in range(5):
                     ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs)
                 torch.cuda.synchronize()
@@ -71,9 +83,11 @@ def main():
                 row["pass_kernel_ms"] = min(row["pass_kernel_ms"], kms / launches)
                 row["kernel"] = ctx.pass_kernel_name()
         ctx.set_partition(-1, -1)
+        ctx.set_plan(True)
         lim4, lim2, parts = ctx.get_partition(n)
         for tier, row in best.items():
             print(json.dumps({"model": a.model, "hulls": ctx.K, "points": n, "tier": tier, **row,
+                              "shares": [a.four_share, a.two_share],
                               "default_limits": [lim4, lim2], "default_parts": parts}), flush=True)
         del d_pts, bufs
 

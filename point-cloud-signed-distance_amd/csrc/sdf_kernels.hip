@@ -1911,40 +1911,60 @@ __global__ __launch_bounds__(kPassBlock) __attribute__((amdgpu_waves_per_eu(kPas
   }
 }
 
-// Level 1 of the planned pass's reduction: one wave per kChunkGroup
-// consecutive chunks, lane k summing surface k's (F, M) over the group's
-// chunks in index order (entries in slot order); the group's 1 + 6S sums go
-// to the line-tile partials (column g) that reduce_tiles_kernel sums over the
-// groups in order. Deterministic and independent of the plan.
+// Level 1 of the planned pass's reduction: one wave per kChunkGroup (64)
+// consecutive chunks. Lane j loads chunk j's header, Σ d² and entries in one
+// go (no dependent memory latency in the loop); then, chunk by chunk in index
+// order, each entry (k, F, M) is broadcast from its lane (readlane) and lane
+// k adds it. The group's 1 + 6S sums go to the line-tile partials (column g)
+// that reduce_tiles_kernel sums over the groups in order. Deterministic and
+// independent of the plan. (A dense chunk's row is read by lane k directly.)
+__device__ __forceinline__ double readlane_d(double v, int c) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, c);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), c);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 __global__ __launch_bounds__(64) void reduce_chunks_kernel(const I4* __restrict__ hdr, const double* __restrict__ ent,
                                                            const double* __restrict__ csum,
                                                            const double* __restrict__ dense, int nc, int S,
                                                            double* __restrict__ partials, int ngroups) {
+  static_assert(kChunkGroup == 64, "one chunk per lane");
   const int g = blockIdx.x, lane = threadIdx.x;
+  const int c0 = g * kChunkGroup;
+  const int nchunks = min(kChunkGroup, nc - c0);
+  const bool mine = lane < nchunks;
+  const I4 h = mine ? hdr[c0 + lane] : I4{-1, -1, -1, -1};
+  const double cs_l = mine ? csum[c0 + lane] : 0.0;
+  double e[4][6];
+  const double* src = ent + (int64_t)(mine ? c0 + lane : 0) * 24;
+#pragma unroll
+  for (int sl = 0; sl < 4; ++sl)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) e[sl][j] = (mine && h[sl] >= 0) ? src[6 * sl + j] : 0.0;
   double a[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   double cs = 0.0;
-  const int c0 = g * kChunkGroup, c1 = min(nc, c0 + kChunkGroup);
-  for (int c = c0; c < c1; ++c) {
-    const I4 h = hdr[c];
-    cs += csum[c];
-    if (h[0] == -2) {
+  for (int c = 0; c < nchunks; ++c) {
+    cs += readlane_d(cs_l, c);
+    const int h0 = __builtin_amdgcn_readlane(h[0], c);
+    if (h0 == -2) {
       if (lane < S) {
-        const double* r = dense + ((int64_t)c * 64 + lane) * 6;
+        const double* r = dense + ((int64_t)(c0 + c) * 64 + lane) * 6;
 #pragma unroll
         for (int j = 0; j < 6; ++j) a[j] += r[j];
       }
-    } else {
+      continue;
+    }
 #pragma unroll
-      for (int sl = 0; sl < 4; ++sl) {
-        if (h[sl] < 0) break;
-        const double* e = ent + ((int64_t)c * 4 + sl) * 6;
-        double v[6];
+    for (int sl = 0; sl < 4; ++sl) {
+      const int k = __builtin_amdgcn_readlane(h[sl], c);
+      if (k < 0) break;
+      double v[6];
 #pragma unroll
-        for (int j = 0; j < 6; ++j) v[j] = e[j];
-        if (lane == h[sl]) {
+      for (int j = 0; j < 6; ++j) v[j] = readlane_d(e[sl][j], c);
+      if (lane == k) {
 #pragma unroll
-          for (int j = 0; j < 6; ++j) a[j] += v[j];
-        }
+        for (int j = 0; j < 6; ++j) a[j] += v[j];
       }
     }
   }

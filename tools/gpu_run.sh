@@ -6,6 +6,9 @@
 #
 # Steps (outputs under gpurun_out/TAG/):
 #   tests           pytest -m gpu (one process)
+#   pytest:FILES    pytest of the given test files only (commas between files)  -> pytest.log
+#   ktrace:ARGS     rocprofv3 --kernel-trace --stats of bench.py ARGS (commas = spaces) -> ktrace_N/ + summary
+#   smoke           __graft_entry__.smoke() (no build: the in-tree .so files travel)  -> smoke.log
 #   bench           bench.py default line            -> bench_default.json
 #   bench:ARGS      bench.py with ARGS (commas = spaces), e.g. bench:--points,131072
 #   prof            tools/rocprof_round.sh (kernel trace + PMC passes)
@@ -34,6 +37,26 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
         > $O/gpu_tests.log 2>&1 || { echo TESTS FAILED; tail -40 $O/gpu_tests.log; exit 1; }
       tail -1 $O/gpu_tests.log ;;
+    pytest:*)
+      F=${step#pytest:}; F=${F//,/ }
+      timeout -k 10 600 python -u -m pytest $F -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 \
+        || { echo PYTEST FAILED; tail -40 $O/pytest.log; exit 1; }
+      tail -3 $O/pytest.log ;;
+    ktrace:*)
+      A=${step#ktrace:}; A=${A//,/ }; N=$(echo "$A" | tr -c 'a-zA-Z0-9' '_')
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d $GRAFT_REPO_ROOT/$O/ktrace_$N -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 3 \
+          --no-cpu-baseline --no-full-iteration $A > $GRAFT_REPO_ROOT/$O/ktrace_$N.log 2>&1 ) \
+        || { echo KTRACE FAILED; tail $O/ktrace_$N.log; exit 1; }
+      python3 -c "
+import csv, glob
+f = glob.glob('$O/ktrace_$N/**/run_kernel_stats.csv', recursive=True)[0]
+for r in csv.DictReader(open(f)):
+    print('$N', r['Name'][:70], r['Calls'], round(float(r['AverageNs']) / 1e3, 2), 'us')" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g._paths(); g.smoke()" > $O/smoke.log 2>&1 \
+        || { echo SMOKE FAILED; tail $O/smoke.log; exit 1; }
+      tail -2 $O/smoke.log ;;
     bench)
       timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_default.json 2> $O/bench_default.err \
         || { echo BENCH FAILED; tail $O/bench_default.err; exit 1; }

@@ -44,6 +44,12 @@ void dfree(P*& p) {
 
 }  // namespace
 
+// the planned pass's default size limit (fsdf_set_plan max_points)
+#ifndef FSDF_PLAN_MAX_POINTS
+#define FSDF_PLAN_MAX_POINTS 524288
+#endif
+static constexpr int64_t kPlanMaxPointsDefault = FSDF_PLAN_MAX_POINTS;
+
 struct fsdf_ctx {
   int device = 0;
   int precision = 64;
@@ -128,6 +134,7 @@ struct fsdf_ctx {
   int plan_enable = 1;
   double plan_f4 = 1.0 / 32, plan_f2 = 1.0 / 16;  // shares of the chunks split over 4 / 2 waves
   int wave_slots = 0;                // device wave slots at the pass's occupancy (0: not queried yet)
+  int64_t plan_max_points = kPlanMaxPointsDefault;  // planned pass up to this cloud size (per device)
   double* d_accum = nullptr;
   int32_t* d_kstar = nullptr;
   double* d_d = nullptr;
@@ -938,7 +945,8 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
   out.perm = d_perm;
   out.stats = c->stats_on ? c->d_stats : nullptr;
   out.chunk_ws = FSDF_CHUNK_WS && d_pts == c->d_pts && n == c->n ? c->d_chunk_ws : nullptr;  // resident cloud only
-  if (schedule && n > 0 && c->plan_enable && c->precision == 64 && fsdf::planned_pass(c->lm, n)) {
+  if (schedule && n > 0 && c->plan_enable && n <= c->plan_max_points && c->precision == 64 &&
+      fsdf::planned_pass(c->lm, n)) {
     const bool prof = c->profiling && c->prof_used + 3 <= c->prof_ev.size();
     hipEvent_t* pe = prof ? &c->prof_ev[c->prof_used] : nullptr;
     rc = run_planned(c, *P, d_pts, n, d_accum, out, pe);
@@ -1012,13 +1020,16 @@ extern "C" int fsdf_get_partition(fsdf_ctx* c, int64_t n, int64_t* four_way_max_
 
 extern "C" const char* fsdf_pass_kernel_name(const fsdf_ctx* c) { return c ? c->pass_kernel.c_str() : ""; }
 
-extern "C" int fsdf_set_plan(fsdf_ctx* c, int32_t enable, double four_way_share, double two_way_share) {
+extern "C" int fsdf_set_plan(fsdf_ctx* c, int32_t enable, double four_way_share, double two_way_share,
+                             int64_t max_points) {
   if (!c) return FSDF_ERR_ARG;
   if (!(four_way_share >= 0.0 && four_way_share <= 1.0 && two_way_share >= 0.0 && two_way_share <= 1.0))
     return fail(c, FSDF_ERR_ARG, "set_plan: shares must lie in [0, 1]");
+  if (max_points < -1) return fail(c, FSDF_ERR_ARG, "set_plan: max_points is -1 (default) or a point count");
   c->plan_enable = enable != 0;
   c->plan_f4 = four_way_share;
   c->plan_f2 = two_way_share;
+  c->plan_max_points = max_points < 0 ? kPlanMaxPointsDefault : max_points;
   c->plan_nc = -1;  // rebuilt on the next pass
   return FSDF_OK;
 }

@@ -78,7 +78,7 @@ _PROTOS = {
     "fsdf_kernel_stats": (c_int32, [c_void_p, c_int32, c_void_p]),
     "fsdf_pass_kernel_name": (ctypes.c_char_p, [c_void_p]),
     "fsdf_set_partition": (c_int32, [c_void_p, c_int64, c_int64]),
-    "fsdf_set_plan": (c_int32, [c_void_p, c_int32, c_double, c_double]),
+    "fsdf_set_plan": (c_int32, [c_void_p, c_int32, c_double, c_double, c_int64]),
     "fsdf_get_partition": (c_int32, [c_void_p, c_int64, POINTER(c_int64), POINTER(c_int64), POINTER(c_int32)]),
     "fsdf_tree_transforms": (c_int32, [c_int32] + [c_void_p] * 13),
     "fsdf_config_gradient": (c_int32, [c_int32] + [c_void_p] * 7 + [c_int32] + [c_void_p] * 5),
@@ -323,11 +323,12 @@ class Context:
         check(self._lib.fsdf_set_partition(self._ctx, int(four_way_max_points), int(two_way_max_points)), self._ctx,
               "set_partition")
 
-    def set_plan(self, enable: bool = True, four_way_share: float = 1.0 / 32, two_way_share: float = 1.0 / 16):
-        """Planned pass of resident clouds (fsdf_set_plan): enable, and the
-        shares of chunks split over 4 / 2 waves."""
-        check(self._lib.fsdf_set_plan(self._ctx, int(enable), float(four_way_share), float(two_way_share)),
-              self._ctx, "set_plan")
+    def set_plan(self, enable: bool = True, four_way_share: float = 1.0 / 32, two_way_share: float = 1.0 / 16,
+                 max_points: int = -1):
+        """Planned pass of resident clouds (fsdf_set_plan): enable, the shares
+        of chunks split over 4 / 2 waves, the largest cloud it runs (-1: default)."""
+        check(self._lib.fsdf_set_plan(self._ctx, int(enable), float(four_way_share), float(two_way_share),
+                                      int(max_points)), self._ctx, "set_plan")
 
     def get_partition(self, n: int = 0):
         """(4-way limit, 2-way limit, waves per chunk a pass over n points runs)."""

@@ -382,7 +382,7 @@ def test_planned_pass_bits_independent_of_plan(m64, oracle_mod, ctx_factory, sor
     res = []
     for shares in ((0.0, 0.0), (1.0 / 32, 1.0 / 16), (0.25, 0.5), (1.0, 0.0)):
         ctx = ctx_factory(m64, sort_points=sort_points)
-        ctx.set_plan(True, *shares)
+        ctx.set_plan(True, *shares, 1 << 30)
         ctx.set_points(pts)
         runs = [ctx.eval(poses, per_point=True) for _ in range(3)]  # default shape, then planned
         assert ctx.pass_kernel_name().startswith("planned_pass_kernel")

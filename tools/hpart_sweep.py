@@ -63,10 +63,10 @@ def main():
         best = {}
         for _ in range(a.rounds):
             for tier, (l4, l2, plan) in TIERS.items():
-                if a.tiers and tier not in a.tiers.split(","):
+                if a.tiers and tier not in a.tiers.replace("+", ",").split(","):
                     continue
                 ctx.set_partition(l4, l2)
-                ctx.set_plan(plan, a.four_share, a.two_share)
+                ctx.set_plan(plan, a.four_share, a.two_share, 1 << 30)
                 for i in range(5):
                     ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs)
                 torch.cuda.synchronize()

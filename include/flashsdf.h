@@ -344,6 +344,12 @@ int fsdf_get_partition(fsdf_ctx* ctx, int64_t n, int64_t* four_way_max_out, int6
  * unplanned grid measured faster). */
 int fsdf_set_plan(fsdf_ctx* ctx, int32_t enable, double four_way_share, double two_way_share, int64_t max_points);
 
+/* Diagnostics: the serial-equivalent durations (100 MHz ticks) the last
+ * planned pass measured per 64-point chunk of the resident cloud (resident
+ * order), as the plan is built from them. *count_out = the chunk count (0
+ * before a planned pass); costs_out may be NULL to query it. */
+int fsdf_chunk_costs(fsdf_ctx* ctx, uint32_t* costs_out, int64_t* count_out);
+
 /* Kernel work counters (diagnostics). enable=1 zeroes and starts counting in
  * every following pass; enable=0 stops and writes the counters:
  *   [0] wave-iterations (64 points each)  [1] hull evaluations (per wave)

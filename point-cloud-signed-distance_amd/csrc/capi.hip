@@ -1020,6 +1020,16 @@ extern "C" int fsdf_get_partition(fsdf_ctx* c, int64_t n, int64_t* four_way_max_
 
 extern "C" const char* fsdf_pass_kernel_name(const fsdf_ctx* c) { return c ? c->pass_kernel.c_str() : ""; }
 
+extern "C" int fsdf_chunk_costs(fsdf_ctx* c, uint32_t* costs_out, int64_t* count_out) {
+  if (!c || !count_out) return FSDF_ERR_ARG;
+  const int64_t nc = c->plan_nc > 0 ? c->plan_nc : 0;
+  *count_out = nc;
+  if (!costs_out || nc == 0) return FSDF_OK;
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  HIPCHECK(c, hipMemcpy(costs_out, c->co.dur, (size_t)nc * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return FSDF_OK;
+}
+
 extern "C" int fsdf_set_plan(fsdf_ctx* c, int32_t enable, double four_way_share, double two_way_share,
                              int64_t max_points) {
   if (!c) return FSDF_ERR_ARG;

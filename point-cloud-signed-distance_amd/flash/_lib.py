@@ -79,6 +79,7 @@ _PROTOS = {
     "fsdf_pass_kernel_name": (ctypes.c_char_p, [c_void_p]),
     "fsdf_set_partition": (c_int32, [c_void_p, c_int64, c_int64]),
     "fsdf_set_plan": (c_int32, [c_void_p, c_int32, c_double, c_double, c_int64]),
+    "fsdf_chunk_costs": (c_int32, [c_void_p, c_void_p, POINTER(c_int64)]),
     "fsdf_get_partition": (c_int32, [c_void_p, c_int64, POINTER(c_int64), POINTER(c_int64), POINTER(c_int32)]),
     "fsdf_tree_transforms": (c_int32, [c_int32] + [c_void_p] * 13),
     "fsdf_config_gradient": (c_int32, [c_int32] + [c_void_p] * 7 + [c_int32] + [c_void_p] * 5),
@@ -329,6 +330,15 @@ class Context:
         of chunks split over 4 / 2 waves, the largest cloud it runs (-1: default)."""
         check(self._lib.fsdf_set_plan(self._ctx, int(enable), float(four_way_share), float(two_way_share),
                                       int(max_points)), self._ctx, "set_plan")
+
+    def chunk_costs(self) -> np.ndarray:
+        """Per-chunk serial-equivalent durations (100 MHz ticks) of the last planned pass."""
+        cnt = c_int64(0)
+        check(self._lib.fsdf_chunk_costs(self._ctx, None, ctypes.byref(cnt)), self._ctx, "chunk_costs")
+        out = np.empty(cnt.value, np.uint32)
+        if cnt.value:
+            check(self._lib.fsdf_chunk_costs(self._ctx, out.ctypes.data, ctypes.byref(cnt)), self._ctx, "chunk_costs")
+        return out
 
     def get_partition(self, n: int = 0):
         """(4-way limit, 2-way limit, waves per chunk a pass over n points runs)."""

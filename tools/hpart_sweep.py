@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--tiers", default="", help="comma-separated subset of " + ",".join(TIERS))
     ap.add_argument("--four-share", type=float, default=1.0 / 32)
     ap.add_argument("--two-share", type=float, default=1.0 / 16)
+    ap.add_argument("--dump-costs", default="", help="npz path: the planned pass's per-chunk durations per size")
     a = ap.parse_args()
     import torch
     import flash
@@ -53,6 +54,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
     accum = torch.zeros(ctx.accum_len, dtype=torch.float64, device=dev)
+    dumps = {}
     for n in (int(s) for s in a.sizes.split(",")):
         pts = synthetic.depth_cloud(m, qt, n, seed=a.seed + 17, order="shuffled")
         d_pts = torch.as_tensor(pts, device=dev)
@@ -82,6 +84,12 @@ def main():
                 row["step_ms"] = min(row["step_ms"], step)
                 row["pass_kernel_ms"] = min(row["pass_kernel_ms"], kms / launches)
                 row["kernel"] = ctx.pass_kernel_name()
+        if a.dump_costs:
+            ctx.set_partition(-1, -1)
+            ctx.set_plan(True, 0.0, 0.0, 1 << 30)  # one wave per chunk: raw durations
+            for i in range(3):
+                ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs)
+            dumps[f"n{n}"] = ctx.chunk_costs()
         ctx.set_partition(-1, -1)
         ctx.set_plan(True)
         lim4, lim2, parts = ctx.get_partition(n)
@@ -90,6 +98,8 @@ def main():
                               "shares": [a.four_share, a.two_share],
                               "default_limits": [lim4, lim2], "default_parts": parts}), flush=True)
         del d_pts, bufs
+    if a.dump_costs:
+        np.savez_compressed(a.dump_costs, **dumps)
 
 
 if __name__ == "__main__":

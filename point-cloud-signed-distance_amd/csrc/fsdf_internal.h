@@ -151,7 +151,7 @@ struct ChunkOutputs {
   int dparts = 1;              // waves per chunk without a plan (4, 2 or 1)
 };
 constexpr int kPlanPartsShift = 24;
-constexpr int kChunkGroup = 64;          // chunks per level-1 reduce wave (one per lane)
+constexpr int kChunkGroup = 16;          // chunks per level-1 reduce wave (one per lane)
 constexpr int64_t kMaxPlanChunks = 1 << 16;  // planned passes: clouds of <= 4,194,304 points per device
 
 // a resident pass over n points of this model can run planned

@@ -1925,23 +1925,38 @@ __device__ __forceinline__ double readlane_d(double v, int c) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
-// Adds the chunks [c0, c0 + 64) ∩ [0, nc) into (a, cs) in index order (one
-// wave; lane k owns surface k). Lane j loads chunk j's row up front.
-__device__ __forceinline__ void sum_chunk_group(const I4* __restrict__ hdr, const double* __restrict__ ent,
-                                                const double* __restrict__ csum, const double* __restrict__ dense,
-                                                int nc, int S, int c0, double (&a)[6], double& cs) {
-  static_assert(kChunkGroup == 64, "one chunk per lane");
-  const int lane = threadIdx.x & 63;
-  const int nchunks = min(kChunkGroup, nc - c0);
+// Level 1 of the planned pass's reduction: one wave per group of
+// kChunkGroup (16) consecutive chunks. Lanes 0..15 load their chunk's header,
+// Σ d² and entries at once (one memory latency per group, no dependent loads
+// in the loop); then, chunk by chunk in index order, each entry is broadcast
+// by v_readlane and lane k adds it (a dense chunk's row is read by lane k
+// directly: > 4 surfaces in one chunk, ~4 % of a sorted cloud's chunks). The
+// group's 1 + 6S sums go to the line-tile partials, column g, which
+// reduce_tiles_kernel sums over the groups in order: deterministic and
+// independent of the plan.
+__global__ __launch_bounds__(64) void reduce_chunks_kernel(const I4* __restrict__ hdr, const double* __restrict__ ent,
+                                                           const double* __restrict__ csum,
+                                                           const double* __restrict__ dense, int nc, int S,
+                                                           double* __restrict__ partials, int ngroups) {
+  static_assert(kChunkGroup <= 64, "one chunk per lane");
+  const int g = blockIdx.x, lane = threadIdx.x;
+  const int c0 = g * kChunkGroup;
+  const int nchunks = min(kChunkGroup, nc - c0);  // (uniform: g and nc are)
   const bool mine = lane < nchunks;
-  const I4 h = mine ? hdr[c0 + lane] : I4{-1, -1, -1, -1};
-  const double cs_l = mine ? csum[c0 + lane] : 0.0;
+  const int cl = mine ? c0 + lane : c0;
+  const I4 hv = hdr[cl];
+  const I4 h = mine ? hv : I4{-1, -1, -1, -1};
+  const double cs_l = mine ? csum[cl] : 0.0;
+  // all 24 entry values, loaded unconditionally (unused slots hold stale
+  // values that are never added): no per-slot branches around the loads
   double e[4][6];
-  const double* src = ent + (int64_t)(mine ? c0 + lane : 0) * 24;
+  const double* src = ent + (int64_t)cl * 24;
 #pragma unroll
   for (int sl = 0; sl < 4; ++sl)
 #pragma unroll
-    for (int j = 0; j < 6; ++j) e[sl][j] = (mine && h[sl] >= 0) ? src[6 * sl + j] : 0.0;
+    for (int j = 0; j < 6; ++j) e[sl][j] = src[6 * sl + j];
+  double a[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  double cs = 0.0;
   for (int c = 0; c < nchunks; ++c) {
     cs += readlane_d(cs_l, c);
     const int h0 = __builtin_amdgcn_readlane(h[0], c);
@@ -1966,50 +1981,10 @@ __device__ __forceinline__ void sum_chunk_group(const I4* __restrict__ hdr, cons
       }
     }
   }
-}
-
-// Level 1 (large clouds): one wave per group of 64 chunks -> line-tile
-// partials column g (reduce_tiles_kernel sums the groups in order).
-__global__ __launch_bounds__(64) void reduce_chunks_kernel(const I4* __restrict__ hdr, const double* __restrict__ ent,
-                                                           const double* __restrict__ csum,
-                                                           const double* __restrict__ dense, int nc, int S,
-                                                           double* __restrict__ partials, int ngroups) {
-  const int g = blockIdx.x, lane = threadIdx.x;
-  double a[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  double cs = 0.0;
-  sum_chunk_group(hdr, ent, csum, dense, nc, S, g * kChunkGroup, a, cs);
   if (lane == 0) partials[pidx(0, g, ngroups)] = cs;
   if (lane < S) {
 #pragma unroll
     for (int j = 0; j < 6; ++j) partials[pidx(1 + 6 * lane + j, g, ngroups)] = a[j];
-  }
-}
-
-// Small clouds (<= kChunkSingleMax chunks): the whole reduction in one
-// workgroup — wave w sums the groups w, w + 16, ... in order, then the 16
-// wave rows are added in wave order into accum. One launch instead of two
-// (the strong-scaling shards' step is short enough for a launch to matter).
-constexpr int kChunkSingleWaves = 16;
-constexpr int64_t kChunkSingleMax = 4096;  // chunks (2^18 points): one wave walks <= 4 groups
-__global__ __launch_bounds__(64 * kChunkSingleWaves) void reduce_chunks_single_kernel(
-    const I4* __restrict__ hdr, const double* __restrict__ ent, const double* __restrict__ csum,
-    const double* __restrict__ dense, int nc, int S, double* __restrict__ accum) {
-  __shared__ double rows[kChunkSingleWaves][1 + 6 * 64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  double a[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  double cs = 0.0;
-  for (int c0 = w * kChunkGroup; c0 < nc; c0 += kChunkSingleWaves * kChunkGroup)
-    sum_chunk_group(hdr, ent, csum, dense, nc, S, c0, a, cs);
-  if (lane == 0) rows[w][0] = cs;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) rows[w][1 + 6 * lane + j] = a[j];
-  __syncthreads();
-  const int len = 1 + 6 * S;
-  for (int t = threadIdx.x; t < len; t += 64 * kChunkSingleWaves) {
-    double v = rows[0][t];
-#pragma unroll
-    for (int ww = 1; ww < kChunkSingleWaves; ++ww) v += rows[ww][t];
-    accum[t] = v;
   }
 }
 
@@ -2582,15 +2557,6 @@ hipError_t launch_planned_pass(int precision, bool cull, const LocalModel& lm, c
 
 hipError_t launch_reduce_chunks(const ChunkOutputs& co, int64_t nc, int S, double* partials, double* d_accum,
                                 hipStream_t s, hipEvent_t ev_stop) {
-  if (nc <= kChunkSingleMax) {
-    if (ev_stop)
-      hipExtLaunchKernelGGL(reduce_chunks_single_kernel, dim3(1), dim3(64 * kChunkSingleWaves), 0u, s, nullptr,
-                            ev_stop, 0u, (const I4*)co.hdr, co.ent, co.csum, co.dense, (int)nc, S, d_accum);
-    else
-      hipLaunchKernelGGL(reduce_chunks_single_kernel, dim3(1), dim3(64 * kChunkSingleWaves), 0, s, (const I4*)co.hdr,
-                         co.ent, co.csum, co.dense, (int)nc, S, d_accum);
-    return hipGetLastError();
-  }
   const int ngroups = (int)((nc + kChunkGroup - 1) / kChunkGroup);
   hipLaunchKernelGGL(reduce_chunks_kernel, dim3(ngroups), dim3(64), 0, s, (const I4*)co.hdr, co.ent, co.csum,
                      co.dense, (int)nc, S, partials, ngroups);

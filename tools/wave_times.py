@@ -34,6 +34,7 @@ def main():
     poses = flash.hull_poses(m, qe)
     pts = synthetic.depth_cloud(m, qt, args.points, seed=1234 + 17, order=args.order)
     c = _lib.Context(device=0, precision=64, cull=True, sort_points=True)
+    c.set_plan(False)  # the per-wave timeline is written by the block-structured pass only
     c.set_model([(s.hull.vertices, s.hull.faces, s.hull.planes) for s in m.surfaces])
     c.set_points(pts)
     for _ in range(3):

@@ -890,9 +890,6 @@ static int run_planned(fsdf_ctx* c, const fsdf::PosedModel& P, const void* d_pts
   const int64_t nc = (n + 63) / 64;
   int rc = ensure_chunk_outputs(c, nc);
   if (rc) return rc;
-  rc = ensure_partials(c, (int)((nc + fsdf::kChunkGroup - 1) / fsdf::kChunkGroup));
-  if (rc) return rc;
-  out.partials = c->d_partials;
   out.cost = nullptr;
   out.order = nullptr;
   fsdf::ChunkOutputs co = c->co;

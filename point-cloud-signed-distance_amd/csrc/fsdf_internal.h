@@ -151,7 +151,6 @@ struct ChunkOutputs {
   int dparts = 1;              // waves per chunk without a plan (4, 2 or 1)
 };
 constexpr int kPlanPartsShift = 24;
-constexpr int kChunkGroup = 16;          // chunks per level-1 reduce wave (one per lane)
 constexpr int64_t kMaxPlanChunks = 1 << 16;  // planned passes: clouds of <= 4,194,304 points per device
 
 // a resident pass over n points of this model can run planned
@@ -159,8 +158,8 @@ bool planned_pass(const LocalModel& lm, int64_t n);
 hipError_t launch_planned_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const void* d_pts,
                                int64_t n, int grid, const PassOutputs& out, const ChunkOutputs& co, hipStream_t s,
                                hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
-// level 1 (per group of kChunkGroup chunks into `partials` line tiles) + level 2
-// (reduce_tiles over the groups) -> d_accum [1 + 6S]
+// the accumulator d_accum [1 + 6S] from the chunk rows, in chunk order (one
+// launch; `partials` unused)
 hipError_t launch_reduce_chunks(const ChunkOutputs& co, int64_t nc, int S, double* partials, double* d_accum,
                                 hipStream_t s, hipEvent_t ev_stop = nullptr);
 // the plan of the next passes from the chunk durations of this one

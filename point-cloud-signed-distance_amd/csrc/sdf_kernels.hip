@@ -1776,9 +1776,9 @@ __global__ __launch_bounds__(NB) __attribute__((
 // Every chunk writes its OWN partial row — the chunk's Σ d², and its wrench
 // sums (F, M) per nearest surface as up to 4 (k, F, M) entries, or a dense
 // [64][6] row when more than 4 surfaces meet in the chunk — so the
-// accumulator (reduce_chunks_kernel over fixed groups of kChunkGroup chunks,
-// then reduce_tiles_kernel) sums the chunks in index order whatever the plan:
-// bit-identical across plans, schedules and passes. No block combine, no
+// accumulator (reduce_chunks_kernel, one launch) sums the chunk rows in a
+// fixed order whatever the plan: bit-identical across plans, schedules and
+// passes. No block combine, no
 // barrier after the prologue for one-wave chunks.
 // ---------------------------------------------------------------------------
 constexpr int kPlanChunkMask = (1 << kPlanPartsShift) - 1;
@@ -1911,80 +1911,76 @@ __global__ __launch_bounds__(kPassBlock) __attribute__((amdgpu_waves_per_eu(kPas
   }
 }
 
-// Level 1 of the planned pass's reduction: one wave per kChunkGroup (64)
-// consecutive chunks. Lane j loads chunk j's header, Σ d² and entries in one
-// go (no dependent memory latency in the loop); then, chunk by chunk in index
-// order, each entry (k, F, M) is broadcast from its lane (readlane) and lane
-// k adds it. The group's 1 + 6S sums go to the line-tile partials (column g)
-// that reduce_tiles_kernel sums over the groups in order. Deterministic and
-// independent of the plan. (A dense chunk's row is read by lane k directly.)
-__device__ __forceinline__ double readlane_d(double v, int c) {
-  const uint64_t u = (uint64_t)__double_as_longlong(v);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, c);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), c);
-  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
-// Level 1 of the planned pass's reduction: one wave per group of
-// kChunkGroup (16) consecutive chunks. Lanes 0..15 load their chunk's header,
-// Σ d² and entries at once (one memory latency per group, no dependent loads
-// in the loop); then, chunk by chunk in index order, each entry is broadcast
-// by v_readlane and lane k adds it (a dense chunk's row is read by lane k
-// directly: > 4 surfaces in one chunk, ~4 % of a sorted cloud's chunks). The
-// group's 1 + 6S sums go to the line-tile partials, column g, which
-// reduce_tiles_kernel sums over the groups in order: deterministic and
-// independent of the plan.
-__global__ __launch_bounds__(64) void reduce_chunks_kernel(const I4* __restrict__ hdr, const double* __restrict__ ent,
-                                                           const double* __restrict__ csum,
-                                                           const double* __restrict__ dense, int nc, int S,
-                                                           double* __restrict__ partials, int ngroups) {
-  static_assert(kChunkGroup <= 64, "one chunk per lane");
-  const int g = blockIdx.x, lane = threadIdx.x;
-  const int c0 = g * kChunkGroup;
-  const int nchunks = min(kChunkGroup, nc - c0);  // (uniform: g and nc are)
-  const bool mine = lane < nchunks;
-  const int cl = mine ? c0 + lane : c0;
-  const I4 hv = hdr[cl];
-  const I4 h = mine ? hv : I4{-1, -1, -1, -1};
-  const double cs_l = mine ? csum[cl] : 0.0;
-  // all 24 entry values, loaded unconditionally (unused slots hold stale
-  // values that are never added): no per-slot branches around the loads
-  double e[4][6];
-  const double* src = ent + (int64_t)cl * 24;
+// The planned pass's reduction, one launch: workgroup x sums accumulator
+// entries 8x .. 8x+7 (entry 0 = Σ d², entry 1 + 6k + j = (F, M)_j of surface
+// k) over all chunks. Thread i takes chunks i, i + 1024, ... in order (headers
+// loaded kChunkBatch at a time, so several loads are in flight), adding the
+// entries of its tile from each chunk's sparse entries or dense row; then a
+// fixed-order DPP wave sum and a fixed-order 16-wave combine. Deterministic,
+// and it reads only the chunk rows: independent of the plan.
+constexpr int kChunkBatch = 8;
+constexpr int kChunkReduceBlock = 1024;
+__global__ __launch_bounds__(kChunkReduceBlock) void reduce_chunks_kernel(const I4* __restrict__ hdr,
+                                                                   const double* __restrict__ ent,
+                                                                   const double* __restrict__ csum,
+                                                                   const double* __restrict__ dense, int nc, int S,
+                                                                   double* __restrict__ accum) {
+  const int x = blockIdx.x;
+  const int len = 1 + 6 * S;
+  const int t0 = 8 * x;
+  // the tile's surfaces: entries 1 + 6k .. 6 + 6k
+  const int k_lo = t0 >= 1 ? (t0 - 1) / 6 : 0;
+  const int k_hi = min(S - 1, (t0 + 6) / 6);
+  double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int c0 = threadIdx.x; c0 < nc; c0 += kChunkBatch * kChunkReduceBlock) {
+    I4 h[kChunkBatch];
 #pragma unroll
-  for (int sl = 0; sl < 4; ++sl)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) e[sl][j] = src[6 * sl + j];
-  double a[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  double cs = 0.0;
-  for (int c = 0; c < nchunks; ++c) {
-    cs += readlane_d(cs_l, c);
-    const int h0 = __builtin_amdgcn_readlane(h[0], c);
-    if (h0 == -2) {
-      if (lane < S) {
-        const double* r = dense + ((int64_t)(c0 + c) * 64 + lane) * 6;
-#pragma unroll
-        for (int j = 0; j < 6; ++j) a[j] += r[j];
-      }
-      continue;
+    for (int u = 0; u < kChunkBatch; ++u) {
+      const int c = c0 + u * kChunkReduceBlock;
+      h[u] = c < nc ? hdr[c] : I4{-1, -1, -1, -1};
     }
 #pragma unroll
-    for (int sl = 0; sl < 4; ++sl) {
-      const int k = __builtin_amdgcn_readlane(h[sl], c);
-      if (k < 0) break;
-      double v[6];
+    for (int u = 0; u < kChunkBatch; ++u) {
+      const int c = c0 + u * kChunkReduceBlock;
+      if (c >= nc) break;
+      if (x == 0) acc[0] += csum[c];
+      if (h[u][0] == -2) {
+        for (int q = 0; q < 8; ++q) {
+          const int t = t0 + q;
+          if (t >= 1 && t < len) acc[q] += dense[((int64_t)c * 64 + (t - 1) / 6) * 6 + (t - 1) % 6];
+        }
+        continue;
+      }
 #pragma unroll
-      for (int j = 0; j < 6; ++j) v[j] = readlane_d(e[sl][j], c);
-      if (lane == k) {
+      for (int sl = 0; sl < 4; ++sl) {
+        const int k = h[u][sl];
+        if (k < 0) break;
+        if (k < k_lo || k > k_hi) continue;
+        const double* e = ent + ((int64_t)c * 4 + sl) * 6;
 #pragma unroll
-        for (int j = 0; j < 6; ++j) a[j] += v[j];
+        for (int q = 0; q < 8; ++q) {
+          const int j = t0 + q - 1 - 6 * k;  // entry t0+q as component j of surface k
+          if (j >= 0 && j < 6) acc[q] += e[j];
+        }
       }
     }
   }
-  if (lane == 0) partials[pidx(0, g, ngroups)] = cs;
-  if (lane < S) {
+  constexpr int W = kChunkReduceBlock / 64;
+  __shared__ double sh[8][W];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) partials[pidx(1 + 6 * lane + j, g, ngroups)] = a[j];
+  for (int q = 0; q < 8; ++q) {
+    const double w = wave_sum(acc[q]);
+    if (lane == 0) sh[q][wave] = w;
+  }
+  __syncthreads();
+  const int t = t0 + (int)threadIdx.x;
+  if (threadIdx.x < 8 && t < len) {
+    double a[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      a[g] = (sh[threadIdx.x][4 * g] + sh[threadIdx.x][4 * g + 1]) + (sh[threadIdx.x][4 * g + 2] + sh[threadIdx.x][4 * g + 3]);
+    accum[t] = (a[0] + a[1]) + (a[2] + a[3]);
   }
 }
 
@@ -2557,16 +2553,14 @@ hipError_t launch_planned_pass(int precision, bool cull, const LocalModel& lm, c
 
 hipError_t launch_reduce_chunks(const ChunkOutputs& co, int64_t nc, int S, double* partials, double* d_accum,
                                 hipStream_t s, hipEvent_t ev_stop) {
-  const int ngroups = (int)((nc + kChunkGroup - 1) / kChunkGroup);
-  hipLaunchKernelGGL(reduce_chunks_kernel, dim3(ngroups), dim3(64), 0, s, (const I4*)co.hdr, co.ent, co.csum,
-                     co.dense, (int)nc, S, partials, ngroups);
+  (void)partials;
   const int len = 1 + 6 * S;
   if (ev_stop)
-    hipExtLaunchKernelGGL(reduce_tiles_kernel, dim3((len + 7) / 8), dim3(kTileBlock), 0u, s, nullptr, ev_stop, 0u,
-                          partials, ngroups, len, d_accum);
+    hipExtLaunchKernelGGL(reduce_chunks_kernel, dim3((len + 7) / 8), dim3(kChunkReduceBlock), 0u, s, nullptr, ev_stop, 0u,
+                          (const I4*)co.hdr, co.ent, co.csum, co.dense, (int)nc, S, d_accum);
   else
-    hipLaunchKernelGGL(reduce_tiles_kernel, dim3((len + 7) / 8), dim3(kTileBlock), 0, s, partials, ngroups, len,
-                       d_accum);
+    hipLaunchKernelGGL(reduce_chunks_kernel, dim3((len + 7) / 8), dim3(kChunkReduceBlock), 0, s, (const I4*)co.hdr, co.ent,
+                       co.csum, co.dense, (int)nc, S, d_accum);
   return hipGetLastError();
 }
 

@@ -336,12 +336,13 @@ int fsdf_get_partition(fsdf_ctx* ctx, int64_t n, int64_t* four_way_max_out, int6
  * are split over 4 waves (hull-partitioned), the next `two_way_share` over 2,
  * the rest run one wave each grouped by similar cost, heaviest workgroups
  * first. enable = 0 runs the unplanned one-block-per-4-chunks grid instead
- * (A/B). Defaults: enabled, 1/32 and 1/16; at least as many chunks go 4 ways
- * as the device has idle wave slots for (a strong-scaling shard smaller than
- * the machine splits its heaviest third). A new cloud's first pass runs the
- * tier shape of fsdf_set_partition. max_points: the largest cloud (points per
- * device) the planned pass runs, -1 = the default (524,288: above it the
- * unplanned grid measured faster). */
+ * (A/B). Shares < 0 select the default: the heaviest 96 chunks over 4 waves
+ * and the next 192 over 2; at least as many chunks go 4 ways as the device has
+ * idle wave slots for (a strong-scaling shard smaller than the machine splits
+ * its heaviest third). A new cloud's first pass runs the tier shape of
+ * fsdf_set_partition. max_points: the largest cloud (points per device) the
+ * planned pass runs, -1 = the default (524,288: above it the unplanned grid
+ * measured faster). */
 int fsdf_set_plan(fsdf_ctx* ctx, int32_t enable, double four_way_share, double two_way_share, int64_t max_points);
 
 /* Diagnostics: the serial-equivalent durations (100 MHz ticks) the last

@@ -49,6 +49,8 @@ void dfree(P*& p) {
 #define FSDF_PLAN_MAX_POINTS 524288
 #endif
 static constexpr int64_t kPlanMaxPointsDefault = FSDF_PLAN_MAX_POINTS;
+// default plan composition: chunks split over 4 / 2 waves (fsdf_set_plan shares < 0)
+static constexpr int64_t kPlanDefault4 = 96, kPlanDefault2 = 192;
 
 struct fsdf_ctx {
   int device = 0;
@@ -132,7 +134,7 @@ struct fsdf_ctx {
   int64_t plan_nc = -1;              // chunks the plan was built for
   int plan_age = 0;                  // planned passes since the plan was rebuilt
   int plan_enable = 1;
-  double plan_f4 = 1.0 / 32, plan_f2 = 1.0 / 16;  // shares of the chunks split over 4 / 2 waves
+  double plan_f4 = -1.0, plan_f2 = -1.0;  // shares of the chunks split over 4 / 2 waves (< 0: default counts)
   int wave_slots = 0;                // device wave slots at the pass's occupancy (0: not queried yet)
   int64_t plan_max_points = kPlanMaxPointsDefault;  // planned pass up to this cloud size (per device)
   double* d_accum = nullptr;
@@ -294,9 +296,7 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   dfree(c->d_block_cost);
   dfree(c->d_block_order);
   dfree(c->co.hdr);
-  dfree(c->co.ent);
-  dfree(c->co.csum);
-  dfree(c->co.dense);
+  dfree(c->co.ent);  // (csum, dense: the same allocation)
   dfree(c->co.dur);
   dfree(c->d_plan);
   dfree(c->d_plan_order);
@@ -847,17 +847,18 @@ static int ensure_chunk_outputs(fsdf_ctx* c, int64_t nc) {
   if (c->co_cap >= nc) return FSDF_OK;
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   dfree(c->co.hdr);
-  dfree(c->co.ent);
-  dfree(c->co.csum);
-  dfree(c->co.dense);
+  dfree(c->co.ent);  // (csum and dense live in the same allocation)
   dfree(c->co.dur);
   dfree(c->d_plan_order);
+  c->co.csum = c->co.dense = nullptr;
   c->co_cap = 0;
   c->plan_nc = -1;
   HIPCHECK(c, hipMalloc(&c->co.hdr, (size_t)nc * 4 * sizeof(int32_t)));
-  HIPCHECK(c, hipMalloc(&c->co.ent, (size_t)nc * 24 * sizeof(double)));
-  HIPCHECK(c, hipMalloc(&c->co.csum, (size_t)nc * sizeof(double)));
-  HIPCHECK(c, hipMalloc(&c->co.dense, (size_t)nc * 64 * 6 * sizeof(double)));
+  // one allocation: entries [nc][24] | Σ d² [nc] | dense rows [nc][64][6] (reduce_chunks_kernel indexes it)
+  HIPCHECK(c, hipMalloc(&c->co.ent, (size_t)nc * (24 + 1 + 64 * 6) * sizeof(double)));
+  c->co.csum = c->co.ent + (size_t)nc * 24;
+  c->co.dense = c->co.ent + (size_t)nc * 25;
+  c->co.cap = nc;
   HIPCHECK(c, hipMalloc(&c->co.dur, (size_t)nc * sizeof(uint32_t)));
   HIPCHECK(c, hipMalloc(&c->d_plan_order, (size_t)nc * sizeof(int32_t)));
   c->co_cap = nc;
@@ -877,9 +878,13 @@ static void plan_shape(fsdf_ctx* c, int64_t nc, int* n4, int* n2) {
     c->wave_slots = cus * 4 * 4;  // 4 SIMDs x 4 waves (the pass's register budget)
   }
   const int64_t spare = std::max<int64_t>(0, (int64_t)c->wave_slots - nc);
-  const int64_t a = std::min<int64_t>(nc, std::max<int64_t>(llround(c->plan_f4 * (double)nc), spare / 3));
+  // default (shares < 0): fixed counts — the heavy tail that outlasts the rest
+  // of a pass is ~100 chunks at 2^18 and at 2^19 points alike (measured)
+  const int64_t want4 = c->plan_f4 < 0 ? kPlanDefault4 : llround(c->plan_f4 * (double)nc);
+  const int64_t want2 = c->plan_f2 < 0 ? kPlanDefault2 : llround(c->plan_f2 * (double)nc);
+  const int64_t a = std::min<int64_t>(nc, std::max<int64_t>(want4, spare / 3));
   *n4 = (int)a;
-  *n2 = (int)std::min<int64_t>(nc - a, llround(c->plan_f2 * (double)nc));
+  *n2 = (int)std::min<int64_t>(nc - a, want2);
 }
 
 // The planned pass of a resident cloud: per-chunk partial rows, the
@@ -1030,8 +1035,8 @@ extern "C" int fsdf_chunk_costs(fsdf_ctx* c, uint32_t* costs_out, int64_t* count
 extern "C" int fsdf_set_plan(fsdf_ctx* c, int32_t enable, double four_way_share, double two_way_share,
                              int64_t max_points) {
   if (!c) return FSDF_ERR_ARG;
-  if (!(four_way_share >= 0.0 && four_way_share <= 1.0 && two_way_share >= 0.0 && two_way_share <= 1.0))
-    return fail(c, FSDF_ERR_ARG, "set_plan: shares must lie in [0, 1]");
+  if (!(four_way_share <= 1.0 && two_way_share <= 1.0) || four_way_share != four_way_share || two_way_share != two_way_share)
+    return fail(c, FSDF_ERR_ARG, "set_plan: shares must lie in [0, 1] (or < 0: the default counts)");
   if (max_points < -1) return fail(c, FSDF_ERR_ARG, "set_plan: max_points is -1 (default) or a point count");
   c->plan_enable = enable != 0;
   c->plan_f4 = four_way_share;

@@ -149,6 +149,7 @@ struct ChunkOutputs {
   uint32_t* dur = nullptr;     // [nc] serial-equivalent chunk durations (100 MHz ticks)
   const int32_t* plan = nullptr;  // [grid][4] workgroup plan (chunk | parts << 24, chunk, chunk, chunk), or null
   int dparts = 1;              // waves per chunk without a plan (4, 2 or 1)
+  int64_t cap = 0;             // chunks allocated: csum = ent + 24 cap, dense = ent + 25 cap (one allocation)
 };
 constexpr int kPlanPartsShift = 24;
 constexpr int64_t kMaxPlanChunks = 1 << 16;  // planned passes: clouds of <= 4,194,304 points per device

@@ -1913,55 +1913,61 @@ __global__ __launch_bounds__(kPassBlock) __attribute__((amdgpu_waves_per_eu(kPas
 
 // The planned pass's reduction, one launch: workgroup x sums accumulator
 // entries 8x .. 8x+7 (entry 0 = Σ d², entry 1 + 6k + j = (F, M)_j of surface
-// k) over all chunks. Thread i takes chunks i, i + 1024, ... in order (headers
-// loaded kChunkBatch at a time, so several loads are in flight), adding the
-// entries of its tile from each chunk's sparse entries or dense row; then a
-// fixed-order DPP wave sum and a fixed-order 16-wave combine. Deterministic,
-// and it reads only the chunk rows: independent of the plan.
-constexpr int kChunkBatch = 8;
+// k) over all chunks. Thread i takes chunks i, i + 1024, ... in order,
+// kChunkBatch at a time: their headers in one round of loads, then every
+// entry of the tile gathered unconditionally (the address is the entry's slot,
+// the dense row, or a dummy whose value is masked to +0.0) — two memory
+// latencies per batch, no load behind a branch; then a fixed-order DPP wave
+// sum and a fixed-order 16-wave combine. Deterministic, and it reads only the
+// chunk rows: independent of the plan.
+constexpr int kChunkBatch = 4;
 constexpr int kChunkReduceBlock = 1024;
+// ent: the chunk rows' one allocation of `cap` chunks, [cap][24] entries |
+// [cap] Σ d² | [cap][64][6] dense rows (ChunkOutputs)
 __global__ __launch_bounds__(kChunkReduceBlock) void reduce_chunks_kernel(const I4* __restrict__ hdr,
-                                                                   const double* __restrict__ ent,
-                                                                   const double* __restrict__ csum,
-                                                                   const double* __restrict__ dense, int nc, int S,
-                                                                   double* __restrict__ accum) {
+                                                                          const double* __restrict__ ent, int64_t cap,
+                                                                          int nc, int S, double* __restrict__ accum) {
   const int x = blockIdx.x;
   const int len = 1 + 6 * S;
   const int t0 = 8 * x;
-  // the tile's surfaces: entries 1 + 6k .. 6 + 6k
-  const int k_lo = t0 >= 1 ? (t0 - 1) / 6 : 0;
-  const int k_hi = min(S - 1, (t0 + 6) / 6);
   double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   for (int c0 = threadIdx.x; c0 < nc; c0 += kChunkBatch * kChunkReduceBlock) {
     I4 h[kChunkBatch];
 #pragma unroll
     for (int u = 0; u < kChunkBatch; ++u) {
       const int c = c0 + u * kChunkReduceBlock;
-      h[u] = c < nc ? hdr[c] : I4{-1, -1, -1, -1};
+      h[u] = hdr[c < nc ? c : 0];
+    }
+    double v[kChunkBatch][8];
+#pragma unroll
+    for (int u = 0; u < kChunkBatch; ++u) {
+      const int c = c0 + u * kChunkReduceBlock;
+      const int cc = c < nc ? c : 0;
+      const bool isd = h[u][0] == -2;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int t = t0 + q;
+        const int k = t >= 1 ? (t - 1) / 6 : 0, j = t >= 1 ? (t - 1) % 6 : 0;
+        const int sl = h[u][0] == k ? 0 : (h[u][1] == k ? 1 : (h[u][2] == k ? 2 : (h[u][3] == k ? 3 : 4)));
+        // one allocation (ent | csum | dense, ChunkOutputs): an index select, not a pointer select
+        // (LLVM splits a select of pointers feeding a load into branches)
+        const int64_t off = t == 0 ? cap * 24 + cc
+                                   : (isd ? cap * 25 + ((int64_t)cc * 64 + (k < 64 ? k : 0)) * 6 + j
+                                          : (int64_t)cc * 24 + (sl < 4 ? 6 * sl + j : 0));
+        v[u][q] = ent[off];
+      }
     }
 #pragma unroll
     for (int u = 0; u < kChunkBatch; ++u) {
       const int c = c0 + u * kChunkReduceBlock;
-      if (c >= nc) break;
-      if (x == 0) acc[0] += csum[c];
-      if (h[u][0] == -2) {
-        for (int q = 0; q < 8; ++q) {
-          const int t = t0 + q;
-          if (t >= 1 && t < len) acc[q] += dense[((int64_t)c * 64 + (t - 1) / 6) * 6 + (t - 1) % 6];
-        }
-        continue;
-      }
+      const bool isd = h[u][0] == -2;
 #pragma unroll
-      for (int sl = 0; sl < 4; ++sl) {
-        const int k = h[u][sl];
-        if (k < 0) break;
-        if (k < k_lo || k > k_hi) continue;
-        const double* e = ent + ((int64_t)c * 4 + sl) * 6;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int j = t0 + q - 1 - 6 * k;  // entry t0+q as component j of surface k
-          if (j >= 0 && j < 6) acc[q] += e[j];
-        }
+      for (int q = 0; q < 8; ++q) {
+        const int t = t0 + q;
+        const int k = t >= 1 ? (t - 1) / 6 : 0;
+        const bool present = t == 0 || isd || h[u][0] == k || h[u][1] == k || h[u][2] == k || h[u][3] == k;
+        // (+0.0 for an absent entry: acc never holds -0.0, so adding it is exact)
+        acc[q] += (c < nc && t < len && present) ? v[u][q] : 0.0;
       }
     }
   }
@@ -2557,10 +2563,10 @@ hipError_t launch_reduce_chunks(const ChunkOutputs& co, int64_t nc, int S, doubl
   const int len = 1 + 6 * S;
   if (ev_stop)
     hipExtLaunchKernelGGL(reduce_chunks_kernel, dim3((len + 7) / 8), dim3(kChunkReduceBlock), 0u, s, nullptr, ev_stop, 0u,
-                          (const I4*)co.hdr, co.ent, co.csum, co.dense, (int)nc, S, d_accum);
+                          (const I4*)co.hdr, co.ent, co.cap, (int)nc, S, d_accum);
   else
     hipLaunchKernelGGL(reduce_chunks_kernel, dim3((len + 7) / 8), dim3(kChunkReduceBlock), 0, s, (const I4*)co.hdr, co.ent,
-                       co.csum, co.dense, (int)nc, S, d_accum);
+                       co.cap, (int)nc, S, d_accum);
   return hipGetLastError();
 }
 

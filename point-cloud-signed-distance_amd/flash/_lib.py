@@ -324,10 +324,11 @@ class Context:
         check(self._lib.fsdf_set_partition(self._ctx, int(four_way_max_points), int(two_way_max_points)), self._ctx,
               "set_partition")
 
-    def set_plan(self, enable: bool = True, four_way_share: float = 1.0 / 32, two_way_share: float = 1.0 / 16,
+    def set_plan(self, enable: bool = True, four_way_share: float = -1.0, two_way_share: float = -1.0,
                  max_points: int = -1):
         """Planned pass of resident clouds (fsdf_set_plan): enable, the shares
-        of chunks split over 4 / 2 waves, the largest cloud it runs (-1: default)."""
+        of chunks split over 4 / 2 waves (< 0: the default counts), the
+        largest cloud it runs (-1: default)."""
         check(self._lib.fsdf_set_plan(self._ctx, int(enable), float(four_way_share), float(two_way_share),
                                       int(max_points)), self._ctx, "set_plan")
 

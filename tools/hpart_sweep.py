@@ -38,8 +38,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--tiers", default="", help="comma-separated subset of " + ",".join(TIERS))
-    ap.add_argument("--four-share", type=float, default=1.0 / 32)
-    ap.add_argument("--two-share", type=float, default=1.0 / 16)
+    ap.add_argument("--four-share", type=float, default=-1.0, help="< 0: the library's default counts")
+    ap.add_argument("--two-share", type=float, default=-1.0)
     ap.add_argument("--dump-costs", default="", help="npz path: the planned pass's per-chunk durations per size")
     a = ap.parse_args()
     import torch

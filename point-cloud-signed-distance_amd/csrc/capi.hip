@@ -854,7 +854,7 @@ static int ensure_chunk_outputs(fsdf_ctx* c, int64_t nc) {
   c->co_cap = 0;
   c->plan_nc = -1;
   HIPCHECK(c, hipMalloc(&c->co.hdr, (size_t)nc * 4 * sizeof(int32_t)));
-  // one allocation: entries [nc][24] | Σ d² [nc] | dense rows [nc][64][6] (reduce_chunks_kernel indexes it)
+  // one allocation: entries [nc][24] | Σ d² [nc] | dense rows [nc][64][6]
   HIPCHECK(c, hipMalloc(&c->co.ent, (size_t)nc * (24 + 1 + 64 * 6) * sizeof(double)));
   c->co.csum = c->co.ent + (size_t)nc * 24;
   c->co.dense = c->co.ent + (size_t)nc * 25;
@@ -888,13 +888,17 @@ static void plan_shape(fsdf_ctx* c, int64_t nc, int* n4, int* n2) {
 }
 
 // The planned pass of a resident cloud: per-chunk partial rows, the
-// two-level chunk reduction, and a plan rebuilt from this pass's chunk
-// durations on the first pass of a cloud and then every kOrderEvery passes.
+// two-level chunk reduction (16-chunk groups, then the tile reduce), and a
+// plan rebuilt from this pass's chunk durations on the first pass of a cloud
+// and then every kOrderEvery passes.
 static int run_planned(fsdf_ctx* c, const fsdf::PosedModel& P, const void* d_pts, int64_t n, double* d_accum,
                        fsdf::PassOutputs& out, hipEvent_t* pe) {
   const int64_t nc = (n + 63) / 64;
   int rc = ensure_chunk_outputs(c, nc);
   if (rc) return rc;
+  rc = ensure_partials(c, (int)std::max<int64_t>(fsdf::pass_blocks(n, c->lm), fsdf::reduce_chunk_groups(nc)));
+  if (rc) return rc;
+  out.partials = c->d_partials;
   out.cost = nullptr;
   out.order = nullptr;
   fsdf::ChunkOutputs co = c->co;

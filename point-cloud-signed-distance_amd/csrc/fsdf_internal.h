@@ -159,8 +159,10 @@ bool planned_pass(const LocalModel& lm, int64_t n);
 hipError_t launch_planned_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const void* d_pts,
                                int64_t n, int grid, const PassOutputs& out, const ChunkOutputs& co, hipStream_t s,
                                hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
-// the accumulator d_accum [1 + 6S] from the chunk rows, in chunk order (one
-// launch; `partials` unused)
+// the accumulator d_accum [1 + 6S] from the chunk rows, in chunk order: 16-chunk
+// group rows into `partials` (reduce_chunk_groups(nc) rows, line-tiled), then
+// the unplanned pass's tile reduce over them
+int64_t reduce_chunk_groups(int64_t nc);
 hipError_t launch_reduce_chunks(const ChunkOutputs& co, int64_t nc, int S, double* partials, double* d_accum,
                                 hipStream_t s, hipEvent_t ev_stop = nullptr);
 // the plan of the next passes from the chunk durations of this one

@@ -1911,82 +1911,59 @@ __global__ __launch_bounds__(kPassBlock) __attribute__((amdgpu_waves_per_eu(kPas
   }
 }
 
-// The planned pass's reduction, one launch: workgroup x sums accumulator
-// entries 8x .. 8x+7 (entry 0 = Σ d², entry 1 + 6k + j = (F, M)_j of surface
-// k) over all chunks. Thread i takes chunks i, i + 1024, ... in order,
-// kChunkBatch at a time: their headers in one round of loads, then every
-// entry of the tile gathered unconditionally (the address is the entry's slot,
-// the dense row, or a dummy whose value is masked to +0.0) — two memory
-// latencies per batch, no load behind a branch; then a fixed-order DPP wave
-// sum and a fixed-order 16-wave combine. Deterministic, and it reads only the
-// chunk rows: independent of the plan.
-constexpr int kChunkBatch = 4;
-constexpr int kChunkReduceBlock = 1024;
-// ent: the chunk rows' one allocation of `cap` chunks, [cap][24] entries |
-// [cap] Σ d² | [cap][64][6] dense rows (ChunkOutputs)
-__global__ __launch_bounds__(kChunkReduceBlock) void reduce_chunks_kernel(const I4* __restrict__ hdr,
-                                                                          const double* __restrict__ ent, int64_t cap,
-                                                                          int nc, int S, double* __restrict__ accum) {
-  const int x = blockIdx.x;
+// The planned pass's reduction, stage 1: workgroup g sums the chunk rows of
+// chunks 16g .. 16g+15 into row g of the line-tiled partials, which
+// reduce_tiles_kernel (the unplanned pass's stage 2) then sums. The group's
+// rows are expanded in LDS into a dense [16][len] table — zeros, each sparse
+// entry scattered to its surface's columns, dense rows copied — and thread t
+// sums column t over the 16 chunks in order. The sparse entries and Σ d² are
+// one coalesced, unconditional read each (whatever the header says), issued
+// before the headers are known: one memory latency per group. Deterministic,
+// and it reads only the chunk rows: independent of the plan.
+// (Gathering entry columns straight from the chunk rows — a thread per entry,
+// a lane per chunk — touches 64 lines per wave load: 17 us at 2^17 points,
+// 70 us at 2^20, tag-lookup bound on the few CUs the 49 tiles occupy.)
+constexpr int kGroupChunks = 16;
+constexpr int kGroupBlock = 512;
+static_assert(kGroupChunks * 24 <= kGroupBlock, "one sparse entry per thread");
+__global__ __launch_bounds__(kGroupBlock) void chunk_groups_kernel(const I4* __restrict__ hdr,
+                                                                   const double* __restrict__ ent,
+                                                                   const double* __restrict__ csum,
+                                                                   const double* __restrict__ dense, int nc, int S,
+                                                                   double* __restrict__ partials, int ngroups) {
   const int len = 1 + 6 * S;
-  const int t0 = 8 * x;
-  double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  for (int c0 = threadIdx.x; c0 < nc; c0 += kChunkBatch * kChunkReduceBlock) {
-    I4 h[kChunkBatch];
-#pragma unroll
-    for (int u = 0; u < kChunkBatch; ++u) {
-      const int c = c0 + u * kChunkReduceBlock;
-      h[u] = hdr[c < nc ? c : 0];
-    }
-    double v[kChunkBatch][8];
-#pragma unroll
-    for (int u = 0; u < kChunkBatch; ++u) {
-      const int c = c0 + u * kChunkReduceBlock;
-      const int cc = c < nc ? c : 0;
-      const bool isd = h[u][0] == -2;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int t = t0 + q;
-        const int k = t >= 1 ? (t - 1) / 6 : 0, j = t >= 1 ? (t - 1) % 6 : 0;
-        const int sl = h[u][0] == k ? 0 : (h[u][1] == k ? 1 : (h[u][2] == k ? 2 : (h[u][3] == k ? 3 : 4)));
-        // one allocation (ent | csum | dense, ChunkOutputs): an index select, not a pointer select
-        // (LLVM splits a select of pointers feeding a load into branches)
-        const int64_t off = t == 0 ? cap * 24 + cc
-                                   : (isd ? cap * 25 + ((int64_t)cc * 64 + (k < 64 ? k : 0)) * 6 + j
-                                          : (int64_t)cc * 24 + (sl < 4 ? 6 * sl + j : 0));
-        v[u][q] = ent[off];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kChunkBatch; ++u) {
-      const int c = c0 + u * kChunkReduceBlock;
-      const bool isd = h[u][0] == -2;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int t = t0 + q;
-        const int k = t >= 1 ? (t - 1) / 6 : 0;
-        const bool present = t == 0 || isd || h[u][0] == k || h[u][1] == k || h[u][2] == k || h[u][3] == k;
-        // (+0.0 for an absent entry: acc never holds -0.0, so adding it is exact)
-        acc[q] += (c < nc && t < len && present) ? v[u][q] : 0.0;
-      }
-    }
+  const int g = blockIdx.x, tid = threadIdx.x;
+  const int c0 = g * kGroupChunks;
+  double* tab = (double*)fsdf_lds;                // [kGroupChunks][len]
+  I4* sh = (I4*)(tab + kGroupChunks * len);       // [kGroupChunks] headers
+  const int ec = tid / 24;                         // this thread's sparse entry: chunk c0 + ec, slot (tid % 24) / 6
+  const bool inr = tid < kGroupChunks * 24 && c0 + ec < nc;
+  const double v = ent[inr ? (int64_t)c0 * 24 + tid : 0];
+  const int hc = c0 + (tid & (kGroupChunks - 1));
+  const bool hv = hc < nc;
+  const I4 h = hdr[hv ? hc : 0];
+  const double cs = csum[hv ? hc : 0];
+  for (int i = tid; i < kGroupChunks * len; i += kGroupBlock) tab[i] = 0.0;
+  if (tid < kGroupChunks) sh[tid] = hv ? h : I4{-1, -1, -1, -1};
+  __syncthreads();
+  if (tid < kGroupChunks && hv) tab[tid * len] = cs;
+  if (inr) {
+    const I4 hh = sh[ec];
+    const int sl = (tid % 24) / 6, j = tid % 6;
+    const int k = sl == 0 ? hh[0] : (sl == 1 ? hh[1] : (sl == 2 ? hh[2] : hh[3]));
+    if (hh[0] != -2 && k >= 0 && k < S) tab[ec * len + 1 + 6 * k + j] = v;
   }
-  constexpr int W = kChunkReduceBlock / 64;
-  __shared__ double sh[8][W];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const double w = wave_sum(acc[q]);
-    if (lane == 0) sh[q][wave] = w;
+  // dense rows (a chunk that met more than 4 surfaces): entry 1 + i = dense[i]
+  for (int c = 0; c < kGroupChunks; ++c) {
+    if (sh[c][0] == -2)
+      for (int i = tid; i < 6 * S; i += kGroupBlock) tab[c * len + 1 + i] = dense[(int64_t)(c0 + c) * 64 * 6 + i];
   }
   __syncthreads();
-  const int t = t0 + (int)threadIdx.x;
-  if (threadIdx.x < 8 && t < len) {
-    double a[4];
+  for (int t = tid; t < len; t += kGroupBlock) {
+    double s = 0.0;
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
-      a[g] = (sh[threadIdx.x][4 * g] + sh[threadIdx.x][4 * g + 1]) + (sh[threadIdx.x][4 * g + 2] + sh[threadIdx.x][4 * g + 3]);
-    accum[t] = (a[0] + a[1]) + (a[2] + a[3]);
+    for (int c = 0; c < kGroupChunks; ++c) s += tab[c * len + t];
+    partials[pidx(t, g, ngroups)] = s;
   }
 }
 
@@ -2559,16 +2536,15 @@ hipError_t launch_planned_pass(int precision, bool cull, const LocalModel& lm, c
 
 hipError_t launch_reduce_chunks(const ChunkOutputs& co, int64_t nc, int S, double* partials, double* d_accum,
                                 hipStream_t s, hipEvent_t ev_stop) {
-  (void)partials;
   const int len = 1 + 6 * S;
-  if (ev_stop)
-    hipExtLaunchKernelGGL(reduce_chunks_kernel, dim3((len + 7) / 8), dim3(kChunkReduceBlock), 0u, s, nullptr, ev_stop, 0u,
-                          (const I4*)co.hdr, co.ent, co.cap, (int)nc, S, d_accum);
-  else
-    hipLaunchKernelGGL(reduce_chunks_kernel, dim3((len + 7) / 8), dim3(kChunkReduceBlock), 0, s, (const I4*)co.hdr, co.ent,
-                       co.cap, (int)nc, S, d_accum);
-  return hipGetLastError();
+  const int ngroups = (int)reduce_chunk_groups(nc);
+  const size_t lds = (size_t)kGroupChunks * len * sizeof(double) + kGroupChunks * sizeof(I4);
+  hipLaunchKernelGGL(chunk_groups_kernel, dim3(ngroups), dim3(kGroupBlock), lds, s, (const I4*)co.hdr, co.ent, co.csum,
+                     co.dense, (int)nc, S, partials, ngroups);
+  return launch_reduce(partials, ngroups, len, d_accum, s, nullptr, nullptr, ev_stop);
 }
+
+int64_t reduce_chunk_groups(int64_t nc) { return (nc + kGroupChunks - 1) / kGroupChunks; }
 
 hipError_t launch_plan(const uint32_t* dur, int64_t nc, int n4, int n2, int32_t* order, int32_t* plan, hipStream_t s) {
   hipLaunchKernelGGL(plan_kernel, dim3(1), dim3(kPlanBlock), 0, s, dur, (int)nc, n4, n2, order, (I4*)plan);

@@ -44,11 +44,6 @@ void dfree(P*& p) {
 
 }  // namespace
 
-// the planned pass's default size limit (fsdf_set_plan max_points)
-#ifndef FSDF_PLAN_MAX_POINTS
-#define FSDF_PLAN_MAX_POINTS 524288
-#endif
-static constexpr int64_t kPlanMaxPointsDefault = FSDF_PLAN_MAX_POINTS;
 // default plan composition: chunks split over 4 / 2 waves (fsdf_set_plan shares < 0)
 static constexpr int64_t kPlanDefault4 = 96, kPlanDefault2 = 192;
 
@@ -136,7 +131,7 @@ struct fsdf_ctx {
   int plan_enable = 1;
   double plan_f4 = -1.0, plan_f2 = -1.0;  // shares of the chunks split over 4 / 2 waves (< 0: default counts)
   int wave_slots = 0;                // device wave slots at the pass's occupancy (0: not queried yet)
-  int64_t plan_max_points = kPlanMaxPointsDefault;  // planned pass up to this cloud size (per device)
+  int64_t plan_max_points = -1;      // planned pass up to this cloud size (per device; -1: the model's default)
   double* d_accum = nullptr;
   int32_t* d_kstar = nullptr;
   double* d_d = nullptr;
@@ -951,7 +946,8 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
   out.perm = d_perm;
   out.stats = c->stats_on ? c->d_stats : nullptr;
   out.chunk_ws = FSDF_CHUNK_WS && d_pts == c->d_pts && n == c->n ? c->d_chunk_ws : nullptr;  // resident cloud only
-  if (schedule && n > 0 && c->plan_enable && n <= c->plan_max_points && c->precision == 64 &&
+  const int64_t plan_max = c->plan_max_points >= 0 ? c->plan_max_points : fsdf::planned_default_max_points(c->lm);
+  if (schedule && n > 0 && c->plan_enable && n <= plan_max && c->precision == 64 &&
       fsdf::planned_pass(c->lm, n)) {
     const bool prof = c->profiling && c->prof_used + 3 <= c->prof_ev.size();
     hipEvent_t* pe = prof ? &c->prof_ev[c->prof_used] : nullptr;
@@ -1045,7 +1041,7 @@ extern "C" int fsdf_set_plan(fsdf_ctx* c, int32_t enable, double four_way_share,
   c->plan_enable = enable != 0;
   c->plan_f4 = four_way_share;
   c->plan_f2 = two_way_share;
-  c->plan_max_points = max_points < 0 ? kPlanMaxPointsDefault : max_points;
+  c->plan_max_points = max_points < 0 ? -1 : max_points;
   c->plan_nc = -1;  // rebuilt on the next pass
   return FSDF_OK;
 }

@@ -422,8 +422,14 @@ constexpr int kHpartBlock = kPassBlock;
 // M64-measured tiers, smaller ones kHpartSmall4 / kHpartSmall2 (measured on
 // IRB140, C2)
 constexpr int kHpartFullHulls = 32;
-constexpr int64_t kHpartSmall4 = 196608;
-constexpr int64_t kHpartSmall2 = 393216;
+constexpr int64_t kHpartSmall4 = 98304;
+constexpr int64_t kHpartSmall2 = 327680;
+// planned pass up to (fsdf_set_plan max_points -1): above it the unplanned
+// grid measured faster — M64 between 2^19 and 2^20 points, IRB140 between
+// 393,216 and 2^19 (the planned reduction's extra launch outweighs a pass that
+// is already short; profiles/r04/hpart_sweep_c2.jsonl)
+constexpr int64_t kPlanMaxFull = 524288;
+constexpr int64_t kPlanMaxSmall = 393216;
 constexpr int kAliasBlock = kPassBlock;
 
 // The one diagnostic build (-DFSDF_WAVE_TIMES=1, tools/wave_times.py): a
@@ -2225,10 +2231,11 @@ static size_t hpart_lds_bytes(const LocalModel& lm, int parts) {
 // hpart4 limit, 2 up to its hpart2 limit (LocalModel; fsdf_set_partition
 // overrides them per context, 0 disables a tier).
 void hpart_default_limits(const LocalModel& lm, int64_t* four, int64_t* two) {
-  // Measured crossovers (same-box A/B): M64 (64 hulls) 4-way up
-  // to 196,608 points, 2-way up to 393,216; IRB140 (7 hulls) — the partition
-  // splits a chunk's few candidate hulls over the waves, see the C2 sweep
-  // (profiles/r04/hpart_sweep_c2.json) — HPART_SMALL_* below.
+  // Measured crossovers (same-box size sweeps of every tier):
+  // M64 (64 hulls) 4-way up to 196,608 points, 2-way up to 393,216
+  // (profiles/r04/plan_sweeps_r04def.jsonl); IRB140 (7 hulls) 4-way up to
+  // 98,304, 2-way up to 327,680 (profiles/r04/hpart_sweep_c2.jsonl: 4-way
+  // best at 2^16, 2-way at 2^17..2^18, one wave from 393,216)
   if (lm.K >= kHpartFullHulls) {
     *four = 196608;
     *two = 393216;
@@ -2236,6 +2243,10 @@ void hpart_default_limits(const LocalModel& lm, int64_t* four, int64_t* two) {
     *four = kHpartSmall4;
     *two = kHpartSmall2;
   }
+}
+
+int64_t planned_default_max_points(const LocalModel& lm) {
+  return lm.K >= kHpartFullHulls ? kPlanMaxFull : kPlanMaxSmall;
 }
 
 int hpart_parts(const LocalModel& lm, int64_t n) {

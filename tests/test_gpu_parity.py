@@ -403,3 +403,25 @@ def test_planned_pass_bits_independent_of_plan(m64, oracle_mod, ctx_factory, sor
     assert np.allclose(al, a0, rtol=1e-11, atol=1e-12 * np.abs(a0).max())
     om = oracle_mod.OracleModel.from_manipulator(m64)
     _check_against(om.skin(poses, pts), p0[1], p0[0], p0[2], a0, om.cost_accum(poses, pts))
+
+
+@pytest.mark.parametrize("model,limit", [("m64", 524288), ("irb", 393216)])
+def test_planned_pass_default_limit_per_model(m64, irb, ctx_factory, model, limit):
+    """The planned pass's default size limit follows the model (fsdf_set_plan
+    max_points -1; DESIGN.md §7, profiles/r04/hpart_sweep_c2.jsonl): up to the
+    limit a resident pass runs planned, one point more runs the unplanned grid
+    — with the same per-point bits on the points both clouds share."""
+    import flash
+    from flash import synthetic
+    m = {"m64": m64, "irb": irb}[model]
+    qt, qe = synthetic.perturbed_configuration(m, 505)
+    poses = flash.hull_poses(m, qe)
+    pts = synthetic.depth_cloud(m, qt, limit + 1, seed=506, order="shuffled")
+    out = {}
+    for mm, planned in ((limit, True), (limit + 1, False)):
+        ctx = ctx_factory(m)
+        ctx.set_points(pts[:mm])
+        out[mm] = ctx.eval(poses, per_point=True)
+        assert ctx.pass_kernel_name().startswith("planned_pass_kernel") == planned, (mm, ctx.pass_kernel_name())
+    for x, y in zip(out[limit][2], out[limit + 1][2]):
+        assert np.array_equal(x, y[:limit])

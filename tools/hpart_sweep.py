@@ -24,10 +24,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "point-cloud-signed-distance_amd"))
 
 # tier: (4-way limit, 2-way limit, planned pass) — the first three run the
-# unplanned grid (fsdf_set_plan off) at a forced tier; "planned" is the
-# product default (per-chunk plan from measured durations, fsdf_set_plan)
+# unplanned grid (fsdf_set_plan off) at a forced tier, "unplanned" at the
+# model's default tier; "planned" forces the planned pass (per-chunk plan from
+# measured durations, fsdf_set_plan) at every size; "default" is the product
+# default (planned up to the model's size limit, unplanned above)
 TIERS = {"4-way": (1 << 40, 0, False), "2-way": (0, 1 << 40, False), "one-wave": (0, 0, False),
-         "unplanned": (-1, -1, False), "planned": (-1, -1, True)}
+         "unplanned": (-1, -1, False), "planned": (-1, -1, True), "default": (-1, -1, None)}
 
 
 def main():
@@ -68,7 +70,7 @@ def main():
                 if a.tiers and tier not in a.tiers.replace("+", ",").split(","):
                     continue
                 ctx.set_partition(l4, l2)
-                ctx.set_plan(plan, a.four_share, a.two_share, 1 << 30)
+                ctx.set_plan(plan is not False, a.four_share, a.two_share, -1 if plan is None else 1 << 30)
                 for i in range(5):
                     ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs)
                 torch.cuda.synchronize()

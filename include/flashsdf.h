@@ -341,9 +341,10 @@ int fsdf_get_partition(fsdf_ctx* ctx, int64_t n, int64_t* four_way_max_out, int6
  * idle wave slots for (a strong-scaling shard smaller than the machine splits
  * its heaviest third). A new cloud's first pass runs the tier shape of
  * fsdf_set_partition. max_points: the largest cloud (points per device) the
- * planned pass runs, -1 = the model's default (524,288 points for models of
- * >= 32 hulls, 393,216 for smaller ones: above them the unplanned grid
- * measured faster). */
+ * planned pass runs, -1 = the model's default window: more than 98,304 and
+ * at most 524,288 points for models of >= 32 hulls, 393,216 for smaller ones
+ * (outside it the unplanned grid measured faster); a value >= 0
+ * runs it for every cloud of 1 .. max_points points. */
 int fsdf_set_plan(fsdf_ctx* ctx, int32_t enable, double four_way_share, double two_way_share, int64_t max_points);
 
 /* Diagnostics: the serial-equivalent durations (100 MHz ticks) the last

@@ -946,8 +946,10 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
   out.perm = d_perm;
   out.stats = c->stats_on ? c->d_stats : nullptr;
   out.chunk_ws = FSDF_CHUNK_WS && d_pts == c->d_pts && n == c->n ? c->d_chunk_ws : nullptr;  // resident cloud only
+  // planned window: (default min, model's default max], or (0, max_points] when set
   const int64_t plan_max = c->plan_max_points >= 0 ? c->plan_max_points : fsdf::planned_default_max_points(c->lm);
-  if (schedule && n > 0 && c->plan_enable && n <= plan_max && c->precision == 64 &&
+  const int64_t plan_min = c->plan_max_points >= 0 ? 0 : fsdf::planned_default_min_points();
+  if (schedule && n > plan_min && c->plan_enable && n <= plan_max && c->precision == 64 &&
       fsdf::planned_pass(c->lm, n)) {
     const bool prof = c->profiling && c->prof_used + 3 <= c->prof_ev.size();
     hipEvent_t* pe = prof ? &c->prof_ev[c->prof_used] : nullptr;

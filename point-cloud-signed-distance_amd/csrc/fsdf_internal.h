@@ -156,8 +156,10 @@ constexpr int64_t kMaxPlanChunks = 1 << 16;  // planned passes: clouds of <= 4,1
 
 // a resident pass over n points of this model can run planned
 bool planned_pass(const LocalModel& lm, int64_t n);
-// the largest cloud the planned pass runs by default (fsdf_set_plan max_points -1)
+// the cloud sizes the planned pass runs by default (fsdf_set_plan max_points
+// -1): min < n <= max
 int64_t planned_default_max_points(const LocalModel& lm);
+int64_t planned_default_min_points();
 hipError_t launch_planned_pass(int precision, bool cull, const LocalModel& lm, const PosedModel& pm, const void* d_pts,
                                int64_t n, int grid, const PassOutputs& out, const ChunkOutputs& co, hipStream_t s,
                                hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);

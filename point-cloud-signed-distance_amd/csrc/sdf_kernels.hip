@@ -430,6 +430,10 @@ constexpr int64_t kHpartSmall2 = 327680;
 // is already short; profiles/r04/hpart_sweep_c2.jsonl)
 constexpr int64_t kPlanMaxFull = 524288;
 constexpr int64_t kPlanMaxSmall = 393216;
+// ... and from above kPlanMinPoints: below it the unplanned 4-way tier measured
+// faster for both models (2^16 points: M64 0.0644 vs 0.0662 ms, IRB140 0.0433
+// vs 0.0448 — the planned reduction's second launch is not paid back)
+constexpr int64_t kPlanMinPoints = 98304;
 constexpr int kAliasBlock = kPassBlock;
 
 // The one diagnostic build (-DFSDF_WAVE_TIMES=1, tools/wave_times.py): a
@@ -2248,6 +2252,7 @@ void hpart_default_limits(const LocalModel& lm, int64_t* four, int64_t* two) {
 int64_t planned_default_max_points(const LocalModel& lm) {
   return lm.K >= kHpartFullHulls ? kPlanMaxFull : kPlanMaxSmall;
 }
+int64_t planned_default_min_points() { return kPlanMinPoints; }
 
 int hpart_parts(const LocalModel& lm, int64_t n) {
   if (!(FSDF_RED_IN_STAGE && lm.planes64 && lm.S <= 64 && lm.R == 0 && n > 0)) return 0;

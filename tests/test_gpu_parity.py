@@ -339,7 +339,7 @@ def test_hull_partitioned_pass_matches_one_wave_per_chunk(m64, irb, ctx_factory,
     for cull in (True, False):
         for mm in (n, n + 1):
             ctx = ctx_factory(m, cull=cull)
-            ctx.set_plan(planned)
+            ctx.set_plan(planned, -1, -1, 1 << 30)  # (planned at every size: the tier's first-pass shape)
             ctx.set_points(pts[:mm])
             out[cull, mm] = ctx.eval(poses, per_point=True)
             name = ctx.pass_kernel_name()
@@ -348,7 +348,7 @@ def test_hull_partitioned_pass_matches_one_wave_per_chunk(m64, irb, ctx_factory,
             else:
                 assert name.endswith(f"true, true, 256, {tier}>") == (mm == n), name
     forced = ctx_factory(m)
-    forced.set_plan(planned)
+    forced.set_plan(planned, -1, -1, 1 << 30)
     forced.set_partition(0, 0)
     forced.set_points(pts[:n])
     _, _, (kf, df, gf) = forced.eval(poses, per_point=True)
@@ -405,12 +405,14 @@ def test_planned_pass_bits_independent_of_plan(m64, oracle_mod, ctx_factory, sor
     _check_against(om.skin(poses, pts), p0[1], p0[0], p0[2], a0, om.cost_accum(poses, pts))
 
 
-@pytest.mark.parametrize("model,limit", [("m64", 524288), ("irb", 393216)])
-def test_planned_pass_default_limit_per_model(m64, irb, ctx_factory, model, limit):
-    """The planned pass's default size limit follows the model (fsdf_set_plan
+@pytest.mark.parametrize("model,limit,above", [("m64", 524288, False), ("irb", 393216, False), ("irb", 98304, True)])
+def test_planned_pass_default_limit_per_model(m64, irb, ctx_factory, model, limit, above):
+    """The planned pass's default size window follows the model (fsdf_set_plan
     max_points -1; DESIGN.md §7, profiles/r04/hpart_sweep_c2.jsonl): up to the
-    limit a resident pass runs planned, one point more runs the unplanned grid
-    — with the same per-point bits on the points both clouds share."""
+    upper limit a resident pass runs planned, one point more runs the unplanned
+    grid; at the lower limit (98,304 points, both models) unplanned, one point
+    more planned — with the same per-point bits on the points both clouds
+    share."""
     import flash
     from flash import synthetic
     m = {"m64": m64, "irb": irb}[model]
@@ -418,7 +420,7 @@ def test_planned_pass_default_limit_per_model(m64, irb, ctx_factory, model, limi
     poses = flash.hull_poses(m, qe)
     pts = synthetic.depth_cloud(m, qt, limit + 1, seed=506, order="shuffled")
     out = {}
-    for mm, planned in ((limit, True), (limit + 1, False)):
+    for mm, planned in ((limit, not above), (limit + 1, above)):
         ctx = ctx_factory(m)
         ctx.set_points(pts[:mm])
         out[mm] = ctx.eval(poses, per_point=True)

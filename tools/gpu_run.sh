@@ -58,7 +58,7 @@ for r in csv.DictReader(open(f)):
         || { echo SMOKE FAILED; tail $O/smoke.log; exit 1; }
       tail -2 $O/smoke.log ;;
     bench)
-      timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_default.json 2> $O/bench_default.err \
+      timeout -k 10 300 python bench.py > $O/bench_default.json 2> $O/bench_default.err \
         || { echo BENCH FAILED; tail $O/bench_default.err; exit 1; }
       cut -c1-400 $O/bench_default.json ;;
     bench:*)

@@ -74,6 +74,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--settle-ms", type=float, default=200.0,
+                   help="untimed passes for this long before the W warmup steps: the GPU's clocks ramp up over "
+                        "the first tens of ms of load (2^20 pass kernel 0.103 ms after 5 passes, 0.093 after 300, "
+                        "profiles/r04/warmup_ab.txt)")
     p.add_argument("--config", default="m64", choices=sorted(CONFIGS))
     g = p.add_mutually_exclusive_group()
     g.add_argument("--points", type=int, default=None, help="points per GPU (weak scaling)")
@@ -249,6 +253,16 @@ def main():
                     pending[s_].wait()
                     pending[s_] = None
 
+        # settle: untimed passes (no collectives: the ranks' counts differ) until
+        # the clocks have ramped, wall-clock bound
+        t_settle = time.perf_counter()
+        i = 0
+        while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+            ctx.eval_device(poses[i & 1], accums[i & 1].data_ptr(), *outs)
+            i += 1
+            if i % 16 == 0:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
         for i in range(args.warmup):
             step(i)
         drain()
@@ -365,6 +379,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_ms": args.settle_ms,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": scaling,

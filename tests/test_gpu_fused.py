@@ -11,8 +11,11 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["irb140", "arm_grid", "table"])
-def test_fused_matches_composed(name):
+@pytest.mark.parametrize("name,n", [("irb140", 60000), ("arm_grid", 60000), ("table", 20000),
+                                    ("irb140", 150000), ("arm_grid", 150000)])
+def test_fused_matches_composed(name, n):
+    """(150,000 points: inside the planned pass's window — its per-chunk rows and
+    two-level reduction write the accumulator straight into pinned host memory)"""
     import flash
     from flash import Models, synthetic, _lib
     from flash.core import surface_poses
@@ -24,13 +27,14 @@ def test_fused_matches_composed(name):
         x[:4] = [0.9, 0.2, -0.3, 0.1]  # un-normalized quaternion
         x[4:7] = [0.05, -0.02, 0.01]
         qt = mech.normalize(x)
-        pts = qt[4:7] + np.random.default_rng(3).uniform(-0.4, 0.4, size=(20000, 3))
+        pts = qt[4:7] + np.random.default_rng(3).uniform(-0.4, 0.4, size=(n, 3))
     else:
         qt, x = synthetic.perturbed_configuration(m, 17)
-        pts = synthetic.depth_cloud(m, qt, 60000, seed=18)
+        pts = synthetic.depth_cloud(m, qt, n, seed=18)
     cf = CostFunctor(m, pts)
     assert cf._native
     c1, g1 = cf.value_and_gradient(x)
+    assert cf.ctx.pass_kernel_name().startswith("planned_pass_kernel") == (n > 98304)
     # composed host path on the same context
     poses = surface_poses(m, mech.normalize(x))
     c0, acc, _ = cf.ctx.eval(poses)

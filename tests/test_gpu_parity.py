@@ -427,3 +427,28 @@ def test_planned_pass_default_limit_per_model(m64, irb, ctx_factory, model, limi
         assert ctx.pass_kernel_name().startswith("planned_pass_kernel") == planned, (mm, ctx.pass_kernel_name())
     for x, y in zip(out[limit][2], out[limit + 1][2]):
         assert np.array_equal(x, y[:limit])
+
+
+def test_planned_pass_follows_cloud_changes(m64, ctx_factory):
+    """A context's plan belongs to its cloud: after set_points with a smaller,
+    then a larger cloud (chunk rows reallocated, plan rebuilt on the new cloud's
+    first pass) every pass equals a fresh context's on that cloud bit for bit —
+    no stale plan entry, no stale chunk row."""
+    import flash
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(m64, 707)
+    poses = flash.hull_poses(m64, qe)
+    big = synthetic.depth_cloud(m64, qt, 300000 + 77, seed=708, order="shuffled")
+    small = synthetic.depth_cloud(m64, qt, 150000 + 5, seed=709, order="shuffled")
+    ctx = ctx_factory(m64, sort_points=True)
+    for pts in (big[:300000], small, big):
+        fresh = ctx_factory(m64, sort_points=True)
+        fresh.set_points(pts)
+        want = fresh.eval(poses, per_point=True)
+        ctx.set_points(pts)
+        for _ in range(3):  # first pass (tier shape), then planned
+            c, a, pp = ctx.eval(poses, per_point=True)
+            assert ctx.pass_kernel_name().startswith("planned_pass_kernel")
+            assert c == want[0] and np.array_equal(a, want[1])
+            for x, y in zip(pp, want[2]):
+                assert np.array_equal(x, y)

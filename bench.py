@@ -78,6 +78,10 @@ def parse():
                    help="untimed passes for this long before the W warmup steps: the GPU's clocks ramp up over "
                         "the first tens of ms of load (2^20 pass kernel 0.103 ms after 5 passes, 0.093 after 300, "
                         "profiles/r04/warmup_ab.txt)")
+    p.add_argument("--inflight", type=int, default=2,
+                   help="independent passes in flight: C contexts over the same resident cloud, each on its own HIP "
+                        "stream, step i on context i %% C (each context's results bit-identical to serial steps; "
+                        "profiles/r04/inflight.jsonl). 1 = one pass at a time")
     p.add_argument("--config", default="m64", choices=sorted(CONFIGS))
     g = p.add_mutually_exclusive_group()
     g.add_argument("--points", type=int, default=None, help="points per GPU (weak scaling)")
@@ -206,59 +210,85 @@ def main():
     q_alt = q_eval + 1e-3  # alternate between two configurations step to step
     poses = [flash.hull_poses(manip, q_eval), flash.hull_poses(manip, q_alt)]
 
-    ctx = manip.engine(device=local, precision=args.precision, cull=not args.no_cull, sort_points=not args.no_sort)
-    ctx.set_output_order(not args.caller_order)
-    stream = torch.cuda.current_stream(dev)
-    ctx.set_stream(stream.cuda_stream)
-    accums = [torch.zeros(ctx.accum_len, dtype=torch.float64, device=dev) for _ in range(2)]
-    accum = accums[0]
+    C = max(1, args.inflight)
+    ctxs = [manip.engine(device=local, precision=args.precision, cull=not args.no_cull,
+                         sort_points=not args.no_sort, slot=c) for c in range(C)]
+    # every context on a stream of its own, none of them HIP's null stream (whose
+    # implicit synchronisation would serialise the passes in flight); the first
+    # is made torch's current stream, so the collectives and timing events order
+    # after it
+    streams = [torch.cuda.Stream(dev) for _ in range(C)]
+    torch.cuda.set_stream(streams[0])
+    stream = streams[0]
+    for c, cx in enumerate(ctxs):
+        cx.set_output_order(not args.caller_order)
+        cx.set_stream(streams[c].cuda_stream)
+    ctx = ctxs[0]
+    # two accumulators per context (the all-reduce of one overlaps the next pass)
+    accums = [[torch.zeros(ctx.accum_len, dtype=torch.float64, device=dev) for _ in range(2)] for _ in range(C)]
+    accum = accums[0][0]
 
     def run_cloud(pts_host):
-        """Upload the cloud (timed per frame), then W untimed + K timed steps
-        bracketed by barrier + synchronize; returns the max-over-ranks
+        """Upload the cloud (timed per frame, every context), then W untimed + K
+        timed steps bracketed by barrier + synchronize; returns the max-over-ranks
         (elapsed s, whole-pass ms, pass-kernel ms, set_points ms)."""
         d_pts = torch.as_tensor(pts_host, device=dev)
         torch.cuda.synchronize()
-        ctx.set_points_device(d_pts.data_ptr(), len(pts_host))  # first upload (allocations)
+        for cx in ctxs:
+            cx.set_points_device(d_pts.data_ptr(), len(pts_host))  # first upload (allocations)
         set_ms = []
-        for _ in range(3):  # once per frame: copy (+ Hilbert sort)
+        for _ in range(3):  # once per frame: copy (+ Hilbert sort), every context
             t_set = time.perf_counter()
-            ctx.set_points_device(d_pts.data_ptr(), len(pts_host))
+            for cx in ctxs:
+                cx.set_points_device(d_pts.data_ptr(), len(pts_host))
             set_ms.append((time.perf_counter() - t_set) * 1e3)
         del d_pts
         n_ = len(pts_host)
-        if args.no_per_point:
-            outs = (0, 0, 0)
-        else:
-            bufs = (torch.empty(max(n_, 1), dtype=torch.int32, device=dev),
-                    torch.empty(max(n_, 1), dtype=torch.float64, device=dev),
-                    torch.empty((max(n_, 1), 3), dtype=torch.float64, device=dev))
-            outs = tuple(b_.data_ptr() for b_ in bufs)
+        outs, bufs = [], []
+        for _ in range(C):
+            if args.no_per_point:
+                outs.append((0, 0, 0))
+            else:
+                b_ = (torch.empty(max(n_, 1), dtype=torch.int32, device=dev),
+                      torch.empty(max(n_, 1), dtype=torch.float64, device=dev),
+                      torch.empty((max(n_, 1), 3), dtype=torch.float64, device=dev))
+                bufs.append(b_)
+                outs.append(tuple(x.data_ptr() for x in b_))
 
-        # W > 1: two accumulators and an asynchronous all-reduce — step i+1's
-        # pass runs while step i's collective is in flight (flash/distributed.py);
-        # a buffer is reused only after its previous collective completed
-        pending = [None, None]
+        # step i: context i % C, its accumulator (i // C) & 1, configuration
+        # (i // C) & 1. W > 1: an asynchronous all-reduce ordered after the
+        # context's stream — step i+1's pass runs while step i's collective is
+        # in flight (flash/distributed.py); a buffer is reused only after its
+        # previous collective completed
+        pending = [[None, None] for _ in range(C)]
 
         def step(i):
-            s_ = i & 1
-            if pending[s_] is not None:
-                pending[s_].wait()
-            ctx.eval_device(poses[s_], accums[s_].data_ptr(), *outs)
-            pending[s_] = allreduce_accum(accums[s_], async_op=True)
+            c, s_ = i % C, (i // C) & 1
+            with torch.cuda.stream(streams[c]):
+                if pending[c][s_] is not None:
+                    pending[c][s_].wait()
+                ctxs[c].eval_device(poses[s_], accums[c][s_].data_ptr(), *outs[c])
+                pending[c][s_] = allreduce_accum(accums[c][s_], async_op=True)
 
         def drain():
-            for s_ in (0, 1):
-                if pending[s_] is not None:
-                    pending[s_].wait()
-                    pending[s_] = None
+            for c in range(C):
+                for s_ in (0, 1):
+                    if pending[c][s_] is not None:
+                        with torch.cuda.stream(streams[c]):
+                            pending[c][s_].wait()
+                        pending[c][s_] = None
+
+        def join():  # the default stream waits for every context's stream
+            for st in streams[1:]:
+                stream.wait_stream(st)
 
         # settle: untimed passes (no collectives: the ranks' counts differ) until
         # the clocks have ramped, wall-clock bound
         t_settle = time.perf_counter()
         i = 0
         while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
-            ctx.eval_device(poses[i & 1], accums[i & 1].data_ptr(), *outs)
+            c = i % C
+            ctxs[c].eval_device(poses[(i // C) & 1], accums[c][(i // C) & 1].data_ptr(), *outs[c])
             i += 1
             if i % 16 == 0:
                 torch.cuda.synchronize()
@@ -267,7 +297,8 @@ def main():
             step(i)
         drain()
         torch.cuda.synchronize()
-        ctx.profile_pass(True)
+        for cx in ctxs:
+            cx.profile_pass(True)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         if world > 1:
             dist.barrier()
@@ -277,25 +308,48 @@ def main():
         for i in range(args.steps):
             step(i)
         drain()
+        join()
         ev1.record(stream)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-        kernel_ms, pass_ms, launches = ctx.pass_times()
-        ctx.profile_pass(False)
+        kernel_ms = pass_ms = 0.0
+        launches = 0
+        for cx in ctxs:
+            k_, p_, l_ = cx.pass_times()
+            kernel_ms, pass_ms, launches = kernel_ms + k_, pass_ms + p_, launches + l_
+            cx.profile_pass(False)
         elapsed_ = max(wall, ev0.elapsed_time(ev1) / 1e3)
         t = torch.tensor([elapsed_, pass_ms / max(launches, 1), kernel_ms / max(launches, 1),
                           float(np.median(set_ms))], dtype=torch.float64, device=dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        # sanity: the last pass is finite and non-trivial
-        acc = accums[(args.steps - 1) & 1].cpu().numpy()
+        # sanity: the last pass is finite and non-trivial; every context's
+        # accumulators equal context 0's (the same configurations)
+        acc = accums[0][0].cpu().numpy()
         assert np.isfinite(acc).all() and acc[0] > 0
+        if args.steps >= 2 * C:
+            for c in range(1, C):
+                for s_ in (0, 1):
+                    assert torch.equal(accums[c][s_], accums[0][s_]), "in-flight contexts disagree"
         return float(t[0]), float(t[1]), float(t[2]), float(t[3])
+
+    def serial_step_ms():
+        """One context, one pass at a time (no collective): the step's latency."""
+        outs0 = (0, 0, 0)
+        for i in range(3):
+            ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs0)
+        torch.cuda.synchronize()
+        t_s = time.perf_counter()
+        for i in range(args.steps):
+            ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs0)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t_s) / args.steps * 1e3
 
     n = len(pts)
     elapsed, pass_avg_ms, kernel_avg_ms, set_points_ms = run_cloud(pts)
+    serial_ms = serial_step_ms()
 
     allreduce_ms = dependent_ms = None
     if world > 1:
@@ -401,6 +455,13 @@ def main():
                 "allreduce_ms": allreduce_ms,
                 "allreduce_overlap": ("asynchronous all-reduce, two accumulators: step i+1's pass overlaps step "
                                       "i's collective" if world > 1 else None),
+                "inflight": C,
+                "inflight_note": (f"{C} independent passes in flight: {C} contexts over the same resident cloud, each on "
+                                  f"its own HIP stream, step i on context i % {C} (two configurations alternate); every "
+                                  f"context's accumulators checked equal" if C > 1 else "one pass at a time"),
+                "serial_step_ms": serial_ms,
+                "serial_step_note": "one context, one pass at a time, no collective, no per-point outputs: the "
+                                    "latency of one pass (pose + pass + reduce)",
                 "dependent_step_ms": dependent_ms,
                 "dependent_step_note": ("pass + all-reduce + host read-back per step, no overlap (a track! "
                                         "iteration's latency; no per-point outputs)" if world > 1 else None),
@@ -416,6 +477,11 @@ def main():
                 "bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": hbm_achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": ran, "kernel_ms": kernel_avg_ms,
+                # (with passes in flight a launch shares the GPU with its neighbour: its
+                # duration is longer than alone, so `achieved` per launch understates the
+                # device's rate; the aggregate is the algorithmic bytes of all timed
+                # launches over the timed region)
+                "achieved_aggregate": bytes_per_launch * args.steps / elapsed / 1e9,
                 "pass_and_reduce_ms": pass_avg_ms,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "valu_issue_frac": issue,

@@ -82,11 +82,13 @@ class Manipulator:
         return [s for s in self.surfaces if isinstance(s, ConvexGeometry)]
 
     def engine(self, device: int = 0, precision: int = 64, cull: bool = True,
-               sort_points: bool = True) -> "_lib.Context":
+               sort_points: bool = True, slot: int = 0) -> "_lib.Context":
         """The native context holding this model on `device` (created once).
         sort_points: the resident cloud is Hilbert-ordered on the device once per
-        frame (set_points); outputs still come back in caller order."""
-        key = (device, precision, cull, sort_points)
+        frame (set_points); outputs still come back in caller order. slot: further
+        independent contexts of the same model (each its own cloud copy, stream
+        and buffers — passes over independent states in flight together)."""
+        key = (device, precision, cull, sort_points, slot)
         ctx = self._engines.get(key)
         if ctx is None:
             ctx = _lib.Context(device=device, precision=precision, cull=cull, sort_points=sort_points)

@@ -29,7 +29,7 @@ def main():
     for r in range(rounds):
         for lib in libs:
             env = dict(os.environ, FLASHSDF_LIB=os.path.abspath(lib))
-            cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--steps", "30",
+            cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--inflight", "1", "--steps", "30",
                    "--warmup", "5"] + extra
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
             line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

@@ -146,6 +146,10 @@ for r in csv.DictReader(open(f)):
 import json
 for l in open('$O/hpart_sweep_$N.jsonl'):
     d = json.loads(l); print(d['points'], d['tier'], d['shares'], round(d['step_ms'], 4), round(d['pass_kernel_ms'], 4), d['default_parts'])" ;;
+    inflight:*)
+      S=${step#inflight:}
+      timeout -k 10 300 python tools/inflight_probe.py --sizes $S > $O/inflight.jsonl 2> $O/inflight.err || { echo INFLIGHT FAILED; tail $O/inflight.err; exit 1; }
+      cat $O/inflight.jsonl ;;
     c5sweep)
       timeout -k 10 300 python tools/precision_sweep.py --json $O/c5_sweep.json > $O/c5_sweep.log 2>&1 \
         || { echo C5 SWEEP FAILED; tail $O/c5_sweep.log; exit 1; }

@@ -12,8 +12,9 @@ cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/prof
 mkdir -p $OUT
-# the timed bench passes only (the full-iteration passes write no per-point outputs)
-ARGS="$R/bench.py --steps $STEPS --warmup 3 --no-cpu-baseline --no-full-iteration"
+# the timed bench passes only (the full-iteration passes write no per-point outputs), one pass at a time
+# (--inflight 1): each launch alone on the device, so its duration is the kernel's own
+ARGS="$R/bench.py --steps $STEPS --warmup 3 --no-cpu-baseline --no-full-iteration --inflight 1"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_trace -o run -- python3 $ARGS > $OUT/${TAG}_trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/${TAG}_fetch -o run -- python3 $ARGS > $OUT/${TAG}_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/${TAG}_write -o run -- python3 $ARGS > $OUT/${TAG}_write.log 2>&1

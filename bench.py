@@ -59,6 +59,8 @@ FP32_VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md
 SIMDS, CLOCK_HZ, CYCLES_PER_WAVE_OP = 1024, 2.4e9, 2   # MI355X_MICROARCH.md §Wave scheduling
 ITERS_PER_FRAME = 30           # src/tracking.jl:10-13 default NaiveSolver iteration_limit (manipulator.ipynb: 30)
 
+SERIAL = {}  # run_cloud's serial re-run of the timed passes (one at a time)
+
 CONFIGS = {
     # name: (model, default points, scaling, description)
     "m64": ("arm_grid", 1 << 20, "strong",
@@ -292,6 +294,20 @@ def main():
             i += 1
             if i % 16 == 0:
                 torch.cuda.synchronize()
+        # K passes one at a time on context 0 (no collective), right after the
+        # settle: the kernel's own launch duration (the roofline's, as rocprofv3
+        # sees it in tools/rocprof_round.sh) and one step's latency
+        torch.cuda.synchronize()
+        ctx.profile_pass(True)
+        t_s = time.perf_counter()
+        for i in range(args.steps):
+            ctx.eval_device(poses[i & 1], accums[0][i & 1].data_ptr(), *outs[0])
+        torch.cuda.synchronize()
+        serial_step = (time.perf_counter() - t_s) / args.steps * 1e3
+        k_, p_, l_ = ctx.pass_times()
+        ctx.profile_pass(False)
+        global SERIAL
+        SERIAL = {"step_ms": serial_step, "kernel_ms": k_ / max(l_, 1), "pass_and_reduce_ms": p_ / max(l_, 1)}
         torch.cuda.synchronize()
         for i in range(args.warmup):
             step(i)
@@ -335,21 +351,13 @@ def main():
                     assert torch.equal(accums[c][s_], accums[0][s_]), "in-flight contexts disagree"
         return float(t[0]), float(t[1]), float(t[2]), float(t[3])
 
-    def serial_step_ms():
-        """One context, one pass at a time (no collective): the step's latency."""
-        outs0 = (0, 0, 0)
-        for i in range(3):
-            ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs0)
-        torch.cuda.synchronize()
-        t_s = time.perf_counter()
-        for i in range(args.steps):
-            ctx.eval_device(poses[i & 1], accum.data_ptr(), *outs0)
-        torch.cuda.synchronize()
-        return (time.perf_counter() - t_s) / args.steps * 1e3
-
     n = len(pts)
-    elapsed, pass_avg_ms, kernel_avg_ms, set_points_ms = run_cloud(pts)
-    serial_ms = serial_step_ms()
+    elapsed, inflight_pass_ms, inflight_kernel_ms, set_points_ms = run_cloud(pts)
+    serial = dict(SERIAL)
+    # the roofline prices the kernel alone on the device (its serial launches,
+    # measured above with HIP events on its stream); with passes in flight each
+    # launch shares the device with its neighbour and lasts longer
+    kernel_avg_ms, pass_avg_ms = serial["kernel_ms"], serial["pass_and_reduce_ms"]
 
     allreduce_ms = dependent_ms = None
     if world > 1:
@@ -459,9 +467,9 @@ def main():
                 "inflight_note": (f"{C} independent passes in flight: {C} contexts over the same resident cloud, each on "
                                   f"its own HIP stream, step i on context i % {C} (two configurations alternate); every "
                                   f"context's accumulators checked equal" if C > 1 else "one pass at a time"),
-                "serial_step_ms": serial_ms,
-                "serial_step_note": "one context, one pass at a time, no collective, no per-point outputs: the "
-                                    "latency of one pass (pose + pass + reduce)",
+                "serial_step_ms": serial["step_ms"],
+                "serial_step_note": "K passes one at a time on one context, untimed, before the timed region (no "
+                                    "collective, per-point outputs written): one pass's latency",
                 "dependent_step_ms": dependent_ms,
                 "dependent_step_note": ("pass + all-reduce + host read-back per step, no overlap (a track! "
                                         "iteration's latency; no per-point outputs)" if world > 1 else None),
@@ -477,10 +485,12 @@ def main():
                 "bound": "hbm", "achieved": hbm_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": hbm_achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": ran, "kernel_ms": kernel_avg_ms,
-                # (with passes in flight a launch shares the GPU with its neighbour: its
-                # duration is longer than alone, so `achieved` per launch understates the
-                # device's rate; the aggregate is the algorithmic bytes of all timed
-                # launches over the timed region)
+                "kernel_ms_source": ("HIP events on the kernel's stream, K passes one at a time between the settle "
+                                     "and the timed region (the kernel alone on the device, as in the committed "
+                                     "rocprofv3 summary)"),
+                # with passes in flight a launch shares the device with its neighbour
+                "kernel_ms_inflight": inflight_kernel_ms,
+                # algorithmic bytes of all timed launches / the timed region
                 "achieved_aggregate": bytes_per_launch * args.steps / elapsed / 1e9,
                 "pass_and_reduce_ms": pass_avg_ms,
                 "algorithmic_bytes_per_launch": bytes_per_launch,

@@ -452,3 +452,44 @@ def test_planned_pass_follows_cloud_changes(m64, ctx_factory):
             assert c == want[0] and np.array_equal(a, want[1])
             for x, y in zip(pp, want[2]):
                 assert np.array_equal(x, y)
+
+
+def test_passes_in_flight_bit_identical(m64, ctx_factory):
+    """Independent passes in flight (bench.py --inflight): two
+    contexts over the same resident cloud on two non-null HIP streams, passes
+    interleaved without synchronisation — every accumulator and per-point output
+    equals a serial context's bit for bit (planned window and 2^20 unplanned)."""
+    import torch
+    import flash
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(m64, 808)
+    poses = [flash.hull_poses(m64, qe), flash.hull_poses(m64, qe + 1e-3)]
+    dev = torch.device("cuda", 0)
+    for n in (200000, 1 << 20):
+        pts = synthetic.depth_cloud(m64, qt, n, seed=809, order="shuffled")
+        serial = ctx_factory(m64, sort_points=True)
+        serial.set_points(pts)
+        want = [serial.eval(p, per_point=True) for p in poses]
+        d_pts = torch.as_tensor(pts, device=dev)
+        streams = [torch.cuda.Stream(dev) for _ in range(2)]
+        ctxs, accs, outs = [], [], []
+        for c in range(2):
+            cx = ctx_factory(m64, sort_points=True)
+            cx.set_stream(streams[c].cuda_stream)
+            cx.set_points_device(d_pts.data_ptr(), n)
+            ctxs.append(cx)
+            accs.append([torch.zeros(cx.accum_len, dtype=torch.float64, device=dev) for _ in range(2)])
+            outs.append([(torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.float64, device=dev),
+                          torch.empty((n, 3), dtype=torch.float64, device=dev)) for _ in range(2)])
+        torch.cuda.synchronize()
+        for i in range(24):  # first passes, then planned; never synchronised in between
+            c, s = i % 2, (i // 2) & 1
+            ctxs[c].eval_device(poses[s], accs[c][s].data_ptr(), *(b.data_ptr() for b in outs[c][s]))
+        torch.cuda.synchronize()
+        for c in range(2):
+            for s in (0, 1):  # (per-point outputs in caller order, the default)
+                assert np.array_equal(accs[c][s].cpu().numpy(), want[s][1])
+                k, d, g = (b.cpu().numpy() for b in outs[c][s])
+                assert np.array_equal(k, want[s][2][0]) and np.array_equal(d, want[s][2][1])
+                assert np.array_equal(g, want[s][2][2])
+        del d_pts

@@ -24,6 +24,7 @@
 #   rehearse        bench.py N=2 on one GPU (gloo, both ranks on device 0)
 #   hsweep:MODEL:SIZES[:EXTRA]  partition tiers / planned pass against cloud size (tools/hpart_sweep.py; MODEL
 #                   irb140 | arm_grid, SIZES and EXTRA arguments comma-separated) -> hpart_sweep_MODEL*.jsonl
+#   inflight:SIZES[:EXTRA]  independent passes in flight (tools/inflight_probe.py)  -> inflight.jsonl
 #   c5sweep         BASELINE C5 precision sweep on the reference cloud (tools/precision_sweep.py) -> c5_sweep.json
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -147,8 +148,10 @@ import json
 for l in open('$O/hpart_sweep_$N.jsonl'):
     d = json.loads(l); print(d['points'], d['tier'], d['shares'], round(d['step_ms'], 4), round(d['pass_kernel_ms'], 4), d['default_parts'])" ;;
     inflight:*)
-      S=${step#inflight:}
-      timeout -k 10 300 python tools/inflight_probe.py --sizes $S > $O/inflight.jsonl 2> $O/inflight.err || { echo INFLIGHT FAILED; tail $O/inflight.err; exit 1; }
+      # inflight:SIZES[:EXTRA] — tools/inflight_probe.py (EXTRA: more arguments, commas = spaces)
+      R=${step#inflight:}; S=${R%%:*}; X=""; [ "$R" != "$S" ] && X=${R#*:}; X=${X//,/ }
+      timeout -k 10 300 python tools/inflight_probe.py --sizes $S $X >> $O/inflight.jsonl 2>> $O/inflight.err \
+        || { echo INFLIGHT FAILED; tail $O/inflight.err; exit 1; }
       cat $O/inflight.jsonl ;;
     c5sweep)
       timeout -k 10 300 python tools/precision_sweep.py --json $O/c5_sweep.json > $O/c5_sweep.log 2>&1 \

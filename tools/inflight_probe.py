@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--sizes", default="131072,262144,524288,1048576")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--plan-max", type=int, default=-1, help="fsdf_set_plan max_points (-1: the default window)")
+    ap.add_argument("--counts", default="1,2,3", help="contexts in flight to measure (commas or +)")
     a = ap.parse_args()
     import torch
     import flash
@@ -35,15 +37,16 @@ def main():
     for n in (int(s) for s in a.sizes.split(",")):
         pts = synthetic.depth_cloud(m, qt, n, seed=a.seed + 17, order="shuffled")
         d_pts = torch.as_tensor(pts, device=dev)
-        res = {"points": n}
+        res = {"points": n, "plan_max": a.plan_max}
         ref = None
-        for C in (1, 2, 3):
+        for C in (int(c) for c in a.counts.replace("+", ",").split(",")):
             streams = [torch.cuda.Stream(dev) for _ in range(C)]
             ctxs, accs, outs = [], [], []
             for c in range(C):
                 ctx = _lib.Context(device=0, precision=64, cull=True, sort_points=True)
                 ctx.set_surfaces([("hull", (s_.hull.vertices, s_.hull.faces, s_.hull.planes)) for s_ in m.surfaces])
                 ctx.set_output_order(True)
+                ctx.set_plan(True, -1, -1, a.plan_max)
                 ctx.set_stream(streams[c].cuda_stream)
                 ctx.set_points_device(d_pts.data_ptr(), n)
                 ctxs.append(ctx)

@@ -59,12 +59,16 @@ class ShardedCostFunctor:
 
     def __init__(self, manipulator: Manipulator, local_points, rank: int = 0, world: int = 1, device: int = 0,
                  precision: int = 64, group=None, deformation_cost_weight=default_deformation_cost_weight,
-                 engine=None):
+                 engine=None, inflight: int = 1):
         """engine: an already-built context-like object to drive instead of
         manipulator.engine(device, precision) — with engine.device_type == "cpu"
         the accumulator lives in host memory and no HIP stream is used (the CPU
         gloo tests drive this class's sharding / all-reduce / read-back / chain
-        rule through a stand-in engine; the product engine is the HIP context)."""
+        rule through a stand-in engine; the product engine is the HIP context).
+        inflight = 2 (HIP contexts only): a second context over the shard on a
+        stream of its own (manipulator.engine(..., slot=1)) takes every other
+        launch, so value_and_gradient_many's consecutive passes run together
+        (INTEGRATION.md; bit-identical)."""
         import contextlib
         import torch
         self.torch = torch
@@ -88,20 +92,33 @@ class ShardedCostFunctor:
         self.h_accum = torch.empty(self.ctx.accum_len, dtype=torch.float64, pin_memory=not on_host)
         if on_host:
             self.stream = None
-            self._on_stream = contextlib.nullcontext
-            self._sync = lambda: None
+            self._on_stream = lambda slot=0: contextlib.nullcontext()
+            self._sync = lambda slot=0: None
+            self.ctxs, self.streams = [self.ctx], [None]
         else:
-            self.stream = torch.cuda.current_stream(self.dev)
+            two = inflight > 1 and engine is None
+            # (in flight: both contexts on streams of their own — HIP's null stream,
+            # torch's default, would serialise their passes)
+            self.stream = torch.cuda.Stream(self.dev) if two else torch.cuda.current_stream(self.dev)
             self.ctx.set_stream(self.stream.cuda_stream)
-            self._on_stream = lambda: torch.cuda.stream(self.stream)
-            self._sync = self.stream.synchronize
+            self.ctxs, self.streams = [self.ctx], [self.stream]
+            if two:
+                c2 = manipulator.engine(device, precision, slot=1)
+                s2 = torch.cuda.Stream(self.dev)
+                c2.set_stream(s2.cuda_stream)
+                c2.set_points_device(pts.data_ptr(), pts.shape[0])
+                self.ctxs.append(c2)
+                self.streams.append(s2)
+            self._on_stream = lambda slot=0: torch.cuda.stream(self.streams[slot % len(self.streams)])
+            self._sync = lambda slot=0: self.streams[slot % len(self.streams)].synchronize()
         # native iterations (fsdf_eval_state_device + fsdf_state_gradient: FK,
         # RBF solve, poses, pass; chain rule after the all-reduce)
         self._native = native_capable(manipulator) and getattr(self.ctx, "native_iterations", True)
 
-    def _ensure_native(self):
-        if getattr(self.ctx, "_mechanism_of", None) != (self.manipulator, self.weight):
-            register_native(self.manipulator, self.ctx, self.weight)
+    def _ensure_native(self, ctx=None):
+        ctx = self.ctx if ctx is None else ctx
+        if getattr(ctx, "_mechanism_of", None) != (self.manipulator, self.weight):
+            register_native(self.manipulator, ctx, self.weight)
 
     def launch(self, x, slot=None):
         """Enqueue one residual pass into accumulator `slot` (default: the
@@ -111,16 +128,17 @@ class ShardedCostFunctor:
             slot = self._slot ^ 1
         self._slot = slot
         acc = self.accums[slot]
-        with self._on_stream():
+        ctx = self.ctxs[slot % len(self.ctxs)]  # (inflight: slot 1's passes on the second context)
+        with self._on_stream(slot):
             if self._native:
-                self._ensure_native()
-                self.ctx.eval_state_device(np.asarray(x, np.float64), acc.data_ptr())
+                self._ensure_native(ctx)
+                ctx.eval_state_device(np.asarray(x, np.float64), acc.data_ptr())
             else:
                 unflatten(self.state, x)
                 normalize(self.state)
-                poses, self._solves = prepare_pass(self.ctx, self.manipulator, self.state.q,
+                poses, self._solves = prepare_pass(ctx, self.manipulator, self.state.q,
                                                    self.state.deformation_data)
-                self.ctx.eval_device(poses, acc.data_ptr())
+                ctx.eval_device(poses, acc.data_ptr())
             work = allreduce_accum(acc, self.group, async_op=True)
         self.accum = acc
         return slot, work
@@ -131,15 +149,16 @@ class ShardedCostFunctor:
         this copy only."""
         slot, work = pending
         out = self.h_accum if out is None else out
-        with self._on_stream():
+        with self._on_stream(slot):
             if work is not None:
                 work.wait()  # RCCL: the stream waits for the collective; gloo: the host does
             out.copy_(self.accums[slot], non_blocking=True)
-            self._sync()
+            self._sync(slot)
         return out.numpy()
 
     def _gradient(self, x, acc, solves):
         if self._native:
+            self._ensure_native()
             return self.ctx.state_gradient(x, acc)  # (re-prepares x's FK / solve if a later pass was enqueued)
         unflatten(self.state, x)  # the state of THIS x (a pipelined later launch moved it)
         normalize(self.state)

@@ -195,3 +195,32 @@ def test_set_surfaces_drops_the_mechanism():
     assert "mechanism" in str(e.value)
     with pytest.raises(ValueError):
         ctx.value_and_gradient(np.zeros(3))  # short x is refused before the C call
+
+
+@pytest.mark.parametrize("name", ["arm_grid", "c5_scene"])
+def test_sharded_functor_inflight_same_bits(name):
+    """ShardedCostFunctor(inflight=2): every other launch on a second context
+    over the shard, on a stream of its own, so value_and_gradient_many's
+    consecutive passes run together — the same bits as one pass at a time
+    (one rank, no collective; rigid M64 at a planned-window size and the RBF
+    C5 scene)."""
+    from flash import Models, synthetic
+    from flash.distributed import ShardedCostFunctor
+    if name == "c5_scene":
+        m = _rbf_scene(name)
+        import os
+        from conftest import GOLDEN
+        z = np.load(os.path.join(GOLDEN, name + ".npz"))
+        pts, x0 = z["points"], np.asarray(z["x"], np.float64)
+    else:
+        m = getattr(Models, name)()
+        qt, x0 = synthetic.perturbed_configuration(m, 31)
+        pts = synthetic.depth_cloud(m, qt, 150000, seed=32)
+    xs = [x0 + 1e-3 * i for i in range(6)]
+    one = ShardedCostFunctor(m, pts)
+    want = [one.value_and_gradient(x) for x in xs]
+    two = ShardedCostFunctor(m, pts, inflight=2)
+    assert len(two.ctxs) == 2
+    got = two.value_and_gradient_many(xs)
+    for (c0, g0), (c1, g1) in zip(want, got):
+        assert c1 == c0 and np.array_equal(g1, g0)

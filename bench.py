@@ -9,7 +9,11 @@ A step is ONE residual pass of the hot path over the resident cloud: the pose
 kernel (the 12·S pose doubles ride in its arguments), the pass kernel (per
 point: nearest hull d*, k*, ∇d* written to HBM + the cost/wrench partial sums),
 the fixed-order reduce kernel and, for N > 1, the RCCL all-reduce of the
-1+6S-double accumulator.
+1+6S-double accumulator. Steps run one pass at a time (the
+headline `value`), as a track! iteration does; at N = 1 the line also carries
+the dependent step (pass + accumulator read-back + host wait, every step) and,
+labelled as such, the aggregate of two independent passes in flight
+(config.inflight_throughput).
 
 Sharding (contiguous ⌈N/W⌉ point ranges, uploaded once per frame):
   (default)           strong scaling of the metric's cloud: ONE 2^20-point M64
@@ -60,6 +64,7 @@ SIMDS, CLOCK_HZ, CYCLES_PER_WAVE_OP = 1024, 2.4e9, 2   # MI355X_MICROARCH.md §W
 ITERS_PER_FRAME = 30           # src/tracking.jl:10-13 default NaiveSolver iteration_limit (manipulator.ipynb: 30)
 
 SERIAL = {}  # run_cloud's serial re-run of the timed passes (one at a time)
+SIDE_RES = {}  # run_cloud's N = 1 side figures (dependent step, passes in flight)
 
 CONFIGS = {
     # name: (model, default points, scaling, description)
@@ -80,10 +85,15 @@ def parse():
                    help="untimed passes for this long before the W warmup steps: the GPU's clocks ramp up over "
                         "the first tens of ms of load (2^20 pass kernel 0.103 ms after 5 passes, 0.093 after 300, "
                         "profiles/r04/warmup_ab.txt)")
-    p.add_argument("--inflight", type=int, default=2,
-                   help="independent passes in flight: C contexts over the same resident cloud, each on its own HIP "
-                        "stream, step i on context i %% C (each context's results bit-identical to serial steps; "
-                        "profiles/r04/inflight.jsonl). 1 = one pass at a time")
+    p.add_argument("--inflight", type=int, default=1,
+                   help="passes in flight in the timed region: C contexts over the same resident cloud, each on its "
+                        "own HIP stream, step i on context i %% C (each context's results bit-identical to serial "
+                        "steps; profiles/r04/inflight.jsonl). Default 1: one pass at a time, as a track! iteration "
+                        "runs (each iteration needs the gradient of the one before)")
+    p.add_argument("--inflight-side", type=int, default=2,
+                   help="N = 1: after the timed region, also measure the aggregate throughput of this many "
+                        "independent passes in flight (config.inflight_throughput; 0 = skip). Not the headline: "
+                        "only independent configurations (line-search trials, several hypotheses) can overlap")
     p.add_argument("--config", default="m64", choices=sorted(CONFIGS))
     g = p.add_mutually_exclusive_group()
     g.add_argument("--points", type=int, default=None, help="points per GPU (weak scaling)")
@@ -213,13 +223,15 @@ def main():
     poses = [flash.hull_poses(manip, q_eval), flash.hull_poses(manip, q_alt)]
 
     C = max(1, args.inflight)
+    SIDE = args.inflight_side if (world == 1 and args.inflight_side > 1) else 0
+    CS = max(C, SIDE)  # contexts: the timed region uses the first C, the in-flight side figure the first SIDE
     ctxs = [manip.engine(device=local, precision=args.precision, cull=not args.no_cull,
-                         sort_points=not args.no_sort, slot=c) for c in range(C)]
+                         sort_points=not args.no_sort, slot=c) for c in range(CS)]
     # every context on a stream of its own, none of them HIP's null stream (whose
     # implicit synchronisation would serialise the passes in flight); the first
     # is made torch's current stream, so the collectives and timing events order
     # after it
-    streams = [torch.cuda.Stream(dev) for _ in range(C)]
+    streams = [torch.cuda.Stream(dev) for _ in range(CS)]
     torch.cuda.set_stream(streams[0])
     stream = streams[0]
     for c, cx in enumerate(ctxs):
@@ -227,7 +239,8 @@ def main():
         cx.set_stream(streams[c].cuda_stream)
     ctx = ctxs[0]
     # two accumulators per context (the all-reduce of one overlaps the next pass)
-    accums = [[torch.zeros(ctx.accum_len, dtype=torch.float64, device=dev) for _ in range(2)] for _ in range(C)]
+    accums = [[torch.zeros(ctx.accum_len, dtype=torch.float64, device=dev) for _ in range(2)] for _ in range(CS)]
+    h_acc = torch.empty(ctx.accum_len, dtype=torch.float64, pin_memory=True)
     accum = accums[0][0]
 
     def run_cloud(pts_host):
@@ -236,18 +249,18 @@ def main():
         (elapsed s, whole-pass ms, pass-kernel ms, set_points ms)."""
         d_pts = torch.as_tensor(pts_host, device=dev)
         torch.cuda.synchronize()
-        for cx in ctxs:
+        for cx in ctxs:  # (every context, the side figure's too)
             cx.set_points_device(d_pts.data_ptr(), len(pts_host))  # first upload (allocations)
         set_ms = []
-        for _ in range(3):  # once per frame: copy (+ Hilbert sort), every context
+        for _ in range(3):  # once per frame: copy (+ Hilbert sort), every context of the timed region
             t_set = time.perf_counter()
-            for cx in ctxs:
+            for cx in ctxs[:C]:
                 cx.set_points_device(d_pts.data_ptr(), len(pts_host))
             set_ms.append((time.perf_counter() - t_set) * 1e3)
         del d_pts
         n_ = len(pts_host)
         outs, bufs = [], []
-        for _ in range(C):
+        for _ in range(CS):
             if args.no_per_point:
                 outs.append((0, 0, 0))
             else:
@@ -262,10 +275,10 @@ def main():
         # context's stream — step i+1's pass runs while step i's collective is
         # in flight (flash/distributed.py); a buffer is reused only after its
         # previous collective completed
-        pending = [[None, None] for _ in range(C)]
+        pending = [[None, None] for _ in range(CS)]
 
-        def step(i):
-            c, s_ = i % C, (i // C) & 1
+        def step(i, nctx=C):
+            c, s_ = i % nctx, (i // nctx) & 1
             with torch.cuda.stream(streams[c]):
                 if pending[c][s_] is not None:
                     pending[c][s_].wait()
@@ -273,15 +286,15 @@ def main():
                 pending[c][s_] = allreduce_accum(accums[c][s_], async_op=True)
 
         def drain():
-            for c in range(C):
+            for c in range(CS):
                 for s_ in (0, 1):
                     if pending[c][s_] is not None:
                         with torch.cuda.stream(streams[c]):
                             pending[c][s_].wait()
                         pending[c][s_] = None
 
-        def join():  # the default stream waits for every context's stream
-            for st in streams[1:]:
+        def join(nctx=C):  # the first context's stream waits for every other context's stream
+            for st in streams[1:nctx]:
                 stream.wait_stream(st)
 
         # settle: untimed passes (no collectives: the ranks' counts differ) until
@@ -337,6 +350,40 @@ def main():
             kernel_ms, pass_ms, launches = kernel_ms + k_, pass_ms + p_, launches + l_
             cx.profile_pass(False)
         elapsed_ = max(wall, ev0.elapsed_time(ev1) / 1e3)
+        # N = 1 side figures, after the timed region: (a) a dependent step — the
+        # pass, then the accumulator read back to pinned host memory and the host
+        # waits, every step (what a track! iteration pays besides its host FK and
+        # chain rule); (b) SIDE independent passes in flight (aggregate throughput)
+        global SIDE_RES
+        SIDE_RES = {}
+        if world == 1:
+            for i in range(3):
+                ctx.eval_device(poses[i & 1], accums[0][i & 1].data_ptr(), *outs[0])
+                h_acc.copy_(accums[0][i & 1], non_blocking=True)
+                stream.synchronize()
+            t_d = time.perf_counter()
+            for i in range(args.steps):
+                ctx.eval_device(poses[i & 1], accums[0][i & 1].data_ptr(), *outs[0])
+                h_acc.copy_(accums[0][i & 1], non_blocking=True)
+                stream.synchronize()
+            SIDE_RES["dependent_step_ms"] = (time.perf_counter() - t_d) / args.steps * 1e3
+        if SIDE > 1:
+            for i in range(4 * SIDE):
+                step(i, SIDE)
+            drain()
+            join(SIDE)
+            torch.cuda.synchronize()
+            t_f = time.perf_counter()
+            for i in range(args.steps):
+                step(i, SIDE)
+            drain()
+            join(SIDE)
+            torch.cuda.synchronize()
+            SIDE_RES["inflight_ms_per_pass"] = (time.perf_counter() - t_f) / args.steps * 1e3
+            if args.steps >= 2 * SIDE:
+                for c in range(1, SIDE):
+                    for s_ in (0, 1):
+                        assert torch.equal(accums[c][s_], accums[0][s_]), "in-flight contexts disagree"
         t = torch.tensor([elapsed_, pass_ms / max(launches, 1), kernel_ms / max(launches, 1),
                           float(np.median(set_ms))], dtype=torch.float64, device=dev)
         if world > 1:
@@ -352,14 +399,16 @@ def main():
         return float(t[0]), float(t[1]), float(t[2]), float(t[3])
 
     n = len(pts)
-    elapsed, inflight_pass_ms, inflight_kernel_ms, set_points_ms = run_cloud(pts)
+    elapsed, timed_pass_ms, timed_kernel_ms, set_points_ms = run_cloud(pts)
     serial = dict(SERIAL)
+    side = dict(SIDE_RES)
     # the roofline prices the kernel alone on the device (its serial launches,
     # measured above with HIP events on its stream); with passes in flight each
     # launch shares the device with its neighbour and lasts longer
     kernel_avg_ms, pass_avg_ms = serial["kernel_ms"], serial["pass_and_reduce_ms"]
 
-    allreduce_ms = dependent_ms = None
+    allreduce_ms = None
+    dependent_ms = side.get("dependent_step_ms")
     if world > 1:
         # a dependent iteration (track!: x_{k+1} needs the all-reduced accumulator
         # of x_k): pass, collective, host read-back, every step — the latency the
@@ -466,13 +515,24 @@ def main():
                 "inflight": C,
                 "inflight_note": (f"{C} independent passes in flight: {C} contexts over the same resident cloud, each on "
                                   f"its own HIP stream, step i on context i % {C} (two configurations alternate); every "
-                                  f"context's accumulators checked equal" if C > 1 else "one pass at a time"),
+                                  f"context's accumulators checked equal" if C > 1 else
+                                  "one pass at a time (the timed region), as a track! iteration runs"),
+                "inflight_throughput": ({"passes_in_flight": SIDE, "ms_per_pass": side["inflight_ms_per_pass"],
+                                         "value": global_points / (side["inflight_ms_per_pass"] / 1e3),
+                                         "note": f"NOT the headline: {SIDE} independent passes in flight on {SIDE} "
+                                                 "contexts / streams (two configurations alternating), measured after "
+                                                 "the timed region; only independent configurations can overlap, a "
+                                                 "dependent track! iteration cannot"}
+                                        if "inflight_ms_per_pass" in side else None),
                 "serial_step_ms": serial["step_ms"],
                 "serial_step_note": "K passes one at a time on one context, untimed, before the timed region (no "
                                     "collective, per-point outputs written): one pass's latency",
                 "dependent_step_ms": dependent_ms,
                 "dependent_step_note": ("pass + all-reduce + host read-back per step, no overlap (a track! "
-                                        "iteration's latency; no per-point outputs)" if world > 1 else None),
+                                        "iteration's latency; no per-point outputs)" if world > 1 else
+                                        "pass (per-point outputs written) + accumulator read back to pinned host "
+                                        "memory + host wait, every step (a track! iteration's device latency; its "
+                                        "host FK and chain rule are in full_iteration_ms)"),
                 "set_points_ms_per_frame": set_points_ms,
                 "frame_ms_at_30_iterations": frame_ms,
                 "frame_note": "set_points (H2D-resident copy + Hilbert sort) once + 30 residual passes",
@@ -488,8 +548,9 @@ def main():
                 "kernel_ms_source": ("HIP events on the kernel's stream, K passes one at a time between the settle "
                                      "and the timed region (the kernel alone on the device, as in the committed "
                                      "rocprofv3 summary)"),
-                # with passes in flight a launch shares the device with its neighbour
-                "kernel_ms_inflight": inflight_kernel_ms,
+                # the pass kernel's mean HIP-event time inside the timed region (= kernel_ms
+                # when passes run one at a time; longer with passes in flight)
+                "kernel_ms_timed_region": timed_kernel_ms,
                 # algorithmic bytes of all timed launches / the timed region
                 "achieved_aggregate": bytes_per_launch * args.steps / elapsed / 1e9,
                 "pass_and_reduce_ms": pass_avg_ms,

@@ -193,9 +193,11 @@ int fsdf_set_deformations(fsdf_ctx* ctx, int32_t n_deform, double weight);
  * the context's stream); after the caller's all-reduce (RCCL) and read-back,
  * fsdf_state_gradient(x, accum) returns cost and gradient as
  * fsdf_value_and_gradient does, on the FK / weight solve of that pass. x may
- * be an earlier pass's x (pipelined passes: the next pass is enqueued before
- * the previous all-reduce completes): the host FK and weight solve are then
- * redone for x — the same arithmetic, the same bits. */
+ * be the x of either of this context's last two fsdf_eval_state_device passes
+ * (pipelined passes: the next pass is enqueued before the previous all-reduce
+ * completes): the host FK and weight solve are then redone for x — the same
+ * arithmetic, the same bits. Any other x (not the configuration of an
+ * accumulator this context produced) is refused with FSDF_ERR_STATE. */
 int fsdf_eval_state_device(fsdf_ctx* ctx, const double* x, double* d_accum);
 int fsdf_state_gradient(fsdf_ctx* ctx, const double* x, const double* accum, double* cost_out, double* grad_out);
 
@@ -344,7 +346,10 @@ int fsdf_get_partition(fsdf_ctx* ctx, int64_t n, int64_t* four_way_max_out, int6
  * planned pass runs, -1 = the model's default window: more than 98,304 and
  * at most 524,288 points for models of >= 32 hulls, 393,216 for smaller ones
  * (outside it the unplanned grid measured faster); a value >= 0
- * runs it for every cloud of 1 .. max_points points. */
+ * runs it for every cloud of 1 .. max_points points. Memory: the per-chunk
+ * rows take (25 + 6 S) doubles per 64-point chunk per context (1.6 KB at
+ * S = 64: 13 MB for the default window's 524,288 points, 105 MB at the
+ * 4,194,304-point limit); a second context in flight holds its own. */
 int fsdf_set_plan(fsdf_ctx* ctx, int32_t enable, double four_way_share, double two_way_share, int64_t max_points);
 
 /* Diagnostics: the serial-equivalent durations (100 MHz ticks) the last

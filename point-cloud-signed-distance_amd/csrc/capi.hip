@@ -122,6 +122,7 @@ struct fsdf_ctx {
   // durations and the workgroup plan built from them (fsdf_set_plan)
   fsdf::ChunkOutputs co;             // device arrays, [co_cap] chunks
   int64_t co_cap = 0;
+  int co_s = 0;                      // surfaces the dense rows of co were sized for
   int32_t* d_plan = nullptr;         // [plan_cap][4]
   int32_t* d_plan_order = nullptr;   // [co_cap] plan_kernel scratch
   int64_t plan_cap = 0;
@@ -164,6 +165,11 @@ struct fsdf_ctx {
     int n_deform = 0;
     double weight = 10.0;  // default_deformation_cost_weight (src/gradientdescent.jl:7)
     std::vector<double> rows, body_wrench, x_prepared;
+    // the x of the last two fsdf_eval_state_device passes (their accumulators
+    // may still be in flight): fsdf_state_gradient accepts only these (or the
+    // last prepared x) and refuses any other with FSDF_ERR_STATE
+    std::vector<double> x_pass[2];
+    int x_pass_next = 0;
   } mech;
 };
 
@@ -839,7 +845,7 @@ static int release_posed(fsdf_ctx* c, int buf) {
 static constexpr int kOrderEvery = FSDF_ORDER_EVERY;
 
 static int ensure_chunk_outputs(fsdf_ctx* c, int64_t nc) {
-  if (c->co_cap >= nc) return FSDF_OK;
+  if (c->co_cap >= nc && c->co_s >= c->lm.S) return FSDF_OK;
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   dfree(c->co.hdr);
   dfree(c->co.ent);  // (csum and dense live in the same allocation)
@@ -849,8 +855,10 @@ static int ensure_chunk_outputs(fsdf_ctx* c, int64_t nc) {
   c->co_cap = 0;
   c->plan_nc = -1;
   HIPCHECK(c, hipMalloc(&c->co.hdr, (size_t)nc * 4 * sizeof(int32_t)));
-  // one allocation: entries [nc][24] | Σ d² [nc] | dense rows [nc][64][6]
-  HIPCHECK(c, hipMalloc(&c->co.ent, (size_t)nc * (24 + 1 + 64 * 6) * sizeof(double)));
+  // one allocation: entries [nc][24] | Σ d² [nc] | dense rows [nc][S][6] (sized by the surface count:
+  // (25 + 6 S) doubles per chunk, 1.6 KB at S = 64 — per context, so two in flight hold it twice)
+  HIPCHECK(c, hipMalloc(&c->co.ent, (size_t)nc * (24 + 1 + 6 * (size_t)c->lm.S) * sizeof(double)));
+  c->co_s = c->lm.S;
   c->co.csum = c->co.ent + (size_t)nc * 24;
   c->co.dense = c->co.ent + (size_t)nc * 25;
   c->co.cap = nc;
@@ -865,13 +873,18 @@ static int ensure_chunk_outputs(fsdf_ctx* c, int64_t nc) {
 // and at least as many chunks over 4 waves as the device's idle wave slots
 // allow (slots - nc, 3 extra waves per split chunk): a strong-scaling shard
 // that leaves slots free splits its heavy third, a full machine only its tail.
-static void plan_shape(fsdf_ctx* c, int64_t nc, int* n4, int* n2) {
+static int wave_slots(fsdf_ctx* c) {
   if (c->wave_slots == 0) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0)
       cus = 256;
     c->wave_slots = cus * 4 * 4;  // 4 SIMDs x 4 waves (the pass's register budget)
   }
+  return c->wave_slots;
+}
+
+static void plan_shape(fsdf_ctx* c, int64_t nc, int* n4, int* n2) {
+  wave_slots(c);
   const int64_t spare = std::max<int64_t>(0, (int64_t)c->wave_slots - nc);
   // default (shares < 0): fixed counts — the heavy tail that outlasts the rest
   // of a pass is ~100 chunks at 2^18 and at 2^19 points alike (measured)
@@ -1455,7 +1468,12 @@ extern "C" int fsdf_eval_state_device(fsdf_ctx* c, const double* x, double* d_ac
   if (!x || !d_accum) return fail(c, FSDF_ERR_ARG, "eval_state_device: null argument");
   int rc = iteration_prepare(c, x, "eval_state_device");
   if (rc) return rc;
-  return run_pass(c, c->mech.poses.data(), c->d_pts, c->n, d_accum, nullptr, nullptr, nullptr, nullptr, true);
+  rc = run_pass(c, c->mech.poses.data(), c->d_pts, c->n, d_accum, nullptr, nullptr, nullptr, nullptr, true);
+  if (rc) return rc;
+  auto& M = c->mech;
+  M.x_pass[M.x_pass_next] = M.x_prepared;
+  M.x_pass_next ^= 1;
+  return FSDF_OK;
 }
 
 extern "C" int fsdf_state_gradient(fsdf_ctx* c, const double* x, const double* accum, double* cost_out,
@@ -1468,7 +1486,17 @@ extern "C" int fsdf_state_gradient(fsdf_ctx* c, const double* x, const double* a
   // accum; for an x other than the last prepared one (a pipelined earlier
   // pass) that host part is redone — the same arithmetic, the same bits
   if (M.nb == 0) return fail(c, FSDF_ERR_STATE, "state_gradient: no mechanism (call fsdf_set_mechanism)");
-  if (M.x_prepared.size() != nx || memcmp(M.x_prepared.data(), x, nx * sizeof(double)) != 0) {
+  auto same = [&](const std::vector<double>& v) {
+    return v.size() == nx && memcmp(v.data(), x, nx * sizeof(double)) == 0;
+  };
+  if (!same(M.x_prepared)) {
+    // an earlier pass of the ring: its FK / weight solve is redone (the same
+    // arithmetic, the same bits); any other x cannot belong to an accumulator
+    // of this context
+    if (!same(M.x_pass[0]) && !same(M.x_pass[1]))
+      return fail(c, FSDF_ERR_STATE,
+                  "state_gradient: x is not the configuration of either of this context's last two "
+                  "eval_state_device passes (nor the last prepared one)");
     const int rc = iteration_prepare(c, x, "state_gradient", false);
     if (rc) return rc;
   }

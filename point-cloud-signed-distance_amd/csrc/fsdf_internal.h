@@ -145,11 +145,13 @@ struct ChunkOutputs {
   int32_t* hdr = nullptr;      // [nc][4] surfaces of entries 0..3 (-1: none); [c][0] == -2: dense row
   double* ent = nullptr;       // [nc][4][6] (F, M) of each entry
   double* csum = nullptr;      // [nc] Σ d² over the chunk's points
-  double* dense = nullptr;     // [nc][64][6] (F, M) per surface (chunks with > 4 surfaces)
+  double* dense = nullptr;     // [nc][S][6] (F, M) per surface (chunks with > 4 surfaces)
   uint32_t* dur = nullptr;     // [nc] serial-equivalent chunk durations (100 MHz ticks)
   const int32_t* plan = nullptr;  // [grid][4] workgroup plan (chunk | parts << 24, chunk, chunk, chunk), or null
   int dparts = 1;              // waves per chunk without a plan (4, 2 or 1)
-  int64_t cap = 0;             // chunks allocated: csum = ent + 24 cap, dense = ent + 25 cap (one allocation)
+  int64_t cap = 0;             // chunks allocated: csum = ent + 24 cap, dense = ent + 25 cap (one allocation
+                               // of (25 + 6 S) doubles per chunk: 1.6 KB per chunk at S = 64, i.e. 13 MB at
+                               // the default 524,288-point planned window, 105 MB at kMaxPlanChunks)
 };
 constexpr int kPlanPartsShift = 24;
 constexpr int64_t kMaxPlanChunks = 1 << 16;  // planned passes: clouds of <= 4,194,304 points per device

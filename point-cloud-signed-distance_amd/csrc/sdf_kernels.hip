@@ -1785,13 +1785,67 @@ __global__ __launch_bounds__(NB) __attribute__((
 //
 // Every chunk writes its OWN partial row — the chunk's Σ d², and its wrench
 // sums (F, M) per nearest surface as up to 4 (k, F, M) entries, or a dense
-// [64][6] row when more than 4 surfaces meet in the chunk — so the
+// [S][6] row when more than 4 surfaces meet in the chunk — so the
 // accumulator (reduce_chunks_kernel, one launch) sums the chunk rows in a
 // fixed order whatever the plan: bit-identical across plans, schedules and
 // passes. No block combine, no
 // barrier after the prologue for one-wave chunks.
 // ---------------------------------------------------------------------------
 constexpr int kPlanChunkMask = (1 << kPlanPartsShift) - 1;
+
+// One chunk's epilogue in the planned pass: the wave's wrench
+// rows (lane k owns surface k) in its free stage, the per-point outputs, and
+// the chunk's partial row — Σ d², then sparse (k, F, M) entries in ascending k
+// or, when more than 4 surfaces meet in the chunk, a dense [S][6] row.
+template <typename T>
+__device__ __forceinline__ void emit_chunk_row(T px, T py, T pz, bool valid, T best, int bk, T gx, T gy, T gz, int cid,
+                                               int64_t n, const PassModel<T>& m, const PassOutputs& out,
+                                               const ChunkOutputs& co, T* __restrict__ stage) {
+  const int lane = threadIdx.x & 63;
+  const int64_t base = (int64_t)cid * 64;
+  const int64_t i = base + lane;
+  double* acc_row = (double*)stage + lane * 6;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+  for (int j = 0; j < 6; ++j) acc_row[j] = 0.0;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  T* tstage = (T*)((char*)stage + (64 * 6 + 2) * 8);  // gradient transpose after the rows
+  double cost_chunk = 0.0;
+  const uint64_t touched = emit_chunk<T, 1, false>(px, py, pz, valid, best, bk, gx, gy, gz, i, base, n, m, out,
+                                                   acc_row, cost_chunk, nullptr, tstage,
+                                                   m.stage_bytes / (4 * (int)sizeof(T)));
+  cost_chunk = wave_sum(cost_chunk);
+  const int cnt = __builtin_popcountll(touched);
+  if (cnt <= 4) {
+    if ((touched >> lane) & 1) {
+      const int sl = __builtin_popcountll(touched & ((1ull << lane) - 1));
+      double* e = co.ent + ((int64_t)cid * 4 + sl) * 6;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) e[j] = acc_row[j];
+    }
+    if (lane == 0) {
+      I4 h = I4{-1, -1, -1, -1};
+      uint64_t t = touched;
+      for (int sl = 0; sl < 4 && t; ++sl) {
+        h[sl] = __builtin_ctzll(t);
+        t &= t - 1;
+      }
+      ((I4*)co.hdr)[cid] = h;
+      co.csum[cid] = cost_chunk;
+    }
+  } else {
+    if (lane < m.S) {
+      double* r = co.dense + ((int64_t)cid * m.S + lane) * 6;  // [nc][S][6]
+#pragma unroll
+      for (int j = 0; j < 6; ++j) r[j] = acc_row[j];
+    }
+    if (lane == 0) {
+      ((I4*)co.hdr)[cid] = I4{-2, -1, -1, -1};
+      co.csum[cid] = cost_chunk;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // row reads before the stage is overwritten
+}
 
 template <typename T, bool CULL>
 __global__ __launch_bounds__(kPassBlock) __attribute__((amdgpu_waves_per_eu(kPassWavesPerSimd))) void planned_pass_kernel(
@@ -1868,50 +1922,8 @@ __global__ __launch_bounds__(kPassBlock) __attribute__((amdgpu_waves_per_eu(kPas
   if (!has || part != 0) return;  // (no barrier follows)
   slot_of(parts, cid);
   base = (int64_t)cid * 64;
-  const int64_t i = base + lane;
   if (!valid) bk = 0;
-  // this wave's wrench rows (lane k owns surface k) live in its free stage
-  double* acc_row = (double*)stage + lane * 6;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-#pragma unroll
-  for (int j = 0; j < 6; ++j) acc_row[j] = 0.0;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  T* tstage = (T*)((char*)stage + (64 * 6 + 2) * 8);  // gradient transpose after the rows
-  double cost_chunk = 0.0;
-  const uint64_t touched = emit_chunk<T, 1, false>(px, py, pz, valid, best, bk, gx, gy, gz, i, base, n, m, out,
-                                                   acc_row, cost_chunk, nullptr, tstage,
-                                                   m.stage_bytes / (4 * (int)sizeof(T)));
-  cost_chunk = wave_sum(cost_chunk);
-  // the chunk's partial row: sparse entries in ascending k, or dense
-  const int cnt = __builtin_popcountll(touched);
-  if (cnt <= 4) {
-    if ((touched >> lane) & 1) {
-      const int sl = __builtin_popcountll(touched & ((1ull << lane) - 1));
-      double* e = co.ent + ((int64_t)cid * 4 + sl) * 6;
-#pragma unroll
-      for (int j = 0; j < 6; ++j) e[j] = acc_row[j];
-    }
-    if (lane == 0) {
-      I4 h = I4{-1, -1, -1, -1};
-      uint64_t t = touched;
-      for (int sl = 0; sl < 4 && t; ++sl) {
-        h[sl] = __builtin_ctzll(t);
-        t &= t - 1;
-      }
-      ((I4*)co.hdr)[cid] = h;
-      co.csum[cid] = cost_chunk;
-    }
-  } else {
-    if (lane < m.S) {
-      double* r = co.dense + ((int64_t)cid * 64 + lane) * 6;
-#pragma unroll
-      for (int j = 0; j < 6; ++j) r[j] = acc_row[j];
-    }
-    if (lane == 0) {
-      ((I4*)co.hdr)[cid] = I4{-2, -1, -1, -1};
-      co.csum[cid] = cost_chunk;
-    }
-  }
+  emit_chunk_row<T>(px, py, pz, valid, best, bk, gx, gy, gz, cid, n, m, out, co, stage);
   if (co.dur && lane == 0) {
     // serial-equivalent duration: a split chunk's wall time scaled by the
     // parallelism its split bought (measured ~2.5x at 4 waves, ~1.6x at 2)
@@ -1966,7 +1978,7 @@ __global__ __launch_bounds__(kGroupBlock) void chunk_groups_kernel(const I4* __r
   // dense rows (a chunk that met more than 4 surfaces): entry 1 + i = dense[i]
   for (int c = 0; c < kGroupChunks; ++c) {
     if (sh[c][0] == -2)
-      for (int i = tid; i < 6 * S; i += kGroupBlock) tab[c * len + 1 + i] = dense[(int64_t)(c0 + c) * 64 * 6 + i];
+      for (int i = tid; i < 6 * S; i += kGroupBlock) tab[c * len + 1 + i] = dense[(int64_t)(c0 + c) * 6 * S + i];
   }
   __syncthreads();
   for (int t = tid; t < len; t += kGroupBlock) {

@@ -89,7 +89,13 @@ class ShardedCostFunctor:
         # pinned read-back of the all-reduced accumulator (a pageable .cpu()
         # goes through the runtime's staging buffer: ~10 us per iteration on
         # the single-GPU path, profiles/r02/experiments/r02pin)
-        self.h_accum = torch.empty(self.ctx.accum_len, dtype=torch.float64, pin_memory=not on_host)
+        # (one per accumulator slot: value_and_gradient_many reads slot i's while slot i+1's pass runs)
+        self.h_accums = [torch.empty(self.ctx.accum_len, dtype=torch.float64, pin_memory=not on_host)
+                         for _ in range(2)]
+        self.h_accum = self.h_accums[0]
+        # the in-flight all-reduce of each accumulator slot: a slot is written
+        # again (next launch, per_point) only after its collective completed
+        self._pending = [None, None]
         if on_host:
             self.stream = None
             self._on_stream = lambda slot=0: contextlib.nullcontext()
@@ -120,13 +126,25 @@ class ShardedCostFunctor:
         if getattr(ctx, "_mechanism_of", None) != (self.manipulator, self.weight):
             register_native(self.manipulator, ctx, self.weight)
 
+    def _wait_slot(self, slot):
+        """Order the slot's stream (RCCL; gloo: the host) after the slot's
+        pending all-reduce, which may still read its accumulator."""
+        work = self._pending[slot]
+        if work is not None:
+            with self._on_stream(slot):
+                work.wait()
+            self._pending[slot] = None
+
     def launch(self, x, slot=None):
         """Enqueue one residual pass into accumulator `slot` (default: the
         other one than last time) and its all-reduce, asynchronously. Returns
-        (slot, work); `finish` turns it into the host accumulator."""
+        (slot, work); `finish` turns it into the host accumulator. A slot whose
+        previous all-reduce is still in flight is waited for first (its
+        accumulator is that collective's buffer)."""
         if slot is None:
             slot = self._slot ^ 1
         self._slot = slot
+        self._wait_slot(slot)
         acc = self.accums[slot]
         ctx = self.ctxs[slot % len(self.ctxs)]  # (inflight: slot 1's passes on the second context)
         with self._on_stream(slot):
@@ -140,6 +158,7 @@ class ShardedCostFunctor:
                                                    self.state.deformation_data)
                 ctx.eval_device(poses, acc.data_ptr())
             work = allreduce_accum(acc, self.group, async_op=True)
+        self._pending[slot] = work
         self.accum = acc
         return slot, work
 
@@ -148,18 +167,21 @@ class ShardedCostFunctor:
         host memory (`out`, default the pinned buffer); the host blocks on
         this copy only."""
         slot, work = pending
-        out = self.h_accum if out is None else out
+        out = self.h_accums[slot] if out is None else out
         with self._on_stream(slot):
             if work is not None:
                 work.wait()  # RCCL: the stream waits for the collective; gloo: the host does
+            if self._pending[slot] is work:
+                self._pending[slot] = None
             out.copy_(self.accums[slot], non_blocking=True)
             self._sync(slot)
         return out.numpy()
 
-    def _gradient(self, x, acc, solves):
+    def _gradient(self, x, acc, solves, slot=0):
         if self._native:
-            self._ensure_native()
-            return self.ctx.state_gradient(x, acc)  # (re-prepares x's FK / solve if a later pass was enqueued)
+            ctx = self.ctxs[slot % len(self.ctxs)]  # the context that ran the pass (its FK / solve is current)
+            self._ensure_native(ctx)
+            return ctx.state_gradient(x, acc)  # (re-prepares x's FK / solve if a later pass was enqueued)
         unflatten(self.state, x)  # the state of THIS x (a pipelined later launch moved it)
         normalize(self.state)
         c = float(acc[0]) + _regularizer(self.state, self.weight)
@@ -176,15 +198,18 @@ class ShardedCostFunctor:
         unflatten(self.state, x)
         normalize(self.state)
         poses, self._solves = prepare_pass(self.ctx, self.manipulator, self.state.q, self.state.deformation_data)
-        with self._on_stream():
+        self._wait_slot(0)  # accumulator 0 may still be read by its last all-reduce
+        self._slot, self.accum = 0, self.accums[0]
+        with self._on_stream(0):
             self.ctx.eval_device(poses, self.accum.data_ptr(), k.data_ptr(), d.data_ptr(), g.data_ptr())
             allreduce_accum(self.accum, self.group)
             return k[:n].cpu().numpy(), d[:n].cpu().numpy(), g[:n].cpu().numpy()
 
     def value_and_gradient(self, x):
         x = np.asarray(x, np.float64)
-        acc = self.finish(self.launch(x))
-        return self._gradient(x, acc, getattr(self, "_solves", ()))
+        pending = self.launch(x)
+        acc = self.finish(pending)
+        return self._gradient(x, acc, getattr(self, "_solves", ()), pending[0])
 
     def value_and_gradient_many(self, xs):
         """[(c, ∂c/∂x)] at independent configurations, pipelined: the pass at
@@ -198,9 +223,9 @@ class ShardedCostFunctor:
             nxt = self.launch(x)  # the other accumulator than `pending`'s
             nxt_solves = getattr(self, "_solves", ())
             if pending is not None:
-                xp, pp = pending
-                out.append(self._gradient(xp, self.finish(pp, self.torch.empty_like(self.h_accum)), solves))
+                xp, pp = pending  # (its own slot's pinned buffer: the other slot's pass is in flight)
+                out.append(self._gradient(xp, self.finish(pp), solves, pp[0]))
             pending, solves = (x, nxt), nxt_solves
         if pending is not None:
-            out.append(self._gradient(pending[0], self.finish(pending[1]), solves))
+            out.append(self._gradient(pending[0], self.finish(pending[1]), solves, pending[1][0]))
         return out

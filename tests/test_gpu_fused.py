@@ -140,6 +140,8 @@ def test_state_split_and_validation():
     ctx.set_stream(None)
     assert c5 == c1 and np.array_equal(g5, g1)
     assert c6 == c4 and np.array_equal(g6, g4)
+    with pytest.raises(FlashNativeError):  # not the x of either of the context's last two passes
+        ctx.state_gradient(x + 0.5, acc.cpu().numpy())
     ctx.set_deformations(1, 10.0)  # the squishable's 13 deformable points need 13 rows
     with pytest.raises(FlashNativeError):
         ctx.value_and_gradient(x[:m.mechanism.num_positions + 3])

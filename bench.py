@@ -15,12 +15,15 @@ the dependent step (pass + accumulator read-back + host wait, every step) and,
 labelled as such, the aggregate of two independent passes in flight
 (config.inflight_throughput).
 
-Sharding (contiguous ⌈N/W⌉ point ranges, uploaded once per frame):
+Sharding (contiguous point ranges, uploaded once per frame):
   (default)           strong scaling of the metric's cloud: ONE 2^20-point M64
-                      cloud (the same seed on every rank) split into W
-                      contiguous shards — `value`; for W > 1 the weak figure
-                      (2^20 points per GPU) is measured in the same run and
-                      reported beside it (`weak`)
+                      cloud (the same seed on every rank) split into W spatial
+                      shards — contiguous ranges of the whole cloud's Hilbert
+                      order (fsdf_set_points_range), rebalanced after the settle
+                      to equal measured chunk time — `value`; for W > 1 the weak
+                      figure (2^20 points per GPU) is measured in the same run
+                      and reported beside it (`weak`)
+  --slice-shards      strong scaling over slices of the caller's order (A/B)
   --points P          weak scaling only: every rank owns its own P-point cloud
   --global-points G   strong scaling only, of a G-point cloud
   --config c4         BASELINE config 4: IRB140, 10·2^20 points, strong scaling
@@ -110,6 +113,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="target wall time of each CPU baseline leg")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-full-iteration", action="store_true")
+    p.add_argument("--slice-shards", action="store_true",
+                   help="W > 1 strong scaling: contiguous slices of the caller's (shuffled) order instead of ranges "
+                        "of the whole cloud's Hilbert order (the round-4 partition; A/B)")
     p.add_argument("--seed", type=int, default=1234)
     return p.parse_args()
 
@@ -192,7 +198,7 @@ def main():
 
     import flash
     from flash import Models, synthetic
-    from flash.distributed import allreduce_accum, shard_range
+    from flash.distributed import allreduce_accum, gather_chunk_costs, shard_range, spatial_bounds
 
     model_name, default_points, scaling, workload = CONFIGS[args.config]
     if args.global_points is not None:
@@ -204,8 +210,17 @@ def main():
     manip = getattr(Models, model_name)()
     q_true, q_eval = synthetic.perturbed_configuration(manip, args.seed)
 
+    # strong scaling: every rank makes the same whole cloud and keeps a range of
+    # its Hilbert order (spatial shards, rebalanced to equal measured chunk time
+    # after the settle); --slice-shards: slices of the caller's (shuffled) order
+    bounds = None
+
     def strong_shard(g):
+        nonlocal bounds
         cloud = synthetic.depth_cloud(manip, q_true, g, seed=args.seed + 17, order=args.order)
+        if world > 1 and not args.slice_shards:
+            bounds = spatial_bounds(g, world)
+            return cloud
         a, b = shard_range(g, rank, world)
         return np.ascontiguousarray(cloud[a:b])
 
@@ -243,21 +258,35 @@ def main():
     h_acc = torch.empty(ctx.accum_len, dtype=torch.float64, pin_memory=True)
     accum = accums[0][0]
 
-    def run_cloud(pts_host):
+    def run_cloud(pts_host, shard_bounds=None):
         """Upload the cloud (timed per frame, every context), then W untimed + K
         timed steps bracketed by barrier + synchronize; returns the max-over-ranks
-        (elapsed s, whole-pass ms, pass-kernel ms, set_points ms)."""
+        (elapsed s, whole-pass ms, pass-kernel ms, set_points ms). shard_bounds:
+        spatial shards — every context keeps this rank's range of the whole
+        cloud's Hilbert order (fsdf_set_points_range), and after the settle the
+        ranks rebalance the ranges to equal measured chunk time (the list is
+        updated in place)."""
         d_pts = torch.as_tensor(pts_host, device=dev)
         torch.cuda.synchronize()
+
+        if shard_bounds is not None:  # (flash.distributed.ShardedCostFunctor._plan_window: measured chunk costs)
+            for cx in ctxs:
+                cx.set_plan(True, -1.0, -1.0, int(min(max(2 * -(-len(pts_host) // world), 98304), 524288)))
+
+        def upload(cx):
+            if shard_bounds is not None:
+                cx.set_points_range_device(d_pts.data_ptr(), len(pts_host), *shard_bounds[rank])
+            else:
+                cx.set_points_device(d_pts.data_ptr(), len(pts_host))
         for cx in ctxs:  # (every context, the side figure's too)
-            cx.set_points_device(d_pts.data_ptr(), len(pts_host))  # first upload (allocations)
+            upload(cx)  # first upload (allocations)
         set_ms = []
         for _ in range(3):  # once per frame: copy (+ Hilbert sort), every context of the timed region
             t_set = time.perf_counter()
             for cx in ctxs[:C]:
-                cx.set_points_device(d_pts.data_ptr(), len(pts_host))
+                upload(cx)
             set_ms.append((time.perf_counter() - t_set) * 1e3)
-        del d_pts
+        # (outputs sized for the whole cloud: a rebalance may grow this rank's range)
         n_ = len(pts_host)
         outs, bufs = [], []
         for _ in range(CS):
@@ -307,6 +336,21 @@ def main():
             i += 1
             if i % 16 == 0:
                 torch.cuda.synchronize()
+        if shard_bounds is not None and world > 1:
+            # rebalance: the ranks' measured per-chunk durations (the planned
+            # pass's, in the whole cloud's chunk order) all-gathered once; new
+            # ranges at equal summed chunk time, every rank re-uploads its range
+            torch.cuda.synchronize()
+            costs = gather_chunk_costs(ctx.chunk_costs())
+            if costs.shape[0] == -(-len(pts_host) // 64):
+                shard_bounds[:] = spatial_bounds(len(pts_host), world, costs)
+                for cx in ctxs:
+                    upload(cx)
+                for i in range(16 * C):  # a new range: its first passes plan anew
+                    c = i % C
+                    ctxs[c].eval_device(poses[(i // C) & 1], accums[c][(i // C) & 1].data_ptr(), *outs[c])
+                torch.cuda.synchronize()
+        del d_pts
         # K passes one at a time on context 0 (no collective), right after the
         # settle: the kernel's own launch duration (the roofline's, as rocprofv3
         # sees it in tools/rocprof_round.sh) and one step's latency
@@ -398,8 +442,8 @@ def main():
                     assert torch.equal(accums[c][s_], accums[0][s_]), "in-flight contexts disagree"
         return float(t[0]), float(t[1]), float(t[2]), float(t[3])
 
-    n = len(pts)
-    elapsed, timed_pass_ms, timed_kernel_ms, set_points_ms = run_cloud(pts)
+    elapsed, timed_pass_ms, timed_kernel_ms, set_points_ms = run_cloud(pts, bounds)
+    n = ctx.n  # this rank's resident points
     serial = dict(SERIAL)
     side = dict(SIDE_RES)
     # the roofline prices the kernel alone on the device (its serial launches,
@@ -508,6 +552,11 @@ def main():
                                 f"{ctx.accum_len} f64 per pass" if world > 1 else
                                 f"one GPU ({scaling} figure of the metric's cloud); at W > 1 one "
                                 f"{ctx.accum_len}-f64 all-reduce per pass"),
+                "partition": (None if world == 1 else
+                              "spatial: contiguous ranges of the whole cloud's Hilbert order (fsdf_set_points_range), "
+                              "rebalanced after the settle to equal measured chunk time" if bounds is not None else
+                              "slices of the caller's order" if scaling == "strong" else "one cloud per rank"),
+                "shard_bounds": bounds,
                 "backend": backend,
                 "allreduce_ms": allreduce_ms,
                 "allreduce_overlap": ("asynchronous all-reduce, two accumulators: step i+1's pass overlaps step "

@@ -245,6 +245,20 @@ int fsdf_set_rbf_params(fsdf_ctx* ctx, const double* params, int64_t n_doubles);
 int fsdf_set_points(fsdf_ctx* ctx, const double* xyz, int64_t n);
 /* Same, from a device-resident AoS buffer (copied device-to-device). */
 int fsdf_set_points_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n);
+/* One rank's shard of a cloud split over several devices (the
+ * cost is a plain sum over points, src/gradientdescent.jl:32): the whole
+ * n-point cloud is uploaded and ordered (the Hilbert order with sort_points,
+ * else the caller's), and positions [begin, end) of that order stay resident —
+ * a contiguous region of space, so the shard keeps the whole cloud's point
+ * density per 64-point chunk (a slice of an arbitrary order would scatter each
+ * rank's points over the whole scene). Every rank of a job passes the same
+ * cloud and its own range; the ranges partition [0, n). Per-point outputs of a
+ * ranged cloud are always in its resident order, and fsdf_get_permutation names
+ * each resident point's index in the whole cloud. fsdf_chunk_costs then reports
+ * the range's chunks — the chunks of the whole cloud's order when begin is a
+ * multiple of 64 — which is what flash.distributed balances the ranges by. */
+int fsdf_set_points_range(fsdf_ctx* ctx, const double* xyz, int64_t n, int64_t begin, int64_t end);
+int fsdf_set_points_range_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n, int64_t begin, int64_t end);
 int fsdf_num_points(const fsdf_ctx* ctx, int64_t* n_out);
 
 /* One residual pass over the resident cloud (synchronous, host buffers).

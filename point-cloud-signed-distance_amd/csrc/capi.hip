@@ -110,6 +110,10 @@ struct fsdf_ctx {
   fsdf::SortScratch sort;            // per-frame sort scratch (grown only)
   double* d_staging = nullptr;       // host-source clouds land here first
   int64_t staging_cap = 0;
+  bool ranged = false;               // the resident cloud is a range of a larger one (fsdf_set_points_range)
+  void* d_range_pts = nullptr;       // fsdf_set_points_range: the whole cloud, sorted (scratch)
+  int32_t* d_range_perm = nullptr;
+  int64_t range_cap = 0;
   // work
   double* d_partials = nullptr;
   size_t partials_cap = 0;
@@ -286,6 +290,8 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   dfree(c->d_perm);
   dfree(c->d_chunk_ws);
   dfree(c->d_staging);
+  dfree(c->d_range_pts);
+  dfree(c->d_range_perm);
   fsdf::free_sort_scratch(c->sort);
   dfree(c->d_partials);
   dfree(c->d_kstar);
@@ -708,11 +714,19 @@ static int adopt_points_device(fsdf_ctx* c, const double* d_src, int64_t n, void
   return FSDF_OK;
 }
 
-static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool device_src) {
+// [begin, end): the resident cloud is that range of the whole cloud's order
+// (the Hilbert order of all n points with sort_points, else the caller's);
+// the permutation then holds the points' indices in the whole cloud
+// (fsdf_set_points_range). begin = 0, end = n: the whole cloud.
+static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool device_src, int64_t begin, int64_t end) {
   if (!c) return FSDF_ERR_ARG;
   if (n < 0 || (n > 0 && !src)) return fail(c, FSDF_ERR_ARG, "set_points: bad buffer (n=%lld)", (long long)n);
-  if (c->sort_points && n > INT32_MAX)
-    return fail(c, FSDF_ERR_ARG, "set_points: sort_points supports < 2^31 points (n=%lld)", (long long)n);
+  if (begin < 0 || end < begin || end > n)
+    return fail(c, FSDF_ERR_ARG, "set_points_range: bad range [%lld, %lld) of %lld points", (long long)begin,
+                (long long)end, (long long)n);
+  if ((c->sort_points || begin > 0 || end < n) && n > INT32_MAX)
+    return fail(c, FSDF_ERR_ARG, "set_points: sorted or ranged clouds support < 2^31 points (n=%lld)", (long long)n);
+  const bool ranged = begin > 0 || end < n;
   HIPCHECK(c, hipSetDevice(c->device));
   // the previous frame's work may still read the staging buffer / the cloud
   HIPCHECK(c, hipStreamSynchronize(c->stream));
@@ -728,29 +742,69 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
     HIPCHECK(c, hipMemcpyAsync(c->d_staging, src, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
     d_src = c->d_staging;
   }
-  if (c->sort_points && n > 0) {
-    // spatially coherent resident order + permutation back to caller order
-    const size_t tsz = c->precision == 64 ? sizeof(double) : sizeof(float);
-    if (c->pts_cap < n) {
+  const int64_t nr = end - begin;  // resident points
+  const size_t tsz = c->precision == 64 ? sizeof(double) : sizeof(float);
+  auto ensure_res = [&]() -> int {
+    if (c->pts_cap < nr || !c->d_pts) {
       dfree(c->d_pts);
       c->pts_cap = 0;
-      HIPCHECK(c, hipMalloc(&c->d_pts, (size_t)n * 3 * tsz));
-      c->pts_cap = n;
+      HIPCHECK(c, hipMalloc(&c->d_pts, (size_t)std::max<int64_t>(nr, 1) * 3 * tsz));
+      c->pts_cap = std::max<int64_t>(nr, 1);
     }
-    if (c->perm_cap < n || !c->d_perm) {
+    if (c->perm_cap < nr || !c->d_perm) {
       dfree(c->d_perm);
       c->perm_cap = 0;
-      HIPCHECK(c, hipMalloc(&c->d_perm, (size_t)n * sizeof(int32_t)));
-      c->perm_cap = n;
+      HIPCHECK(c, hipMalloc(&c->d_perm, (size_t)std::max<int64_t>(nr, 1) * sizeof(int32_t)));
+      c->perm_cap = std::max<int64_t>(nr, 1);
     }
-    hipError_t e = fsdf::sort_points_spatial(d_src, n, c->precision, c->d_pts, c->d_perm, c->sort, c->stream);
-    if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "set_points (sort): %s", hipGetErrorString(e));
+    return FSDF_OK;
+  };
+  if (c->sort_points && n > 0) {
+    // spatially coherent resident order + permutation back to caller order
+    int rc = ensure_res();
+    if (rc) return rc;
+    if (!ranged) {
+      hipError_t e = fsdf::sort_points_spatial(d_src, n, c->precision, c->d_pts, c->d_perm, c->sort, c->stream);
+      if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "set_points (sort): %s", hipGetErrorString(e));
+    } else {
+      // the whole cloud sorted into scratch, then the range kept
+      if (c->range_cap < n) {
+        dfree(c->d_range_pts);
+        dfree(c->d_range_perm);
+        c->range_cap = 0;
+        HIPCHECK(c, hipMalloc(&c->d_range_pts, (size_t)n * 3 * tsz));
+        HIPCHECK(c, hipMalloc(&c->d_range_perm, (size_t)n * sizeof(int32_t)));
+        c->range_cap = n;
+      }
+      hipError_t e =
+          fsdf::sort_points_spatial(d_src, n, c->precision, c->d_range_pts, c->d_range_perm, c->sort, c->stream);
+      if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "set_points_range (sort): %s", hipGetErrorString(e));
+      if (nr > 0) {
+        HIPCHECK(c, hipMemcpyAsync(c->d_pts, (const char*)c->d_range_pts + (size_t)begin * 3 * tsz,
+                                   (size_t)nr * 3 * tsz, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHECK(c, hipMemcpyAsync(c->d_perm, c->d_range_perm + begin, (size_t)nr * sizeof(int32_t),
+                                   hipMemcpyDeviceToDevice, c->stream));
+      }
+    }
+  } else if (ranged) {
+    // a slice of the caller's order; the permutation names the slice's indices
+    int rc = ensure_res();
+    if (rc) return rc;
+    rc = adopt_points_device(c, d_src + 3 * begin, nr, &c->d_pts, &c->pts_cap);
+    if (rc) return rc;
+    std::vector<int32_t> idx((size_t)std::max<int64_t>(nr, 0));
+    for (int64_t i = 0; i < nr; ++i) idx[(size_t)i] = (int32_t)(begin + i);
+    if (nr > 0)
+      HIPCHECK(c, hipMemcpyAsync(c->d_perm, idx.data(), (size_t)nr * sizeof(int32_t), hipMemcpyHostToDevice,
+                                 c->stream));
+    HIPCHECK(c, hipStreamSynchronize(c->stream));  // (idx is a host temporary)
   } else {
     dfree(c->d_perm);
     c->perm_cap = 0;
     int rc = adopt_points_device(c, d_src, n, &c->d_pts, &c->pts_cap);
     if (rc) return rc;
   }
+  n = nr;  // from here on: the resident cloud
   if (n > 0) {  // per-chunk bounding spheres of the resident order (pose-independent)
     // (padded to whole 4-chunk pass workgroups: every wave of a hull-partitioned
     // pass reads its chunk's row, also past the cloud's end)
@@ -767,14 +821,26 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
   // the caller may reuse its buffer once this returns
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   c->n = n;
+  c->ranged = ranged;
   c->plan_nc = -1;  // a new cloud: its first planned pass runs the default shape and measures
   return FSDF_OK;
 }
 
-extern "C" int fsdf_set_points(fsdf_ctx* c, const double* xyz, int64_t n) { return set_points_impl(c, xyz, n, false); }
+extern "C" int fsdf_set_points(fsdf_ctx* c, const double* xyz, int64_t n) {
+  return set_points_impl(c, xyz, n, false, 0, n);
+}
 
 extern "C" int fsdf_set_points_device(fsdf_ctx* c, const double* d_xyz, int64_t n) {
-  return set_points_impl(c, d_xyz, n, true);
+  return set_points_impl(c, d_xyz, n, true, 0, n);
+}
+
+extern "C" int fsdf_set_points_range(fsdf_ctx* c, const double* xyz, int64_t n, int64_t begin, int64_t end) {
+  return set_points_impl(c, xyz, n, false, begin, end);
+}
+
+extern "C" int fsdf_set_points_range_device(fsdf_ctx* c, const double* d_xyz, int64_t n, int64_t begin,
+                                            int64_t end) {
+  return set_points_impl(c, d_xyz, n, true, begin, end);
 }
 
 static int ensure_partials(fsdf_ctx* c, int nblocks) {
@@ -1011,7 +1077,11 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
 
 // per-point outputs of resident-cloud passes: scattered to caller order through
 // the sort permutation, or written in resident order (coalesced)
-static const int32_t* out_perm(const fsdf_ctx* c) { return c->out_order == FSDF_ORDER_RESIDENT ? nullptr : c->d_perm; }
+// (a ranged cloud, fsdf_set_points_range: always resident order — its
+// permutation names indices of the WHOLE cloud, beyond the outputs' length)
+static const int32_t* out_perm(const fsdf_ctx* c) {
+  return c->out_order == FSDF_ORDER_RESIDENT || c->ranged ? nullptr : c->d_perm;
+}
 
 extern "C" int fsdf_set_partition(fsdf_ctx* c, int64_t four_way_max_points, int64_t two_way_max_points) {
   if (!c) return FSDF_ERR_ARG;

@@ -63,6 +63,8 @@ _PROTOS = {
     "fsdf_set_rbf_params": (c_int32, [c_void_p, c_void_p, c_int64]),
     "fsdf_set_points": (c_int32, [c_void_p, c_void_p, c_int64]),
     "fsdf_set_points_device": (c_int32, [c_void_p, c_void_p, c_int64]),
+    "fsdf_set_points_range": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_int64]),
+    "fsdf_set_points_range_device": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_int64]),
     "fsdf_num_points": (c_int32, [c_void_p, POINTER(c_int64)]),
     "fsdf_eval": (c_int32, [c_void_p, c_void_p, POINTER(c_double), c_void_p, c_void_p, c_void_p, c_void_p]),
     "fsdf_eval_device": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -231,6 +233,21 @@ class Context:
     def set_points_device(self, dev_ptr: int, n: int):
         check(self._lib.fsdf_set_points_device(self._ctx, c_void_p(dev_ptr), n), self._ctx, "set_points_device")
         self.n = n
+
+    def set_points_range(self, xyz: np.ndarray, begin: int, end: int):
+        """One shard of a cloud split over devices (fsdf_set_points_range):
+        positions [begin, end) of the whole cloud's (Hilbert) order stay
+        resident; per-point outputs in resident order, permutation() = their
+        indices in the whole cloud."""
+        pts = np.ascontiguousarray(xyz, np.float64).reshape(-1, 3)
+        check(self._lib.fsdf_set_points_range(self._ctx, ptr(pts), pts.shape[0], int(begin), int(end)), self._ctx,
+              "set_points_range")
+        self.n = int(end) - int(begin)
+
+    def set_points_range_device(self, dev_ptr: int, n: int, begin: int, end: int):
+        check(self._lib.fsdf_set_points_range_device(self._ctx, c_void_p(dev_ptr), n, int(begin), int(end)),
+              self._ctx, "set_points_range_device")
+        self.n = int(end) - int(begin)
 
     def _poses(self, poses):
         p = np.ascontiguousarray(poses, np.float64).reshape(-1, 12)

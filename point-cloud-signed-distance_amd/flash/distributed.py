@@ -37,6 +37,62 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     return start, min(start + per, n)
 
 
+CHUNK = 64  # points per wave-chunk of the pass (and per entry of fsdf_chunk_costs)
+
+
+def spatial_bounds(n: int, world: int, chunk_costs=None) -> list[tuple[int, int]]:
+    """Shard ranges [begin, end) over a cloud's SPATIAL order (the device's
+    Hilbert order, fsdf_set_points_range): contiguous, 64-point-chunk aligned,
+    partitioning [0, n). Without costs every rank gets the same number of
+    chunks; with `chunk_costs` (one per chunk of the whole cloud's order — the
+    ranks' fsdf_chunk_costs concatenated) the boundaries split the prefix sum of
+    the costs evenly, so each rank's summed chunk time is ~1/world of the
+    total. A range of the spatial order is a compact region of space: its
+    64-point chunks are as dense as the whole cloud's, where a slice of an
+    arbitrary (e.g. shuffled) order gives every rank a sparse 1/world sample of
+    the whole scene whose chunks each meet more hulls."""
+    nc = -(-n // CHUNK)
+    if world <= 1 or nc == 0:
+        return [(0, n)] + [(n, n)] * max(0, world - 1)
+    if chunk_costs is None:
+        w = np.ones(nc)
+        w[-1] = (n - CHUNK * (nc - 1)) / CHUNK
+    else:
+        w = np.asarray(chunk_costs, np.float64).reshape(-1)
+        if w.shape[0] != nc:
+            raise ValueError(f"spatial_bounds: {w.shape[0]} chunk costs for {nc} chunks")
+        w = np.maximum(w, 1e-9)
+    cum = np.cumsum(w)
+    cuts = [0]
+    for r in range(1, world):
+        c = int(np.searchsorted(cum, cum[-1] * r / world, side="left")) + 1  # first chunk of rank r
+        cuts.append(min(max(c, cuts[-1]), nc))
+    cuts.append(nc)
+    return [(min(CHUNK * a, n), min(CHUNK * b, n)) for a, b in zip(cuts[:-1], cuts[1:])]
+
+
+def gather_chunk_costs(local_costs, group=None) -> np.ndarray:
+    """The ranks' per-chunk costs concatenated in rank order (the whole cloud's
+    chunk order when the shards are spatial_bounds ranges): one all_gather of
+    the padded arrays — a control-path collective, once per rebalance."""
+    import torch
+    import torch.distributed as dist
+    local = np.asarray(local_costs, np.float64).reshape(-1)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return local
+    world = dist.get_world_size(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    cnt = torch.tensor([local.shape[0]], dtype=torch.int64, device=dev)
+    cnts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt, group=group)
+    m = int(max(int(c.item()) for c in cnts))
+    buf = torch.zeros(max(m, 1), dtype=torch.float64, device=dev)
+    buf[:local.shape[0]] = torch.from_numpy(local).to(dev)
+    bufs = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(bufs, buf, group=group)
+    return np.concatenate([b[:int(c.item())].cpu().numpy() for b, c in zip(bufs, cnts)])
+
+
 def allreduce_accum(accum, group=None, async_op=False):
     """Sum the per-rank accumulators in place (torch tensor, any device).
     async_op=True returns the collective's work handle (None on one rank):
@@ -59,7 +115,7 @@ class ShardedCostFunctor:
 
     def __init__(self, manipulator: Manipulator, local_points, rank: int = 0, world: int = 1, device: int = 0,
                  precision: int = 64, group=None, deformation_cost_weight=default_deformation_cost_weight,
-                 engine=None, inflight: int = 1):
+                 engine=None, inflight: int = 1, spatial: bool = False, bounds=None):
         """engine: an already-built context-like object to drive instead of
         manipulator.engine(device, precision) — with engine.device_type == "cpu"
         the accumulator lives in host memory and no HIP stream is used (the CPU
@@ -68,7 +124,13 @@ class ShardedCostFunctor:
         inflight = 2 (HIP contexts only): a second context over the shard on a
         stream of its own (manipulator.engine(..., slot=1)) takes every other
         launch, so value_and_gradient_many's consecutive passes run together
-        (INTEGRATION.md; bit-identical)."""
+        (INTEGRATION.md; bit-identical).
+        spatial = True: `local_points` is the WHOLE cloud (every rank passes the
+        same one) and this rank keeps range `bounds[rank]` (default
+        spatial_bounds(n, world): equal chunk counts) of its spatial order
+        (fsdf_set_points_range); rebalance() moves the boundaries to equal
+        measured cost. Per-point outputs are then in the shard's resident
+        order, global_index() names their indices in the whole cloud."""
         import contextlib
         import torch
         self.torch = torch
@@ -81,7 +143,15 @@ class ShardedCostFunctor:
         self.dev = torch.device("cpu") if on_host else torch.device("cuda", device)
         pts = torch.as_tensor(np.ascontiguousarray(local_points, np.float64).reshape(-1, 3), device=self.dev)
         self._pts = pts  # the context reads the resident copy (set_points_device does not own it)
-        self.ctx.set_points_device(pts.data_ptr(), pts.shape[0])
+        self.rank, self.world, self.spatial = rank, world, spatial
+        if spatial:
+            self.cloud_n = pts.shape[0]
+            self.bounds = list(bounds) if bounds is not None else spatial_bounds(self.cloud_n, world)
+            self.range = self.bounds[rank]
+            self._plan_window(self.ctx)
+            self.ctx.set_points_range_device(pts.data_ptr(), pts.shape[0], *self.range)
+        else:
+            self.ctx.set_points_device(pts.data_ptr(), pts.shape[0])
         # two accumulators: the next pass may run while the previous all-reduce is in flight
         self.accums = [torch.zeros(self.ctx.accum_len, dtype=torch.float64, device=self.dev) for _ in range(2)]
         self.accum = self.accums[0]
@@ -112,7 +182,11 @@ class ShardedCostFunctor:
                 c2 = manipulator.engine(device, precision, slot=1)
                 s2 = torch.cuda.Stream(self.dev)
                 c2.set_stream(s2.cuda_stream)
-                c2.set_points_device(pts.data_ptr(), pts.shape[0])
+                if spatial:
+                    self._plan_window(c2)
+                    c2.set_points_range_device(pts.data_ptr(), pts.shape[0], *self.range)
+                else:
+                    c2.set_points_device(pts.data_ptr(), pts.shape[0])
                 self.ctxs.append(c2)
                 self.streams.append(s2)
             self._on_stream = lambda slot=0: torch.cuda.stream(self.streams[slot % len(self.streams)])
@@ -187,9 +261,44 @@ class ShardedCostFunctor:
         c = float(acc[0]) + _regularizer(self.state, self.weight)
         return c, chain_gradient(self.manipulator, x, acc, self.weight, solves)
 
+    def _plan_window(self, ctx):
+        """Spatial shards run the planned pass up to twice the average shard
+        (at most 524,288 points, the default window's top): its per-chunk
+        durations are what rebalance() splits by, also for shards below the
+        default window's 98,304-point bottom (there it measured within 3 % of
+        the unplanned 4-way tier)."""
+        if hasattr(ctx, "set_plan"):
+            ctx.set_plan(True, -1.0, -1.0, int(min(max(2 * -(-self.cloud_n // self.world), 98304), 524288)))
+
+    def global_index(self) -> np.ndarray:
+        """The whole cloud's index of each resident point (spatial shards; for
+        a plain shard its own caller order is resident, indices 0..n-1 of it)."""
+        return self.ctx.permutation()
+
+    def rebalance(self):
+        """Move the spatial shard boundaries so that every rank's summed chunk
+        time (the planned pass's measured per-chunk durations, fsdf_chunk_costs,
+        all-gathered once) is ~1/world of the total, and re-upload this rank's
+        range. Call on every rank, after at least one pass over the current
+        ranges. Returns the new bounds."""
+        if not self.spatial:
+            raise ValueError("rebalance: not a spatial shard")
+        costs = gather_chunk_costs(self.ctx.chunk_costs(), self.group)
+        nc = -(-self.cloud_n // CHUNK)
+        if costs.shape[0] != nc:  # (no planned pass measured every chunk: keep the ranges)
+            return self.bounds
+        for slot in (0, 1):
+            self._wait_slot(slot)
+        self._sync(0)
+        self.bounds = spatial_bounds(self.cloud_n, self.world, costs)
+        self.range = self.bounds[self.rank]
+        for c in self.ctxs:
+            c.set_points_range_device(self._pts.data_ptr(), self.cloud_n, *self.range)
+        return self.bounds
+
     def per_point(self, x):
         """(k*, d*, ∇d*) of this rank's shard at x, like CostFunctor.per_point (device
-        outputs, caller order)."""
+        outputs, caller order; a spatial shard: its resident order, global_index())."""
         torch = self.torch
         n = self.ctx.n
         k = torch.empty(max(n, 1), dtype=torch.int32, device=self.dev)

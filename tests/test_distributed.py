@@ -104,6 +104,36 @@ class OracleEngine:
     def set_points_device(self, ptr, n):
         self.n = n
         self.pts = self._view(ptr, 3 * n, np.float64).reshape(n, 3).copy()
+        self.perm = np.arange(n)
+
+    @staticmethod
+    def spatial_order(pts):
+        """A deterministic spatial (Morton) order standing in for the device's Hilbert sort."""
+        lo, hi = pts.min(0), pts.max(0)
+        q = np.floor((pts - lo) / np.maximum(hi - lo, 1e-12) * 1023).astype(np.int64)
+        key = np.zeros(len(pts), np.int64)
+        for b in range(10):
+            for a in range(3):
+                key |= ((q[:, a] >> b) & 1) << (3 * b + a)
+        return np.argsort(key, kind="stable")
+
+    def set_points_range_device(self, ptr, n, begin, end):
+        cloud = self._view(ptr, 3 * n, np.float64).reshape(n, 3).copy()
+        order = self.spatial_order(cloud)
+        self.perm = order[begin:end]
+        self.order_pos, self.total = np.arange(begin, end), n
+        self.pts = cloud[self.perm]
+        self.n = end - begin
+
+    def permutation(self):
+        return self.perm.copy()
+
+    def chunk_costs(self):
+        """Deterministic per-chunk stand-in durations, uneven on purpose: chunks
+        of the lower half of the cloud's order cost 1, of the upper half 9."""
+        nc = -(-self.n // 64)
+        return np.array([1.0 + 8.0 * (self.perm[64 * c] >= 0 and self.order_pos[64 * c] * 2 >= self.total)
+                         for c in range(nc)])
 
     def set_rbf_params(self, rows):
         self.rows = np.asarray(rows, np.float64).copy()
@@ -223,3 +253,73 @@ def test_gloo_world2_pipelined_allreduce_same_bits(name):
         for (c1, g1), (c2, g2) in zip(seq, pip):
             assert c1 == c2 and np.array_equal(g1, g2)
         assert len({c for c, _ in seq}) == 4  # the configurations differ
+
+
+def test_spatial_bounds_partition_and_balance():
+    from flash.distributed import spatial_bounds
+    r = np.random.Generator(np.random.PCG64(5))
+    for n in (0, 1, 63, 64, 65, 1000, 131072 + 7):
+        for w in (1, 2, 3, 8):
+            for costs in (None, r.random(-(-n // 64)) ** 4 if n else None):
+                b = spatial_bounds(n, w, costs)
+                assert len(b) == w and b[0][0] == 0 and b[-1][1] == n
+                assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
+                assert all(a % 64 == 0 or a == n for a, _ in b)
+                if costs is not None and n:
+                    per = [costs[a // 64:-(-e // 64)].sum() for a, e in b]
+                    assert max(per) <= costs.sum() / w + costs.max() + 1e-9
+
+
+def _spatial_worker(rank, world, port, q, name):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from flash.distributed import ShardedCostFunctor
+        m, pts, x = _scene(name)
+        f = ShardedCostFunctor(m, pts, rank, world, engine=OracleEngine(m), spatial=True)
+        out = []
+        for _ in range(2):  # equal chunk counts, then cost-balanced
+            c, g = f.value_and_gradient(x)
+            k, d, _ = f.per_point(x)
+            out.append((list(f.bounds), c, g, f.global_index(), k, d))
+            f.rebalance()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["irb140", "beanbag_rbf"])
+def test_gloo_world2_spatial_shards(name):
+    """Spatial shards (contiguous ranges of the cloud's spatial order, every
+    rank given the whole cloud), before and after a cost-balancing rebalance():
+    cost and ∂c/∂x equal the 1-rank functor's, and the per-point outputs placed
+    at global_index() reproduce the whole cloud's."""
+    import multiprocessing as mp
+    from flash.distributed import ShardedCostFunctor
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_spatial_worker, args=(r, 2, port, q, name)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m, pts, x = _scene(name)
+    one = ShardedCostFunctor(m, pts, engine=OracleEngine(m))
+    c1, g1 = one.value_and_gradient(x)
+    k1, d1, _ = one.per_point(x)
+    bounds = [[o[0] for o in r[1]] for r in res]
+    assert bounds[0] == bounds[1]  # every rank agrees on the ranges
+    assert bounds[0][0] != bounds[0][1]  # the rebalance moved them (uneven stand-in costs)
+    for step in range(2):
+        k = np.full(len(pts), -1)
+        d = np.zeros(len(pts))
+        for _, out in res:
+            b, c, g, idx, kk, dd = out[step]
+            assert c == pytest.approx(c1, rel=1e-10)
+            assert np.allclose(g, g1, rtol=1e-9, atol=1e-10 * max(1.0, np.abs(g1).max()))
+            k[idx], d[idx] = kk, dd
+        assert np.array_equal(k, k1) and np.array_equal(d, d1)

@@ -22,6 +22,7 @@
 #   sweep           bench.py at 2^16 .. 2^20 points           -> size_sweep.jsonl
 #   configs         tools/bench_configs.py (BASELINE configs C2-C5, M64)
 #   rehearse        bench.py N=2 on one GPU (gloo, both ranks on device 0)
+#   shards          strong-scaling shards stepped alone at W = 1/2/4/8 (tools/spatial_shards.py) -> spatial_shards.jsonl
 #   hsweep:MODEL:SIZES[:EXTRA]  partition tiers / planned pass against cloud size (tools/hpart_sweep.py; MODEL
 #                   irb140 | arm_grid, SIZES and EXTRA arguments comma-separated) -> hpart_sweep_MODEL*.jsonl
 #   inflight:SIZES[:EXTRA]  independent passes in flight (tools/inflight_probe.py)  -> inflight.jsonl
@@ -137,6 +138,11 @@ for r in csv.DictReader(open(f)):
         || { tail -30 $O/rehearse_n2.err; exit 1; }
       cut -c1-600 $O/rehearse_n2.json
       unset FSDF_BENCH_BACKEND FSDF_BENCH_DEVICE ;;
+    shards)
+      # strong-scaling shards of the bench cloud, each stepped alone (tools/spatial_shards.py)
+      timeout -k 10 600 python -u tools/spatial_shards.py > $O/spatial_shards.jsonl 2> $O/spatial_shards.err \
+        || { echo SHARDS FAILED; tail $O/spatial_shards.err; exit 1; }
+      cut -c1-200 $O/spatial_shards.jsonl ;;
     hsweep:*)
       # hsweep:MODEL:SIZES[:EXTRA] — EXTRA: more tools/hpart_sweep.py arguments, commas = spaces
       R=${step#hsweep:}; M=${R%%:*}; R=${R#*:}; S=${R%%:*}; X=""; [ "$R" != "$S" ] && X=${R#*:}; X=${X//,/ }

@@ -13,14 +13,19 @@ What each count pins:
   implemented RBF interpolant is the reference's.
 * IRB140 2,226 / 4,460 (examples/irb140.ipynb:299) — NOT reproduced: the exact
   polytope SDF gives 2,242 / 4,480, robust to every grid convention. The
-  reference's surface has Euler characteristic V - F/2 = -4 where ours is 2
-  (genus 0), so this is a shape difference, not a rounding flip: single-point
-  flips near the iso level change V, F by (±2k, ±4k), never χ. EnhancedGJK's
-  hill-climbing NeighborMesh support and warm-started simplex (un-vendored
-  @404de6a9) are the candidate cause; an emulation of them
-  (tools/contour_study.py, profiles/r04/contour_study.txt) does not reproduce
-  the count either (2,242 / 4,480; a rounding-level variant of the emulation
-  2,260 / 4,512), so the cause stays open without the package.
+  reference's surface has Euler characteristic V - F/2 = -4 where ours is 2.
+  A single node flip CAN change χ (one isolated node in: (14, 24), χ = 2,
+  test_mesh_counts_closed_surfaces; a node at a thin junction can open or
+  close a tunnel), so χ alone does not tell a shape change from a few flips;
+  moving every node within δ of the iso level (δ 1e-4 .. 1e-2) to either side
+  keeps χ = 2. EnhancedGJK's hill-climbing NeighborMesh support and
+  warm-started simplex (un-vendored @404de6a9) were emulated over three mesh
+  loaders (merged STL, STL triangle soup, .obj face indices), two initial
+  simplices and two warm-start orders (tools/contour_study.py,
+  profiles/r05/contour_study.txt): the merged STL and the .obj give 2,242 /
+  4,480 with no node on the other side of the iso level, the soup 276 / 528
+  or 202 / 384. No variant gives 2,226 / 4,460; the cause stays open without
+  the package.
 * C5 4,494 / 8,912 (examples/irb_and_squishable.ipynb:318) — NOT reproduced:
   4,390 / 8,712; the arm's part is the IRB140 mesh above (same relative grid)
   and the rest depends on the RBF skin's normalization near its zero set.

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Which conventions reproduce the reference's contour-mesh counts
-(tests/golden/contour_pins.json)? CPU study, output in profiles/r04/contour_study.txt.
+(tests/golden/contour_pins.json)? CPU study, output in profiles/r05/contour_study.txt
+(round 4: profiles/r04/contour_study.txt).
 
 1. Grid conventions x level tests (tests/contour_mesh.py variants) for the
    three pinned calls, scene SDF from the C oracle (== the GPU path).
@@ -13,8 +14,12 @@
    simplex with the closest-point weights, atol 1e-6, max 100 iterations,
    one CollisionCache per surface warm-started across the grid sweep in
    GeometryTypes' loop order (z fastest) or x fastest; the support by brute
-   force as the control. The package is un-vendored: this is a restatement
-   of its published design, not of its code.
+   force as the control. Round 5 adds the NeighborMesh adjacency of three
+   loaders (the STL with equal vertices merged, the STL as a triangle soup,
+   the .obj twin's face indices) and the cache's initial simplex at vertex 1
+   or at the first face, and lists the grid nodes on the other side of the
+   iso level from the exact SDF. The package is un-vendored: this is a
+   restatement of its published design, not of its code.
 
     python tools/contour_study.py [--no-gjk]
 """
@@ -88,12 +93,26 @@ def section_rbf(out):
 
 
 # ---- EnhancedGJK emulation ------------------------------------------------------------
-def stl_mesh(name):
+def stl_triangles(name):
     b = open(MESHES + name + "_chull.stl", "rb").read()
     n = struct.unpack("<I", b[80:84])[0]
     tri = np.frombuffer(b[84:84 + 50 * n], dtype=np.dtype([("n", "<f4", 3), ("v", "<f4", (3, 3)), ("a", "<u2")]))
+    return tri["v"].astype(np.float64)
+
+
+def adjacency(nv, faces):
+    nb = [set() for _ in range(nv)]
+    for f in faces:
+        for i, j in itertools.permutations(range(3), 2):
+            if f[i] != f[j]:
+                nb[f[i]].add(f[j])
+    return [sorted(s) for s in nb]
+
+
+def stl_mesh(name):
+    """STL triangles with equal vertices merged (first-seen order)."""
     verts, idx, faces = [], {}, []
-    for t in tri["v"].astype(np.float64):
+    for t in stl_triangles(name):
         f = []
         for p in t:
             key = tuple(p)
@@ -102,12 +121,31 @@ def stl_mesh(name):
                 verts.append(tuple(float(c) for c in p))
             f.append(idx[key])
         faces.append(f)
-    nb = [set() for _ in verts]
-    for f in faces:
-        for i, j in itertools.permutations(range(3), 2):
-            if f[i] != f[j]:
-                nb[f[i]].add(f[j])
-    return verts, [sorted(s) for s in nb]
+    return verts, adjacency(len(verts), faces), faces
+
+
+def stl_raw_mesh(name):
+    """STL as a triangle soup, three vertices per facet and nothing merged (a
+    loader that pushes each facet's corners): every vertex's only neighbours
+    are its own facet's other two corners."""
+    tri = stl_triangles(name)
+    verts = [tuple(float(c) for c in p) for t in tri for p in t]
+    faces = [[3 * i, 3 * i + 1, 3 * i + 2] for i in range(len(tri))]
+    return verts, adjacency(len(verts), faces), faces
+
+
+def obj_mesh(name):
+    """The .obj twin (Meshlab export): its own vertex list and face indices."""
+    verts, faces = [], []
+    for line in open(MESHES + name + "_chull.obj"):
+        w = line.split()
+        if not w:
+            continue
+        if w[0] == "v":
+            verts.append(tuple(float(c) for c in w[1:4]))
+        elif w[0] == "f":
+            faces.append([int(x.split("/")[0]) - 1 for x in w[1:4]])
+    return verts, adjacency(len(verts), faces), faces
 
 
 def closest_weights(S):
@@ -136,10 +174,12 @@ def closest_weights(S):
     return best[1]
 
 
-def gjk_surface(verts, nbrs, R, t, brute, atol=1e-6, max_iter=100):
+def gjk_surface(verts, nbrs, R, t, brute, init=(0, 0, 0, 0), atol=1e-6, max_iter=100):
+    """One ConvexSurface: a CollisionCache whose 4-point simplex starts at the
+    mesh vertices `init` and is carried from call to call (src/Flash.jl:233-249)."""
     V = np.asarray(verts)
     W = V @ R.T + t
-    cache = [0, 0, 0, 0]  # any_inside: the mesh's first vertex
+    cache = list(init)
 
     def climb(start, d):
         s = V @ d
@@ -175,26 +215,67 @@ def gjk_surface(verts, nbrs, R, t, brute, atol=1e-6, max_iter=100):
     return f
 
 
-def section_gjk(out):
+LOADERS = {"stl merged": stl_mesh, "stl soup": stl_raw_mesh, "obj": obj_mesh}
+
+
+def gjk_variant(args):
+    """V, F and the volume of one emulation variant (a worker process)."""
+    loader, init, order, brute = args
     import flash
     from flash import Models
-    out.append("## 3. EnhancedGJK emulation, IRB140 call [(2226, 4460)]")
     m = Models.irb140()
     poses = flash.core.surface_poses(m, m.mechanism.zero_configuration())
     lb, ub, iso, res = cm.REGIONS["irb140"]
     axes = cm.grid_axes(lb, ub, res)
     nx, ny, nz = (len(a) for a in axes)
-    meshes = [stl_mesh(n) for n in LINKS]
-    for order, brute in (("z fastest", False), ("x fastest", False), ("z fastest", True)):
-        surfs = [gjk_surface(v, nb, p[:9].reshape(3, 3), p[9:], brute) for (v, nb), p in zip(meshes, poses)]
-        sweep = itertools.product(range(nx), range(ny), range(nz)) if order == "z fastest" else \
-            ((x, y, z) for z in range(nz) for y in range(ny) for x in range(nx))
-        vol = np.empty((nx, ny, nz))
-        for x, y, z in sweep:
-            p = np.array([axes[0][x], axes[1][y], axes[2][z]])
-            vol[x, y, z] = min(s(p) for s in surfs)
+    surfs = []
+    for name, p in zip(LINKS, poses):
+        v, nb, faces = LOADERS[loader](name)
+        start = (0, 0, 0, 0) if init == "vertex 1" else tuple(faces[0]) + (faces[0][0],)
+        surfs.append(gjk_surface(v, nb, p[:9].reshape(3, 3), p[9:], brute, start))
+    # GeometryTypes' SignedDistanceField fills vol[i, j, k] in `for i, j, k`
+    # order: the last index (z) innermost
+    sweep = itertools.product(range(nx), range(ny), range(nz)) if order == "z fastest" else \
+        ((x, y, z) for z in range(nz) for y in range(ny) for x in range(nx))
+    vol = np.empty((nx, ny, nz))
+    for x, y, z in sweep:
+        p = np.array([axes[0][x], axes[1][y], axes[2][z]])
+        vol[x, y, z] = min(s(p) for s in surfs)
+    return args, vol
+
+
+def section_gjk(out):
+    import multiprocessing as mp
+    out.append("## 3. EnhancedGJK emulation, IRB140 call [(2226, 4460)]")
+    out.append("   support: NeighborMesh hill climbing over the adjacency of the loader named, or brute")
+    out.append("   force (the control); init: the CollisionCache's 4-point simplex from the mesh's")
+    out.append("   vertex 1 or from its first face; sweep: the order the warm start is carried in")
+    out.append("   (z fastest = GeometryTypes' fill order). Differing nodes: grid nodes whose side of")
+    out.append("   the iso level differs from the exact SDF's (oracle), as (i, j, k) exact -> emulated.")
+    m, x, lb, ub, iso, res = cm.pinned_case("irb140")
+    axes = cm.grid_axes(lb, ub, res)
+    exact = cm.to_volume(oracle_parts(m, x)(cm.grid_points(axes)), axes)
+    out.append(f"   meshes: {', '.join(f'{n} ' + '/'.join(str(len(L(n)[0])) for L in LOADERS.values()) for n in LINKS)}"
+               " vertices (stl merged / stl soup / obj)")
+    variants = [(ld, init, order, False) for ld in LOADERS for init in ("vertex 1", "first face")
+                for order in ("z fastest", "x fastest")]
+    variants += [("stl merged", "vertex 1", "z fastest", True)]
+    with mp.get_context("fork").Pool(min(len(variants), max(1, (os.cpu_count() or 2) - 1))) as pool:
+        results = dict(pool.map(gjk_variant, variants))
+    for args in variants:
+        vol = results[args]
         V, F = cm.mesh_counts(vol - iso < 0.0)
-        out.append(f"  support {'brute force' if brute else 'hill climbing'}, sweep {order}: {V} / {F}   chi {V - F // 2}")
+        loader, init, order, brute = args
+        mark = "  <== reference" if (V, F) == cm.EXPECTED["irb140"] else ""
+        out.append(f"  {'brute force' if brute else loader:11s} init {init:10s} sweep {order}: "
+                   f"{V} / {F}   chi {V - F // 2}{mark}")
+        diff = np.argwhere((vol - iso < 0.0) != (exact - iso < 0.0))
+        err = np.abs(vol - exact)[exact > 0]
+        out.append(f"      {len(diff)} differing nodes; max |d_emul - d_exact| outside {err.max():.3g} m")
+        for i, j, k in diff[:12]:
+            out.append(f"      ({i}, {j}, {k}) {exact[i, j, k] - iso:+.4g} -> {vol[i, j, k] - iso:+.4g}")
+        if len(diff) > 12:
+            out.append(f"      ... {len(diff) - 12} more")
 
 
 def main():

@@ -132,6 +132,16 @@ function set_points!{T}(ctx::Context, pts::AbstractVector{SVector{3, T}})
                          ctx.ptr, reinterpret(Float64, P), length(P)), "set_points")
 end
 
+"One GPU's shard of the frame's cloud (the cost is a sum over points,
+src/gradientdescent.jl:32): the whole cloud is Hilbert-sorted on the device and
+this context keeps the contiguous range [first, last] (1-based, inclusive) of
+that order — the partition of DESIGN.md §6, balanced by fsdf_chunk_costs."
+function set_points_range!{T}(ctx::Context, pts::AbstractVector{SVector{3, T}}, first::Integer, last::Integer)
+    P = convert(Vector{SVector{3, Float64}}, pts)
+    check(ctx.ptr, ccall((:fsdf_set_points_range, lib), Cint, (Ptr{Void}, Ptr{Float64}, Int64, Int64, Int64),
+                         ctx.ptr, reinterpret(Float64, P), length(P), first - 1, last), "set_points_range")
+end
+
 "The posed scene in the state's number type (Float64 or Dual): per surface the
 world pose (R, t) (identity for RBF skins) and, per RBF skin, its world centres
 and solved coefficients u = (w; a; b)."

@@ -26,6 +26,7 @@
 #   hsweep:MODEL:SIZES[:EXTRA]  partition tiers / planned pass against cloud size (tools/hpart_sweep.py; MODEL
 #                   irb140 | arm_grid, SIZES and EXTRA arguments comma-separated) -> hpart_sweep_MODEL*.jsonl
 #   inflight:SIZES[:EXTRA]  independent passes in flight (tools/inflight_probe.py)  -> inflight.jsonl
+#   split:MODEL:N   speed-up of 2- / 4-wave chunk splits at N points (tools/split_speedup.py) -> split_speedup.jsonl
 #   c5sweep         BASELINE C5 precision sweep on the reference cloud (tools/precision_sweep.py) -> c5_sweep.json
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -159,6 +160,12 @@ for l in open('$O/hpart_sweep_$N.jsonl'):
       timeout -k 10 300 python tools/inflight_probe.py --sizes $S $X >> $O/inflight.jsonl 2>> $O/inflight.err \
         || { echo INFLIGHT FAILED; tail $O/inflight.err; exit 1; }
       cat $O/inflight.jsonl ;;
+    split:*)
+      # split:MODEL:POINTS — measured speed-up of 2- / 4-wave chunk splits (tools/split_speedup.py)
+      R=${step#split:}; M=${R%%:*}; P=${R#*:}
+      timeout -k 10 300 python tools/split_speedup.py --model $M --points $P >> $O/split_speedup.jsonl \
+        2>> $O/split_speedup.err || { echo SPLIT FAILED; tail $O/split_speedup.err; exit 1; }
+      tail -1 $O/split_speedup.jsonl | cut -c1-600 ;;
     c5sweep)
       timeout -k 10 300 python tools/precision_sweep.py --json $O/c5_sweep.json > $O/c5_sweep.log 2>&1 \
         || { echo C5 SWEEP FAILED; tail $O/c5_sweep.log; exit 1; }

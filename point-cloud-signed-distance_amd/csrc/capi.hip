@@ -976,6 +976,15 @@ static int run_planned(fsdf_ctx* c, const fsdf::PosedModel& P, const void* d_pts
   out.cost = nullptr;
   out.order = nullptr;
   fsdf::ChunkOutputs co = c->co;
+  // the split speed-ups behind the serial-equivalent durations (plan order,
+  // fsdf_chunk_costs, the shard rebalance): M64-class scenes (>= 32 hulls)
+  // measured 1.82-1.87x at 4 waves and 1.28-1.33x at 2 (tools/split_speedup.py,
+  // profiles/r05/split_speedup.jsonl); IRB140-class measurements scattered
+  // (4-way 1.22-1.53x) and their plan ran slower with them (profiles/r05/
+  // keyed_plan), so those keep round 4's 5/2 and 8/5
+  if (c->lm.K >= 32) {
+    co.r4n = 15; co.r4d = 8; co.r2n = 4; co.r2d = 3;
+  }
   const bool planned = c->plan_nc == nc && c->plan_grid > 0;
   co.plan = planned ? c->d_plan : nullptr;
   const int dparts = fsdf::hpart_parts(c->lm, n);

@@ -149,6 +149,10 @@ struct ChunkOutputs {
   uint32_t* dur = nullptr;     // [nc] serial-equivalent chunk durations (100 MHz ticks)
   const int32_t* plan = nullptr;  // [grid][4] workgroup plan (chunk | parts << 24, chunk, chunk, chunk), or null
   int dparts = 1;              // waves per chunk without a plan (4, 2 or 1)
+  // a split chunk's wall time x (num / den) is its serial-equivalent duration
+  // (the speed-up of the 4- / 2-wave split; set per model by the context:
+  // capi.hip run_planned, tools/split_speedup.py)
+  int r4n = 5, r4d = 2, r2n = 8, r2d = 5;
   int64_t cap = 0;             // chunks allocated: csum = ent + 24 cap, dense = ent + 25 cap (one allocation
                                // of (25 + 6 S) doubles per chunk: 1.6 KB per chunk at S = 64, i.e. 13 MB at
                                // the default 524,288-point planned window, 105 MB at kMaxPlanChunks)

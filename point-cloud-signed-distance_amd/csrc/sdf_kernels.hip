@@ -1926,9 +1926,10 @@ __global__ __launch_bounds__(kPassBlock) __attribute__((amdgpu_waves_per_eu(kPas
   emit_chunk_row<T>(px, py, pz, valid, best, bk, gx, gy, gz, cid, n, m, out, co, stage);
   if (co.dur && lane == 0) {
     // serial-equivalent duration: a split chunk's wall time scaled by the
-    // parallelism its split bought (measured ~2.5x at 4 waves, ~1.6x at 2)
+    // speed-up its split buys (ChunkOutputs::r4n / r4d, r2n / r2d)
     const uint64_t dt = __builtin_amdgcn_s_memrealtime() - t0_lds[wave];
-    const uint64_t est = parts == 4 ? (dt * 5) / 2 : (parts == 2 ? (dt * 8) / 5 : dt);
+    const uint64_t est = parts == 4 ? (dt * (uint64_t)co.r4n) / (uint64_t)co.r4d
+                                    : (parts == 2 ? (dt * (uint64_t)co.r2n) / (uint64_t)co.r2d : dt);
     co.dur[cid] = (uint32_t)(est < 0xffffffffull ? est : 0xffffffffull);
   }
 }

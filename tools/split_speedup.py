@@ -22,7 +22,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "point-cloud-signed-distance_amd"))
 
-RESCALE = {4: 5 / 2, 2: 8 / 5}  # the kernel's current constants
+# the serial-equivalent rescale the kernel applies to split chunks (capi.hip run_planned:
+# scenes with >= 32 hulls, fewer); round 4's build used 5/2 and 8/5 for both
+RESCALE = {True: {4: 15 / 8, 2: 4 / 3}, False: {4: 5 / 2, 2: 8 / 5}}
 
 
 def main():
@@ -42,9 +44,14 @@ def main():
     ctx.set_model([(s.hull.vertices, s.hull.faces, s.hull.planes) for s in m.surfaces])
     ctx.set_points(pts)
     nc = -(-len(pts) // 64)
+    # the round-4 default composition's counts (capi.hip kPlanDefault4 / 2, or the spare-slot rule),
+    # as fixed shares: the split set is then the heaviest chunks, whatever the keyed plan would pick
+    slots = 256 * 16
+    n4 = min(nc, max(96, max(0, slots - nc) // 3))
+    n2 = min(nc - n4, 192)
     one, split = [], []
     for r in range(a.rounds):
-        for shares, sink in (((0.0, 0.0), one), ((-1.0, -1.0), split)):
+        for shares, sink in (((0.0, 0.0), one), ((n4 / nc, n2 / nc), split)):
             ctx.set_plan(True, shares[0], shares[1], len(pts))
             for _ in range(20):  # first pass plans, the plan is rebuilt after 16
                 ctx.eval(poses)
@@ -52,14 +59,11 @@ def main():
     one = np.median(np.array(one), axis=0)
     split_d = np.median(np.array(split), axis=0)
     order = np.argsort(-one, kind="stable")
-    # the default composition's counts (capi.hip kPlanDefault4 / 2, or the spare-slot rule)
-    slots = 256 * 16
-    n4 = min(nc, max(96, max(0, slots - nc) // 3))
-    n2 = min(nc - n4, 192)
+    rescale = RESCALE[len(m.surfaces) >= 32]
     out = {"model": a.model, "points": len(pts), "chunks": nc, "rounds": a.rounds, "n4": n4, "n2": n2,
            "heaviest_one_wave_us": float(one.max()) / 100.0, "mean_one_wave_us": float(one.mean()) / 100.0}
     for parts, sel in ((4, order[:n4]), (2, order[n4:n4 + n2])):
-        wall = split_d[sel] / RESCALE[parts]
+        wall = split_d[sel] / rescale[parts]
         s = one[sel] / wall
         out[f"speedup_{parts}way"] = {"median": float(np.median(s)), "p10": float(np.percentile(s, 10)),
                                       "p90": float(np.percentile(s, 90)),

@@ -70,7 +70,6 @@ _PROTOS = {
     "fsdf_eval_device": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "fsdf_skin": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "fsdf_set_output_order": (c_int32, [c_void_p, c_int32]),
-    "fsdf_set_reduce_mode": (c_int32, [c_void_p, c_int32]),
     "fsdf_get_permutation": (c_int32, [c_void_p, c_void_p]),
     "fsdf_get_permutation_device": (c_int32, [c_void_p, c_void_p]),
     "fsdf_synchronize": (c_int32, [c_void_p]),
@@ -307,11 +306,6 @@ class Context:
         """Per-point outputs of eval / eval_device in resident (device, Hilbert)
         order — coalesced stores — or in caller order (the default)."""
         check(self._lib.fsdf_set_output_order(self._ctx, int(bool(resident))), self._ctx, "set_output_order")
-
-    def set_reduce_mode(self, fused: bool):
-        """The accumulator reduction inside the pass kernel (True, default) or
-        as a launch of its own (False); the same bits either way."""
-        check(self._lib.fsdf_set_reduce_mode(self._ctx, int(bool(fused))), self._ctx, "set_reduce_mode")
 
     def permutation(self) -> np.ndarray:
         """perm[i] = caller index of resident point i."""

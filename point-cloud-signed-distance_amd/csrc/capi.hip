@@ -718,7 +718,8 @@ static int adopt_points_device(fsdf_ctx* c, const double* d_src, int64_t n, void
 // (the Hilbert order of all n points with sort_points, else the caller's);
 // the permutation then holds the points' indices in the whole cloud
 // (fsdf_set_points_range). begin = 0, end = n: the whole cloud.
-static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool device_src, int64_t begin, int64_t end) {
+static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool device_src, int64_t begin, int64_t end,
+                           bool range_call = false) {
   if (!c) return FSDF_ERR_ARG;
   if (n < 0 || (n > 0 && !src)) return fail(c, FSDF_ERR_ARG, "set_points: bad buffer (n=%lld)", (long long)n);
   if (begin < 0 || end < begin || end > n)
@@ -821,7 +822,9 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
   // the caller may reuse its buffer once this returns
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   c->n = n;
-  c->ranged = ranged;
+  // (a range call keeps resident-order outputs even when its range is the
+  // whole cloud: the caller indexes them through the permutation)
+  c->ranged = ranged || range_call;
   c->plan_nc = -1;  // a new cloud: its first planned pass runs the default shape and measures
   return FSDF_OK;
 }
@@ -835,12 +838,12 @@ extern "C" int fsdf_set_points_device(fsdf_ctx* c, const double* d_xyz, int64_t 
 }
 
 extern "C" int fsdf_set_points_range(fsdf_ctx* c, const double* xyz, int64_t n, int64_t begin, int64_t end) {
-  return set_points_impl(c, xyz, n, false, begin, end);
+  return set_points_impl(c, xyz, n, false, begin, end, true);
 }
 
 extern "C" int fsdf_set_points_range_device(fsdf_ctx* c, const double* d_xyz, int64_t n, int64_t begin,
                                             int64_t end) {
-  return set_points_impl(c, d_xyz, n, true, begin, end);
+  return set_points_impl(c, d_xyz, n, true, begin, end, true);
 }
 
 static int ensure_partials(fsdf_ctx* c, int nblocks) {

@@ -95,11 +95,13 @@ def gather_chunk_costs(local_costs, group=None) -> np.ndarray:
 
 def allreduce_accum(accum, group=None, async_op=False):
     """Sum the per-rank accumulators in place (torch tensor, any device).
-    async_op=True returns the collective's work handle (None on one rank):
-    `.wait()` orders the caller's current stream (RCCL) or the host (gloo)
-    after it."""
+    async_op=True returns the collective's work handle (None without a process
+    group): `.wait()` orders the caller's current stream (RCCL) or the host
+    (gloo) after it. With a process group the collective runs at every world
+    size, one rank included (the RCCL branch's stream ordering is then the one
+    a multi-GPU run takes; tests/test_gpu_distributed.py::test_nccl_world1_pipelined)."""
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if dist.is_available() and dist.is_initialized():
         work = dist.all_reduce(accum, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
         return work if async_op else accum
     return None if async_op else accum

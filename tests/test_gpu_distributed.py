@@ -203,6 +203,13 @@ def _nccl_worker(port, out_dir):
             out[f"k{int(spatial)}"], out[f"d{int(spatial)}"], out[f"gr{int(spatial)}"] = k, d, gr
             out[f"idx{int(spatial)}"] = f.global_index() if spatial else np.arange(len(pts))
         out["backend"] = np.array(dist.get_backend())
+        # the functor's all-reduce is a real RCCL collective here, not skipped for one rank
+        from flash.distributed import allreduce_accum
+        probe = torch.ones(3, dtype=torch.float64, device="cuda")
+        work = allreduce_accum(probe, async_op=True)
+        out["work"] = np.array(work is not None)
+        work.wait()
+        out["probe"] = probe.cpu().numpy()
         np.savez(os.path.join(out_dir, "nccl.npz"), **out)
     finally:
         dist.destroy_process_group()
@@ -224,7 +231,7 @@ def test_nccl_world1_pipelined(tmp_path):
     p.join(timeout=240)
     assert p.exitcode == 0
     r = dict(np.load(os.path.join(tmp_path, "nccl.npz")))
-    assert str(r["backend"]) == "nccl"
+    assert str(r["backend"]) == "nccl" and bool(r["work"]) and np.array_equal(r["probe"], np.ones(3))
     m = Models.arm_grid()
     qt, qe = synthetic.perturbed_configuration(m, 65)
     pts = synthetic.depth_cloud(m, qt, 200003, seed=66, order="shuffled")

@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--points", type=int, default=1 << 20)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--splits", default="slice,spatial,balanced")
+    ap.add_argument("--no-plan", action="store_true", help="unplanned pass at every shard size (fsdf_set_plan off)")
     a = ap.parse_args()
     import torch
     import flash
@@ -55,6 +56,8 @@ def main():
     d_cloud = torch.as_tensor(cloud, device=dev)
     ctx = m.engine(device=0, precision=64, cull=True, sort_points=True)
     ctx.set_output_order(True)
+    if a.no_plan:
+        ctx.set_plan(False)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
@@ -122,7 +125,7 @@ def main():
             print(json.dumps({"W": w, "split": split, "points": n, "max_step_ms": max(steps),
                               "max_kernel_ms": max(kernels), "step_ms": steps, "kernel_ms": kernels,
                               "bounds": bounds, "heaviest_chunk_us": heavy, "summed_chunk_us": summed,
-                              "kernels": sorted(set(kinds)),
+                              "kernels": sorted(set(kinds)), "planned": not a.no_plan,
                               "projected_value": n / (max(steps) / 1e3)}), flush=True)
     return 0
 

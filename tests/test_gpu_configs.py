@@ -39,7 +39,7 @@ def _c4_state():
     return m, qt, np.asarray(qe, np.float64)
 
 
-def _c4_worker(rank, world, port, cloud_path, out_dir):
+def _c4_worker(rank, world, port, cloud_path, out_dir, spatial=False):
     import sys
     from conftest import ROOT
     sys.path.insert(0, os.path.join(ROOT, "point-cloud-signed-distance_amd"))
@@ -50,20 +50,29 @@ def _c4_worker(rank, world, port, cloud_path, out_dir):
     try:
         m, _, x = _c4_state()
         cloud = np.load(cloud_path, mmap_mode="r")
-        a, b = shard_range(len(cloud), rank, world)
-        f = ShardedCostFunctor(m, np.ascontiguousarray(cloud[a:b]), rank=rank, world=world, device=0)
+        if spatial:  # the whole cloud on every rank, a range of its Hilbert order kept
+            f = ShardedCostFunctor(m, np.ascontiguousarray(cloud), rank=rank, world=world, device=0, spatial=True)
+            a, b = f.range
+        else:
+            a, b = shard_range(len(cloud), rank, world)
+            f = ShardedCostFunctor(m, np.ascontiguousarray(cloud[a:b]), rank=rank, world=world, device=0)
         x2 = x.copy()
         x2[1] += 2e-3
         f.value_and_gradient(x2)  # a pass at another configuration first (resident cloud, schedule)
         c, g = f.value_and_gradient(x)
         acc = f.accum.cpu().numpy()
         k, d, gr = f.per_point(x)
-        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), c=c, g=g, acc=acc, d=d, k=k, gr=gr, a=a, b=b)
+        idx = f.global_index() if spatial else np.arange(a, b)
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), c=c, g=g, acc=acc, d=d, k=k, gr=gr, a=a, b=b, idx=idx)
     finally:
         dist.destroy_process_group()
 
 
-def test_c4_ten_million_points_sharded_over_eight_ranks(tmp_path):
+@pytest.mark.parametrize("spatial", [False, True])
+def test_c4_ten_million_points_sharded_over_eight_ranks(spatial, tmp_path):
+    """Slices of the caller's order (round 4) and density-preserving ranges of
+    the whole cloud's Hilbert order (spatial=True): per-point outputs placed at
+    their whole-cloud indices are the single context's bit for bit."""
     import multiprocessing as mp
     from flash import synthetic
     from flash.gradientdescent import CostFunctor
@@ -73,7 +82,8 @@ def test_c4_ten_million_points_sharded_over_eight_ranks(tmp_path):
     np.save(path, cloud)
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_c4_worker, args=(r, C4_RANKS, port, path, str(tmp_path))) for r in range(C4_RANKS)]
+    procs = [ctx.Process(target=_c4_worker, args=(r, C4_RANKS, port, path, str(tmp_path), spatial))
+             for r in range(C4_RANKS)]
     for p in procs:
         p.start()
     for p in procs:
@@ -91,9 +101,15 @@ def test_c4_ten_million_points_sharded_over_eight_ranks(tmp_path):
         assert np.allclose(r["acc"], acc1, rtol=1e-9, atol=1e-9 * np.abs(acc1).max())
         assert r["c"] == pytest.approx(c1, rel=1e-9)
         assert np.allclose(r["g"], g1, rtol=1e-7, atol=1e-7 * np.abs(g1).max())
-    assert np.array_equal(np.concatenate([r["k"] for r in res]), k1)
-    assert np.array_equal(np.concatenate([r["d"] for r in res]), d1)
-    assert np.array_equal(np.concatenate([r["gr"] for r in res]), gr1)
+    idx = np.concatenate([r["idx"] for r in res])
+    assert np.array_equal(np.sort(idx), np.arange(C4_POINTS))  # the shards partition the cloud
+    k = np.empty_like(k1)
+    d = np.empty_like(d1)
+    gr = np.empty_like(gr1)
+    k[idx] = np.concatenate([r["k"] for r in res])
+    d[idx] = np.concatenate([r["d"] for r in res])
+    gr[idx] = np.concatenate([r["gr"] for r in res])
+    assert np.array_equal(k, k1) and np.array_equal(d, d1) and np.array_equal(gr, gr1)
     # cost = Σ d² over all 10M points (the reduction saw every shard once)
     assert c1 == pytest.approx(float(np.dot(d1, d1)), rel=1e-9)
 

@@ -435,6 +435,11 @@ constexpr int64_t kPlanMaxSmall = 393216;
 // vs 0.0448 — the planned reduction's second launch is not paid back)
 constexpr int64_t kPlanMinPoints = 98304;
 constexpr int kAliasBlock = kPassBlock;
+// scene_eval's best-first seed takes max(sphere, box) lower bounds below this
+// many hulls and the sphere bound alone at or above it (round 5 A/B, DESIGN §7:
+// sphere-only at M64 = 64 hulls 0.0489 -> 0.0460 ms pass at 2^17, 0.0908 ->
+// 0.0899 at 2^20; at C2 = 7 hulls 0.0680 -> 0.0687, so the box stays there)
+constexpr int kSeedBoxMaxHulls = 32;
 
 // The one diagnostic build (-DFSDF_WAVE_TIMES=1, tools/wave_times.py): a
 // per-wave timeline with per-phase 100 MHz clocks and event counts; every hook
@@ -1318,8 +1323,11 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
         const float dx = pxf - sp[0], dy = pyf - sp[1], dz = pzf - sp[2];
         const float dist2 = __builtin_fmaf(dx, dx, __builtin_fmaf(dy, dy, dz * dz));
         ub2 = fminf(ub2, dist2);
-        // seed: the least lower bound (sphere or box)
-        const float lb = fmaxf(__builtin_sqrtf(dist2) - sp[3], box_lower(ht[k], pxf, pyf, pzf));
+        // seed: the least lower bound — sphere, and on scenes of few hulls also
+        // box (a heuristic only: every candidate is still searched, so either
+        // seed gives the same bits; kSeedBoxMaxHulls)
+        float lb = __builtin_sqrtf(dist2) - sp[3];
+        if (K < kSeedBoxMaxHulls) lb = fmaxf(lb, box_lower(ht[k], pxf, pyf, pzf));
         if (lb < lb_min) { lb_min = lb; kseed = k; }
       }
     }

@@ -493,3 +493,48 @@ def test_passes_in_flight_bit_identical(m64, ctx_factory):
                 assert np.array_equal(k, want[s][2][0]) and np.array_equal(d, want[s][2][1])
                 assert np.array_equal(g, want[s][2][2])
         del d_pts
+
+
+@pytest.mark.parametrize("sort_points", [True, False])
+def test_point_ranges_edge_cases(m64, ctx_factory, sort_points):
+    """fsdf_set_points_range at chunk-unaligned, single-point and empty ranges:
+    bad ranges fail with FSDF_ERR_ARG and leave the context usable; an empty
+    range gives zero cost and wrenches; every other range's per-point outputs
+    equal the whole cloud's at the indices permutation() names (the Hilbert
+    order's with sort_points, the caller's without), the ranges' permutations
+    partition the cloud, and their costs and wrenches sum to the whole cloud's."""
+    import flash
+    from flash import synthetic
+    from flash._lib import FlashNativeError
+    qt, qe = synthetic.perturbed_configuration(m64, 731)
+    poses = flash.hull_poses(m64, qe)
+    n = 70001
+    pts = synthetic.depth_cloud(m64, qt, n, seed=732, order="shuffled")
+    whole = ctx_factory(m64, sort_points=sort_points)
+    whole.set_points(pts)
+    whole.set_output_order(False)
+    c_all, acc_all, (ka, da, ga) = whole.eval(poses, per_point=True)
+    ctx = ctx_factory(m64, sort_points=sort_points)
+    for b, e in ((-1, 10), (10, 5), (0, n + 1)):
+        with pytest.raises(FlashNativeError):
+            ctx.set_points_range(pts, b, e)
+    ctx.set_points_range(pts, 500, 500)
+    cost, acc, _ = ctx.eval(poses)
+    assert cost == 0.0 and not acc.any()
+    cuts = [0, 1, 37, 64 * 100 + 5, 64 * 500, n - 1, n]
+    seen = np.zeros(n, np.int32)
+    c_sum, acc_sum = 0.0, np.zeros_like(acc_all)
+    for b, e in zip(cuts[:-1], cuts[1:]):
+        ctx.set_points_range(pts, b, e)
+        cost, acc, (k, d, g) = ctx.eval(poses, per_point=True)
+        perm = ctx.permutation()
+        assert len(perm) == e - b
+        if not sort_points:
+            assert np.array_equal(perm, np.arange(b, e))
+        seen[perm] += 1
+        assert np.array_equal(k, ka[perm]) and np.array_equal(d, da[perm]) and np.array_equal(g, ga[perm])
+        c_sum += cost
+        acc_sum += acc
+    assert (seen == 1).all()
+    assert c_sum == pytest.approx(c_all, rel=RTOL_SUM)
+    assert np.allclose(acc_sum, acc_all, rtol=1e-9, atol=1e-9 * max(1.0, np.abs(acc_all).max()))

@@ -198,7 +198,7 @@ def main():
 
     import flash
     from flash import Models, synthetic
-    from flash.distributed import allreduce_accum, gather_chunk_costs, shard_range, spatial_bounds
+    from flash.distributed import allreduce_accum, gather_chunk_costs, plan_window, shard_range, spatial_bounds
 
     model_name, default_points, scaling, workload = CONFIGS[args.config]
     if args.global_points is not None:
@@ -271,7 +271,7 @@ def main():
 
         if shard_bounds is not None:  # (flash.distributed.ShardedCostFunctor._plan_window: measured chunk costs)
             for cx in ctxs:
-                cx.set_plan(True, -1.0, -1.0, int(min(max(2 * -(-len(pts_host) // world), 98304), 524288)))
+                cx.set_plan(True, -1.0, -1.0, plan_window(len(pts_host), world))
 
         def upload(cx):
             if shard_bounds is not None:

@@ -38,6 +38,22 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
 
 
 CHUNK = 64  # points per wave-chunk of the pass (and per entry of fsdf_chunk_costs)
+PLAN_TOP = 524288  # the planned pass's default window top for M64-class scenes (sdf_kernels.hip kPlanMaxFull)
+
+
+def plan_window(n: int, world: int) -> int:
+    """fsdf_set_plan max_points for a spatial shard of an n-point cloud over
+    `world` ranks: the planned pass up to twice the average shard, also below
+    the default window's 98,304-point bottom (its per-chunk durations are what
+    rebalance() splits by; there it measured within 3 % of the unplanned 4-way
+    tier). One rank keeps the default top (524,288: the
+    whole 2^20 cloud runs the unplanned pass, whose step is shorter); more ranks
+    let a rebalanced range grow 25 % past the average shard, also above that top
+    — at two ranks a range of 530,112 points fell out of the window into the
+    unplanned pass, 0.0643 ms against 0.0523 planned."""
+    share = -(-n // max(world, 1))
+    top = PLAN_TOP if world <= 1 else max(PLAN_TOP, -(-5 * share // 4))
+    return int(min(max(2 * share, 98304), top))
 
 
 def spatial_bounds(n: int, world: int, chunk_costs=None) -> list[tuple[int, int]]:
@@ -264,13 +280,9 @@ class ShardedCostFunctor:
         return c, chain_gradient(self.manipulator, x, acc, self.weight, solves)
 
     def _plan_window(self, ctx):
-        """Spatial shards run the planned pass up to twice the average shard
-        (at most 524,288 points, the default window's top): its per-chunk
-        durations are what rebalance() splits by, also for shards below the
-        default window's 98,304-point bottom (there it measured within 3 % of
-        the unplanned 4-way tier)."""
+        """Spatial shards run the planned pass over plan_window()'s range."""
         if hasattr(ctx, "set_plan"):
-            ctx.set_plan(True, -1.0, -1.0, int(min(max(2 * -(-self.cloud_n // self.world), 98304), 524288)))
+            ctx.set_plan(True, -1.0, -1.0, plan_window(self.cloud_n, self.world))
 
     def global_index(self) -> np.ndarray:
         """The whole cloud's index of each resident point (spatial shards; for

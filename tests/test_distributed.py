@@ -270,6 +270,21 @@ def test_spatial_bounds_partition_and_balance():
                     assert max(per) <= costs.sum() / w + costs.max() + 1e-9
 
 
+def test_plan_window():
+    """The planned pass's window for spatial shards (bench.py and
+    ShardedCostFunctor share it): one rank keeps the default top, so the whole
+    2^20 cloud runs unplanned; more ranks cover twice the average shard, and a
+    rebalanced range 25 % past the average shard even above that top."""
+    from flash.distributed import PLAN_TOP, plan_window
+    n = 1 << 20
+    assert plan_window(n, 1) == PLAN_TOP == 524288
+    assert plan_window(n, 2) == 655360 and plan_window(n, 2) >= 530112  # round 5's rebalanced W = 2 range
+    assert plan_window(n, 4) == 524288 and plan_window(n, 8) == 262144
+    assert plan_window(1000, 8) == 98304 and plan_window(0, 1) == 98304
+    for w in (2, 3, 4, 8, 16):
+        assert plan_window(n, w) >= -(-n // w) * 5 // 4
+
+
 def _spatial_worker(rank, world, port, q, name):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))

@@ -46,7 +46,7 @@ def main():
     import torch
     import flash
     from flash import Models, synthetic
-    from flash.distributed import shard_range, spatial_bounds
+    from flash.distributed import plan_window, shard_range, spatial_bounds
     dev = torch.device("cuda", 0)
     m = Models.arm_grid()
     qt, qe = synthetic.perturbed_configuration(m, a.seed)
@@ -74,9 +74,13 @@ def main():
     def load(split, bounds, r):
         b, e = bounds[r]
         if split == "slice":
+            if not a.no_plan:  # (the model's default window, as bench.py's --slice-shards)
+                ctx.set_plan(True, -1.0, -1.0, -1)
             sl = torch.as_tensor(np.ascontiguousarray(cloud[b:e]), device=dev)
             ctx.set_points_device(sl.data_ptr(), e - b)
         else:
+            if not a.no_plan:  # (the window bench.py and ShardedCostFunctor give spatial shards)
+                ctx.set_plan(True, -1.0, -1.0, plan_window(n, len(bounds)))
             ctx.set_points_range_device(d_cloud.data_ptr(), n, b, e)
 
     def step_rank():

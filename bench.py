@@ -189,10 +189,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         # FSDF_BENCH_BACKEND / FSDF_BENCH_DEVICE: rehearsal of the N>1 path on a
-        # one-GPU box (gloo, every rank on one device); RCCL ("nccl") otherwise
-        dist.init_process_group(os.environ.get("FSDF_BENCH_BACKEND", "nccl"))
+        # one-GPU box (gloo, every rank on one device); RCCL ("nccl") otherwise.
+        # The device is set before the process group exists (RCCL binds to it)
         local = int(os.environ.get("FSDF_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group(os.environ.get("FSDF_BENCH_BACKEND", "nccl"))
     dev = torch.device("cuda", local)
     backend = dist.get_backend() if world > 1 else None
 

@@ -106,6 +106,9 @@ struct fsdf_ctx {
   int32_t* d_perm = nullptr;        // resident i -> caller index (sorted clouds)
   int64_t perm_cap = 0;
   float* d_chunk_ws = nullptr;       // [ceil(n/64)][4] bounding sphere per 64-point chunk
+  uint8_t* d_prior = nullptr;        // [n] each resident point's nearest surface in the last pass (seed hint)
+  int64_t prior_cap = 0;
+  bool prior_ok = false;             // d_prior was written by a pass over the current resident cloud
   int64_t chunk_ws_cap = 0;          // chunks
   fsdf::SortScratch sort;            // per-frame sort scratch (grown only)
   double* d_staging = nullptr;       // host-source clouds land here first
@@ -289,6 +292,7 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   dfree(c->d_pts);
   dfree(c->d_perm);
   dfree(c->d_chunk_ws);
+  dfree(c->d_prior);
   dfree(c->d_staging);
   dfree(c->d_range_pts);
   dfree(c->d_range_perm);
@@ -818,7 +822,14 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
       c->chunk_ws_cap = nc;
     }
     HIPCHECK(c, fsdf::launch_chunk_spheres(c->precision, c->d_pts, n, nc, c->d_chunk_ws, c->stream));
+    if (c->prior_cap < n) {  // (the previous frame's passes are done: synchronised above)
+      dfree(c->d_prior);
+      c->prior_cap = 0;
+      HIPCHECK(c, hipMalloc(&c->d_prior, (size_t)n));
+      c->prior_cap = n;
+    }
   }
+  c->prior_ok = false;  // a new cloud: its first pass seeds from the bounds
   // the caller may reuse its buffer once this returns
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   c->n = n;
@@ -1016,6 +1027,9 @@ static int run_planned(fsdf_ctx* c, const fsdf::PosedModel& P, const void* d_pts
   return FSDF_OK;
 }
 
+#ifndef FSDF_PRIOR_SEEDS
+#define FSDF_PRIOR_SEEDS 1
+#endif
 // schedule: resident-cloud passes (repeated over the same cloud) launch their
 // workgroups heaviest-first by the previous pass's durations
 static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t n, double* d_accum,
@@ -1037,6 +1051,13 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
   out.perm = d_perm;
   out.stats = c->stats_on ? c->d_stats : nullptr;
   out.chunk_ws = FSDF_CHUNK_WS && d_pts == c->d_pts && n == c->n ? c->d_chunk_ws : nullptr;  // resident cloud only
+  // the previous pass's nearest surfaces as seeds (resident cloud, hull-only
+  // scenes of <= 64 surfaces; fsdf_internal.h PassOutputs::prior_in)
+  const bool prior = FSDF_PRIOR_SEEDS && d_pts == c->d_pts && n == c->n && n > 0 && c->d_prior &&
+                     c->prior_cap >= n && c->lm.R == 0 && c->lm.S <= 64;
+  out.prior_out = prior ? c->d_prior : nullptr;
+  out.prior_in = prior && c->prior_ok ? c->d_prior : nullptr;
+  if (prior) c->prior_ok = true;  // (stream-ordered: the next pass reads what this one writes)
   // planned window: (default min, model's default max], or (0, max_points] when set
   const int64_t plan_max = c->plan_max_points >= 0 ? c->plan_max_points : fsdf::planned_default_max_points(c->lm);
   const int64_t plan_min = c->plan_max_points >= 0 ? 0 : fsdf::planned_default_min_points();

@@ -137,6 +137,12 @@ struct PassOutputs {
   // optional [n64/64][4] f32 bounding sphere of each 64-point chunk of the
   // resident cloud (launch_chunk_spheres at set_points; pose-independent)
   const float* chunk_ws = nullptr;
+  // optional [n] nearest surface of each resident point in the previous pass
+  // over this cloud (hull-only scenes of <= 64 surfaces): read as the point's
+  // best-first seed (a heuristic — any seed gives the same bits), rewritten by
+  // this pass. prior_in is null on a cloud's first pass.
+  const uint8_t* prior_in = nullptr;
+  uint8_t* prior_out = nullptr;
 };
 
 // Planned pass (sdf_kernels.hip planned_pass_kernel): per-chunk partial rows

@@ -1242,7 +1242,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
                                            const HullRow* __restrict__ ht, float smax, T* __restrict__ lw,
                                            unsigned long long* __restrict__ stats, T& best, int& bk, T& gx, T& gy,
                                            T& gz, const F4* __restrict__ cws = nullptr, uint64_t partmask = ~0ull,
-                                           double* shbest = nullptr) {
+                                           double* shbest = nullptr, int prior = -1) {
   // partmask (hull-partitioned pass, pass_kernel HPART): this wave evaluates
   // only the hulls whose bit (k & 63) is set; culling and the upper bound
   // still use every hull
@@ -1332,6 +1332,12 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
       }
     }
   }
+  // the point's nearest surface in the previous pass over this cloud, when
+  // known (PassOutputs::prior_in), is its seed instead: tracking passes move
+  // the model little, so it is usually this pass's nearest too, and `best` is
+  // tight after the first evaluation (any seed gives the same bits)
+  const bool prior_ok = CULL && !RBF && SLOTS == 1 && prior >= 0 && prior < K && ((partmask >> (prior & 63)) & 1);
+  if (prior_ok) kseed = prior;
   const float ub = __builtin_sqrtf(ub2);
   tw = wt_add(4, tw);
 #pragma unroll
@@ -1421,7 +1427,7 @@ __device__ __forceinline__ void scene_eval(T px, T py, T pz, bool valid, const P
   // kernel's code to ~40 KB): first each lane's seed hull (Phase B, one
   // evaluation per distinct seed in the wave, so that `best` is tight), then
   // the remaining candidates in index order (Phase C).
-  uint64_t pend = (CULL && K > 0) ? __ballot(valid && lb_min < __builtin_huge_valf()) : 0ull;
+  uint64_t pend = (CULL && K > 0) ? __ballot(valid && (lb_min < __builtin_huge_valf() || prior_ok)) : 0ull;
   int slot = -1;      // Phase C slot; -1 while seeds are pending
   uint64_t cm = 0ull;  // Phase C candidates left in `slot`
   for (;;) {
@@ -1523,6 +1529,7 @@ __device__ __forceinline__ uint64_t emit_chunk(T px, T py, T pz, bool valid, T b
   }
 
   {
+    if (out.prior_out && valid) out.prior_out[i] = (uint8_t)bk;  // the next pass's seed hint (resident order)
     if (out.perm) {  // caller order: scattered through the sort permutation
       if (valid) {
         const int64_t o = out.perm[i];
@@ -1678,6 +1685,7 @@ __global__ __launch_bounds__(NB) __attribute__((
       if (part == 0) ((volatile double*)shb)[lane] = __builtin_huge_val();
       __syncthreads();
     }
+    const int prior = (out.prior_in && valid) ? (int)out.prior_in[i] : -1;
     scene_eval<T, SLOTS, CULL, RBF, ALIAS, kParts>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy,
                                                    gz, cws,
                                                    HPART ? ((kParts == 8 ? 0x0101010101010101ull
@@ -1685,7 +1693,7 @@ __global__ __launch_bounds__(NB) __attribute__((
                                                                                         : 0x5555555555555555ull))
                                                             << part)
                                                          : ~0ull,
-                                                   shb);
+                                                   shb, prior);
     if constexpr (HPART) {
       // the chunk's waves' results meet in their stages; part 0 keeps the
       // lexicographic (d, k) minimum per point
@@ -1908,8 +1916,9 @@ __global__ __launch_bounds__(kPassBlock) __attribute__((amdgpu_waves_per_eu(kPas
     const uint64_t pm = parts == 4 ? (0x1111111111111111ull << part)
                                    : (parts == 2 ? (0x5555555555555555ull << part) : ~0ull);
     const F4* cws = out.chunk_ws ? (const F4*)out.chunk_ws + cid : nullptr;
+    const int prior = (out.prior_in && valid) ? (int)out.prior_in[base + lane] : -1;
     scene_eval<T, 1, CULL, false, true, 0>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy, gz,
-                                           cws, pm, shb);
+                                           cws, pm, shb, prior);
   }
   if (parts > 1) {
     // the chunk's waves' results meet in their stages; part 0 keeps the

@@ -538,3 +538,26 @@ def test_point_ranges_edge_cases(m64, ctx_factory, sort_points):
     assert (seen == 1).all()
     assert c_sum == pytest.approx(c_all, rel=RTOL_SUM)
     assert np.allclose(acc_sum, acc_all, rtol=1e-9, atol=1e-9 * max(1.0, np.abs(acc_all).max()))
+
+
+@pytest.mark.parametrize("n", [20011, 131077, 530000])
+def test_prior_seeds_change_no_bits(m64, ctx_factory, n):
+    """Passes after a cloud's first seed each point's search from its nearest
+    surface in the previous pass (PassOutputs::prior_in): every output — cost,
+    accumulator, k*, d*, ∇d* — equals a first pass at the same configuration
+    (no prior) bit for bit, on the 4-way tier, the planned pass and the
+    one-wave grid; a new cloud (set_points) drops the prior."""
+    import flash
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(m64, 901)
+    poses = [flash.hull_poses(m64, qe + d) for d in (0.0, 2e-3, -3e-3, 2e-3)]
+    pts = synthetic.depth_cloud(m64, qt, n, seed=902, order="shuffled")
+    warm = ctx_factory(m64, sort_points=True)
+    warm.set_points(pts)
+    runs = [warm.eval(p, per_point=True) for p in poses]
+    cold = ctx_factory(m64, sort_points=True)
+    for p, (c1, a1, (k1, d1, g1)) in zip(poses, runs):
+        cold.set_points(pts)  # a first pass each time
+        c0, a0, (k0, d0, g0) = cold.eval(p, per_point=True)
+        assert c1 == c0 and np.array_equal(a1, a0)
+        assert np.array_equal(k1, k0) and np.array_equal(d1, d0) and np.array_equal(g1, g0)

@@ -68,6 +68,7 @@ ITERS_PER_FRAME = 30           # src/tracking.jl:10-13 default NaiveSolver itera
 
 SERIAL = {}  # run_cloud's serial re-run of the timed passes (one at a time)
 SIDE_RES = {}  # run_cloud's N = 1 side figures (dependent step, passes in flight)
+REGROUP_MS = None  # run_cloud's per-frame fsdf_regroup_points time (ms per context)
 
 CONFIGS = {
     # name: (model, default points, scaling, description)
@@ -107,6 +108,8 @@ def parse():
                    help="input order of the synthetic cloud (shuffled = adversarial)")
     p.add_argument("--no-sort", action="store_true", help="keep the input order resident (no Hilbert sort)")
     p.add_argument("--no-per-point", action="store_true", help="reduction-only pass (no per-point outputs)")
+    p.add_argument("--no-regroup", action="store_true",
+                   help="keep the Hilbert resident order (no fsdf_regroup_points after the frame's first passes)")
     p.add_argument("--caller-order", action="store_true",
                    help="per-point outputs scattered to the caller's order (default: resident order, coalesced; "
                         "the permutation is fsdf_get_permutation)")
@@ -200,6 +203,7 @@ def main():
 
     import flash
     from flash import Models, synthetic
+    from flash._lib import FlashNativeError
     from flash.distributed import allreduce_accum, gather_chunk_costs, plan_window, shard_range, spatial_bounds
 
     model_name, default_points, scaling, workload = CONFIGS[args.config]
@@ -349,6 +353,32 @@ def main():
                 for cx in ctxs:
                     upload(cx)
                 for i in range(16 * C):  # a new range: its first passes plan anew
+                    c = i % C
+                    ctxs[c].eval_device(poses[(i // C) & 1], accums[c][(i // C) & 1].data_ptr(), *outs[c])
+                torch.cuda.synchronize()
+        # once per frame, after its first passes: the resident cloud regrouped by
+        # each point's last nearest surface (fsdf_regroup_points; hull-only
+        # scenes with a permutation — otherwise refused and skipped), timed and
+        # charged to the frame beside set_points
+        global REGROUP_MS
+        REGROUP_MS = None
+        if not args.no_regroup:
+            torch.cuda.synchronize()
+            try:
+                for cx in ctxs:  # (the first call also grows the context's sort scratch)
+                    cx.regroup_points()
+                for c in range(C):  # a frame's regroup follows a pass: time one such, steady state
+                    ctxs[c].eval_device(poses[0], accums[c][0].data_ptr(), *outs[c])
+                torch.cuda.synchronize()
+                t_r = time.perf_counter()
+                for cx in ctxs[:C]:
+                    cx.regroup_points()
+                torch.cuda.synchronize()
+                REGROUP_MS = (time.perf_counter() - t_r) * 1e3 / C
+            except FlashNativeError:
+                REGROUP_MS = None
+            if REGROUP_MS is not None:
+                for i in range(16 * C):  # other chunks: their first passes plan and order anew
                     c = i % C
                     ctxs[c].eval_device(poses[(i // C) & 1], accums[c][(i // C) & 1].data_ptr(), *outs[c])
                 torch.cuda.synchronize()
@@ -528,7 +558,7 @@ def main():
                 if executed and executed.get("valu_insts_per_launch"):
                     issue = executed["valu_insts_per_launch"] * CYCLES_PER_WAVE_OP / (
                         SIMDS * CLOCK_HZ * kernel_avg_ms / 1e3)
-        frame_ms = set_points_ms + ITERS_PER_FRAME * ms_per_step
+        frame_ms = set_points_ms + (REGROUP_MS or 0.0) + ITERS_PER_FRAME * ms_per_step
         out = {
             "metric": "SDF+grad point-evals/sec, 1M-pt cloud x 64-prim model (M64)",
             "value": value,
@@ -586,7 +616,13 @@ def main():
                                         "host FK and chain rule are in full_iteration_ms)"),
                 "set_points_ms_per_frame": set_points_ms,
                 "frame_ms_at_30_iterations": frame_ms,
-                "frame_note": "set_points (H2D-resident copy + Hilbert sort) once + 30 residual passes",
+                "regroup_ms_per_frame": REGROUP_MS,
+                "regroup_note": ("fsdf_regroup_points once per frame after its first passes: the resident cloud "
+                                 "grouped by each point's last nearest surface (Hilbert order within a group); "
+                                 "the timed passes run on it, seeded from the previous pass's k* (per-point results "
+                                 "unchanged)" if REGROUP_MS is not None else "not applied (--no-regroup, an RBF "
+                                 "scene or an unsorted cloud)"),
+                "frame_note": "set_points (H2D-resident copy + Hilbert sort) once + regroup once + 30 residual passes",
                 "full_iteration_ms": iter_ms,
                 "full_iteration_note": "CostFunctor.value_and_gradient on the resident cloud (fsdf_value_and_gradient: "
                                        "host FK + surface poses, pass, accumulator read-back, chain rule; rank 0, "

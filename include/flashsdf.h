@@ -260,6 +260,19 @@ int fsdf_set_points_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n);
 int fsdf_set_points_range(fsdf_ctx* ctx, const double* xyz, int64_t n, int64_t begin, int64_t end);
 int fsdf_set_points_range_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n, int64_t begin, int64_t end);
 int fsdf_num_points(const fsdf_ctx* ctx, int64_t* n_out);
+/* Regroup the resident cloud by each point's nearest surface in the last pass
+ * over it, keeping the current (Hilbert) order within each surface's group: a
+ * stable device sort, once per frame after its first pass. The reference has no
+ * counterpart — its track! loop (src/tracking.jl:8-27) evaluates the cost of
+ * one frame's cloud over and over (src/gradientdescent.jl:43), which is what
+ * this exploits: the passes seed each point from its last nearest surface, and
+ * a 64-point chunk whose points share one evaluates fewer hulls. Per-point
+ * results are unchanged; the cost and wrench sums change in rounding only (the
+ * chunks group other points). The resident order changes: re-read
+ * fsdf_get_permutation for FSDF_ORDER_RESIDENT outputs. Requires a sorted
+ * (sort_points) or ranged cloud and a pass over it (hull-only scenes of <= 64
+ * surfaces); asynchronous on the context stream. */
+int fsdf_regroup_points(fsdf_ctx* ctx);
 
 /* One residual pass over the resident cloud (synchronous, host buffers).
  * poses: [K][12] host. Outputs may be NULL when not wanted:

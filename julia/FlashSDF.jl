@@ -142,6 +142,13 @@ function set_points_range!{T}(ctx::Context, pts::AbstractVector{SVector{3, T}}, 
                          ctx.ptr, reinterpret(Float64, P), length(P), first - 1, last), "set_points_range")
 end
 
+"Once per frame, after its first cost evaluation: regroup the resident cloud by
+each point's nearest surface in that pass (fsdf_regroup_points). The frame's
+later evaluations (the rest of track!'s iterations, src/tracking.jl:8-27) give
+the same per-point results and evaluate fewer hulls per 64-point chunk."
+regroup_points!(ctx::Context) = check(ctx.ptr, ccall((:fsdf_regroup_points, lib), Cint, (Ptr{Void},), ctx.ptr),
+                                      "regroup_points")
+
 "The posed scene in the state's number type (Float64 or Dual): per surface the
 world pose (R, t) (identity for RBF skins) and, per RBF skin, its world centres
 and solved coefficients u = (w; a; b)."

@@ -857,6 +857,31 @@ extern "C" int fsdf_set_points_range_device(fsdf_ctx* c, const double* d_xyz, in
   return set_points_impl(c, d_xyz, n, true, begin, end, true);
 }
 
+// Regroup the resident cloud by each point's nearest surface in the last pass
+// (a stable device sort on PassOutputs::prior_out's bytes: the Hilbert order
+// kept within each group), so that a chunk's points share their surface and
+// the seeded passes evaluate fewer hulls per chunk. Per-point results do not
+// change; sums change in rounding only (other chunks). Stream-ordered after
+// the passes already queued.
+extern "C" int fsdf_regroup_points(fsdf_ctx* c) {
+  if (!c) return FSDF_ERR_ARG;
+  if (c->n == 0) return FSDF_OK;
+  if (!c->d_perm)
+    return fail(c, FSDF_ERR_STATE, "regroup_points: needs a sorted (sort_points) or ranged resident cloud");
+  if (!c->prior_ok || !c->d_prior || c->prior_cap < c->n)
+    return fail(c, FSDF_ERR_STATE, "regroup_points: run a pass over the resident cloud first (hull-only scenes)");
+  HIPCHECK(c, hipSetDevice(c->device));
+  void* pts = c->d_pts;
+  hipError_t e = fsdf::regroup_points(&pts, &c->pts_cap, c->n, c->precision, c->d_perm, c->d_prior, c->sort, c->stream);
+  c->d_pts = pts;
+  if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "regroup_points: %s", hipGetErrorString(e));
+  const int64_t nc = ((c->n + 63) / 64 + 3) & ~(int64_t)3;
+  HIPCHECK(c, fsdf::launch_chunk_spheres(c->precision, c->d_pts, c->n, nc, c->d_chunk_ws, c->stream));
+  c->plan_nc = -1;       // other chunks: the next planned pass measures anew
+  c->order_nblocks = 0;  // and the cost-ordered schedule is rebuilt
+  return FSDF_OK;
+}
+
 static int ensure_partials(fsdf_ctx* c, int nblocks) {
   // (rounded up to whole 8-entry tiles: FSDF_PARTIALS_LAYOUT 2)
   const size_t need = (size_t)((accum_len(c) + 7) & ~7) * nblocks;

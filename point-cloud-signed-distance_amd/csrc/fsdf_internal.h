@@ -233,7 +233,8 @@ struct SortScratch {
   uint32_t* k1 = nullptr;
   int32_t* i1 = nullptr;   // alternate index buffer
   void* tmp = nullptr;     // rocPRIM temporary storage
-  size_t part_cap = 0, k_cap0 = 0, k_cap1 = 0, i_cap1 = 0, tmp_cap = 0;
+  void* pts = nullptr;     // (regroup_points) the cloud buffer the regrouped points go to
+  size_t part_cap = 0, k_cap0 = 0, k_cap1 = 0, i_cap1 = 0, tmp_cap = 0, pts_cap = 0;
 };
 void free_sort_scratch(SortScratch& s);
 
@@ -242,6 +243,14 @@ void free_sort_scratch(SortScratch& s);
 // (n < 2^31). Asynchronous on `st`.
 hipError_t sort_points_spatial(const double* d_src, int64_t n, int precision, void* d_dst, int32_t* d_perm,
                               SortScratch& s, hipStream_t st);
+// Regroup a resident cloud by each point's nearest surface in the last pass
+// (prior[i] < 64) within windows of 4,096 points, keeping the current
+// (Hilbert) order within each group (sort.hip regroup_window_kernel). The
+// regrouped points replace *d_pts (the old buffer becomes the scratch's:
+// *d_pts / *pts_cap are updated); d_perm and prior are permuted in place.
+// Asynchronous on `st`.
+hipError_t regroup_points(void** d_pts, int64_t* pts_cap, int64_t n, int precision, int32_t* d_perm, uint8_t* prior,
+                          SortScratch& s, hipStream_t st);
 // d_out[i] = d_perm[i] as int64 (fsdf_get_permutation's layout)
 hipError_t widen_permutation(const int32_t* d_perm, int64_t n, int64_t* d_out, hipStream_t st);
 

@@ -150,6 +150,78 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const double* __restrict
   for (int j = 0; j < 3; ++j) dst[3 * i + j] = (T)src[3 * o + j];
 }
 
+// regroup_points: one workgroup per window of kRegroupWindow resident points
+// groups the window's points by their last nearest surface (prior < 64),
+// stably — the window's order kept within a group. Sub-chunks of 64 points,
+// one per wave-iteration in order: each lane's rank among the earlier lanes of
+// its key (ballots over the key's 6 bits), the sub-chunk's count per key; then
+// per key an exclusive scan over the sub-chunks, keys in ascending order; then
+// every point moves to window + offset[sub][key] + rank. A window is 64 chunks:
+// their points stay in their window, so the cloud's coarse order is unchanged.
+constexpr int kRegroupWindow = 4096;
+constexpr int kRegroupSubs = kRegroupWindow / 64;
+constexpr int kRegroupBlock = 256;
+template <typename T>
+__global__ __launch_bounds__(kRegroupBlock) void regroup_window_kernel(const T* __restrict__ pts,
+                                                                    const int32_t* __restrict__ perm,
+                                                                    const uint8_t* __restrict__ prior, int64_t n,
+                                                                    T* __restrict__ dst_pts, int32_t* __restrict__ dst_perm,
+                                                                    uint8_t* __restrict__ dst_prior) {
+  __shared__ uint16_t cnt[kRegroupSubs][64];  // per sub-chunk, per key: count, then offset
+  __shared__ uint16_t tot[64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t w0 = (int64_t)blockIdx.x * kRegroupWindow;
+  constexpr int kSubsPerWave = kRegroupSubs / (kRegroupBlock / 64);
+  int key[kSubsPerWave], rank[kSubsPerWave];
+#pragma unroll
+  for (int j = 0; j < kSubsPerWave; ++j) {
+    const int sub = wave * kSubsPerWave + j;
+    const int64_t i = w0 + 64 * sub + lane;
+    const bool valid = i < n;
+    const int k = valid ? (int)(prior[i] & 63) : 0;
+    uint64_t eq = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const uint64_t m = __ballot(valid && ((k >> b) & 1));
+      eq &= ((k >> b) & 1) ? m : ~m;
+    }
+    key[j] = valid ? k : -1;
+    rank[j] = __builtin_popcountll(eq & ((1ull << lane) - 1));
+    cnt[sub][lane] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (valid && rank[j] == 0) cnt[sub][k] = (uint16_t)__builtin_popcountll(eq);
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {  // per key: exclusive scan over the sub-chunks, then over the keys
+    const int k = threadIdx.x;
+    unsigned run = 0;
+    for (int sub = 0; sub < kRegroupSubs; ++sub) {
+      const unsigned c = cnt[sub][k];
+      cnt[sub][k] = (uint16_t)run;
+      run += c;
+    }
+    unsigned incl = run;  // inclusive wave scan of the keys' totals
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned o = __shfl_up(incl, off, 64);
+      if (k >= off) incl += o;
+    }
+    tot[k] = (uint16_t)(incl - run);  // the key's group starts here in the window
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSubsPerWave; ++j) {
+    if (key[j] < 0) continue;
+    const int sub = wave * kSubsPerWave + j;
+    const int64_t i = w0 + 64 * sub + lane;
+    const int64_t d = w0 + tot[key[j]] + cnt[sub][key[j]] + rank[j];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) dst_pts[3 * d + c] = pts[3 * i + c];
+    dst_perm[d] = perm[i];
+    dst_prior[d] = (uint8_t)key[j];
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void widen_kernel(const int32_t* __restrict__ src, int64_t n,
                                                        int64_t* __restrict__ dst) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -178,6 +250,7 @@ void free_sort_scratch(SortScratch& s) {
   if (s.k1) (void)hipFree(s.k1);
   if (s.i1) (void)hipFree(s.i1);
   if (s.tmp) (void)hipFree(s.tmp);
+  if (s.pts) (void)hipFree(s.pts);
   s = SortScratch();
 }
 
@@ -214,6 +287,37 @@ hipError_t sort_points_spatial(const double* d_src, int64_t n, int precision, vo
   else
     hipLaunchKernelGGL(gather_kernel<float>, dim3(grid), dim3(kBlock), 0, st, d_src, n, d_perm, (float*)d_dst);
   return hipGetLastError();
+}
+
+hipError_t regroup_points(void** d_pts, int64_t* pts_cap, int64_t n, int precision, int32_t* d_perm, uint8_t* prior,
+                          SortScratch& s, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (n > INT32_MAX) return hipErrorInvalidValue;
+  const size_t tsz = precision == 64 ? sizeof(double) : sizeof(float);
+  hipError_t e;
+  if ((e = grow((char**)&s.pts, &s.pts_cap, (size_t)n * 3 * tsz)) != hipSuccess) return e;
+  if ((e = grow(&s.k0, &s.k_cap0, (size_t)n * sizeof(uint32_t))) != hipSuccess) return e;  // perm, then prior
+  if ((e = grow(&s.k1, &s.k_cap1, (size_t)n)) != hipSuccess) return e;
+  int32_t* perm2 = (int32_t*)s.k0;
+  uint8_t* prior2 = (uint8_t*)s.k1;
+  const unsigned grid = (unsigned)((n + kRegroupWindow - 1) / kRegroupWindow);
+  if (precision == 64)
+    hipLaunchKernelGGL(regroup_window_kernel<double>, dim3(grid), dim3(kRegroupBlock), 0, st, (const double*)*d_pts,
+                       d_perm, prior, n, (double*)s.pts, perm2, prior2);
+  else
+    hipLaunchKernelGGL(regroup_window_kernel<float>, dim3(grid), dim3(kRegroupBlock), 0, st, (const float*)*d_pts,
+                       d_perm, prior, n, (float*)s.pts, perm2, prior2);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // the regrouped cloud becomes the resident one (the old buffer the scratch)
+  void* old = *d_pts;
+  const int64_t old_cap = *pts_cap;
+  *d_pts = s.pts;
+  *pts_cap = (int64_t)(s.pts_cap / (3 * tsz));
+  s.pts = old;
+  s.pts_cap = (size_t)old_cap * 3 * tsz;
+  if ((e = hipMemcpyAsync(d_perm, perm2, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, st)) != hipSuccess)
+    return e;
+  return hipMemcpyAsync(prior, prior2, (size_t)n, hipMemcpyDeviceToDevice, st);
 }
 
 hipError_t widen_permutation(const int32_t* d_perm, int64_t n, int64_t* d_out, hipStream_t st) {

@@ -65,6 +65,7 @@ _PROTOS = {
     "fsdf_set_points_device": (c_int32, [c_void_p, c_void_p, c_int64]),
     "fsdf_set_points_range": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_int64]),
     "fsdf_set_points_range_device": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_int64]),
+    "fsdf_regroup_points": (c_int32, [c_void_p]),
     "fsdf_num_points": (c_int32, [c_void_p, POINTER(c_int64)]),
     "fsdf_eval": (c_int32, [c_void_p, c_void_p, POINTER(c_double), c_void_p, c_void_p, c_void_p, c_void_p]),
     "fsdf_eval_device": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -248,6 +249,13 @@ class Context:
         check(self._lib.fsdf_set_points_range(self._ctx, ptr(pts), pts.shape[0], int(begin), int(end)), self._ctx,
               "set_points_range")
         self.n = int(end) - int(begin)
+
+    def regroup_points(self):
+        """Regroup the resident cloud by each point's nearest surface in the
+        last pass (fsdf_regroup_points): once per frame, after its first pass.
+        Per-point results are unchanged; re-read permutation() for
+        resident-order outputs."""
+        check(self._lib.fsdf_regroup_points(self._ctx), self._ctx, "regroup_points")
 
     def set_points_range_device(self, dev_ptr: int, n: int, begin: int, end: int):
         check(self._lib.fsdf_set_points_range_device(self._ctx, c_void_p(dev_ptr), n, int(begin), int(end)),

@@ -561,3 +561,59 @@ def test_prior_seeds_change_no_bits(m64, ctx_factory, n):
         c0, a0, (k0, d0, g0) = cold.eval(p, per_point=True)
         assert c1 == c0 and np.array_equal(a1, a0)
         assert np.array_equal(k1, k0) and np.array_equal(d1, d0) and np.array_equal(g1, g0)
+
+
+@pytest.mark.parametrize("n", [131077, 530000])
+def test_regroup_points(m64, ctx_factory, n):
+    """fsdf_regroup_points: the resident cloud regrouped by each point's nearest
+    surface in the last pass, within windows of 4,096 points (stable: the
+    Hilbert order kept within a group).
+    The permutation stays a permutation, the groups are contiguous, and later
+    passes give every point's k*, d*, ∇d* bit for bit as an unregrouped
+    context does, their sums to rounding; a ranged cloud regroups within its
+    range; without a pass, or without a permutation, it refuses."""
+    import flash
+    from flash import synthetic
+    from flash._lib import FlashNativeError
+    qt, qe = synthetic.perturbed_configuration(m64, 911)
+    pa, pb = flash.hull_poses(m64, qe), flash.hull_poses(m64, qe + 2e-3)
+    pts = synthetic.depth_cloud(m64, qt, n, seed=912, order="shuffled")
+    plain = ctx_factory(m64, sort_points=True)
+    plain.set_points(pts)
+    cb, accb, (kb, db, gb) = plain.eval(pb, per_point=True)  # caller order
+    for begin, end in ((0, n), (64 * 100, n - 5)):
+        ctx = ctx_factory(m64, sort_points=True)
+        if (begin, end) == (0, n):
+            ctx.set_points(pts)
+        else:
+            ctx.set_points_range(pts, begin, end)
+        with pytest.raises(FlashNativeError):
+            ctx.regroup_points()  # no pass yet
+        ctx.set_output_order(True)
+        _, _, (ka, _, _) = ctx.eval(pa, per_point=True)
+        perm0 = ctx.permutation()
+        ctx.regroup_points()
+        perm1 = ctx.permutation()
+        assert np.array_equal(np.sort(perm1), np.sort(perm0))
+        pos0 = np.empty(perm0.max() + 1, np.int64)
+        pos0[perm0] = np.arange(len(perm0))
+        k_at = np.empty(perm0.max() + 1, np.int32)
+        k_at[perm0] = ka
+        kg, old = k_at[perm1], pos0[perm1]
+        W = 4096  # sort.hip kRegroupWindow: points stay in their window of the previous order
+        new = np.arange(len(perm1))
+        assert np.array_equal(old // W, new // W)
+        inwin = (new[1:] // W) == (new[:-1] // W)
+        assert np.all(np.diff(kg)[inwin] >= 0)  # contiguous groups, ascending surface, per window
+        same = inwin & (np.diff(kg) == 0)
+        assert np.all(np.diff(old)[same] > 0)  # the previous order within a group
+        c1, acc1, (k1, d1, g1) = ctx.eval(pb, per_point=True)
+        assert np.array_equal(k1, kb[perm1]) and np.array_equal(d1, db[perm1]) and np.array_equal(g1, gb[perm1])
+        if (begin, end) == (0, n):
+            assert c1 == pytest.approx(cb, rel=1e-12)
+            assert np.allclose(acc1, accb, rtol=1e-10, atol=1e-12 * np.abs(accb).max())
+    unsorted = ctx_factory(m64, sort_points=False)
+    unsorted.set_points(pts)
+    unsorted.eval(pa)
+    with pytest.raises(FlashNativeError):
+        unsorted.regroup_points()

@@ -332,6 +332,46 @@ def main():
             for st in streams[1:nctx]:
                 stream.wait_stream(st)
 
+        # once per frame, after its first passes: the resident cloud regrouped by
+        # each point's last nearest surface (fsdf_regroup_points; hull-only
+        # scenes with a permutation — otherwise refused and skipped), timed and
+        # charged to the frame beside set_points; before the settle (and again
+        # after a rebalance's re-upload), so every timed and profiled pass runs
+        # on the regrouped cloud
+        # (only where the pass is bound by its summed work — the one-wave grid
+        # above the planned window: the planned pass and the hull-partitioned
+        # tiers are bound by their heaviest chunks, which grouping makes heavier —
+        # 2^17 step 0.0612 -> 0.0677 ms and worse, profiles/r05/regroup/)
+        def regroup_all():
+            if args.no_regroup:
+                return None
+            ms = None
+            # (every context: the same pass, then the same regroup, so that their
+            # resident orders — and the in-flight check's accumulators — agree;
+            # the first call also grows the context's scratch, the second is timed)
+            for rep in range(2):
+                for c in range(CS):
+                    ctxs[c].eval_device(poses[0], accums[c][0].data_ptr(), *outs[c])
+                torch.cuda.synchronize()
+                kname = ctx.pass_kernel_name()  # pass_kernel<T, SLOTS, CULL, RBF, ALIAS, HPART, NB, NPART>
+                if not (kname.startswith("pass_kernel<") and kname.split(",")[5].strip() == "false"):
+                    return None
+                t_r = time.perf_counter()
+                try:
+                    for cx in ctxs:
+                        cx.regroup_points()
+                except FlashNativeError:
+                    return None
+                torch.cuda.synchronize()
+                ms = (time.perf_counter() - t_r) * 1e3 / CS
+            for i in range(16 * CS):  # other chunks: their first passes plan and order anew
+                c = i % CS
+                ctxs[c].eval_device(poses[(i // CS) & 1], accums[c][(i // CS) & 1].data_ptr(), *outs[c])
+            torch.cuda.synchronize()
+            return ms
+
+        global REGROUP_MS
+        REGROUP_MS = regroup_all()
         # settle: untimed passes (no collectives: the ranks' counts differ) until
         # the clocks have ramped, wall-clock bound
         t_settle = time.perf_counter()
@@ -356,32 +396,7 @@ def main():
                     c = i % C
                     ctxs[c].eval_device(poses[(i // C) & 1], accums[c][(i // C) & 1].data_ptr(), *outs[c])
                 torch.cuda.synchronize()
-        # once per frame, after its first passes: the resident cloud regrouped by
-        # each point's last nearest surface (fsdf_regroup_points; hull-only
-        # scenes with a permutation — otherwise refused and skipped), timed and
-        # charged to the frame beside set_points
-        global REGROUP_MS
-        REGROUP_MS = None
-        if not args.no_regroup:
-            torch.cuda.synchronize()
-            try:
-                for cx in ctxs:  # (the first call also grows the context's sort scratch)
-                    cx.regroup_points()
-                for c in range(C):  # a frame's regroup follows a pass: time one such, steady state
-                    ctxs[c].eval_device(poses[0], accums[c][0].data_ptr(), *outs[c])
-                torch.cuda.synchronize()
-                t_r = time.perf_counter()
-                for cx in ctxs[:C]:
-                    cx.regroup_points()
-                torch.cuda.synchronize()
-                REGROUP_MS = (time.perf_counter() - t_r) * 1e3 / C
-            except FlashNativeError:
-                REGROUP_MS = None
-            if REGROUP_MS is not None:
-                for i in range(16 * C):  # other chunks: their first passes plan and order anew
-                    c = i % C
-                    ctxs[c].eval_device(poses[(i // C) & 1], accums[c][(i // C) & 1].data_ptr(), *outs[c])
-                torch.cuda.synchronize()
+                REGROUP_MS = regroup_all()
         del d_pts
         # K passes one at a time on context 0 (no collective), right after the
         # settle: the kernel's own launch duration (the roofline's, as rocprofv3
@@ -620,8 +635,8 @@ def main():
                 "regroup_note": ("fsdf_regroup_points once per frame after its first passes: the resident cloud "
                                  "grouped by each point's last nearest surface (Hilbert order within a group); "
                                  "the timed passes run on it, seeded from the previous pass's k* (per-point results "
-                                 "unchanged)" if REGROUP_MS is not None else "not applied (--no-regroup, an RBF "
-                                 "scene or an unsorted cloud)"),
+                                 "unchanged)" if REGROUP_MS is not None else "not applied (--no-regroup, the "
+                                 "planned pass or a hull-partitioned tier, an RBF scene or an unsorted cloud)"),
                 "frame_note": "set_points (H2D-resident copy + Hilbert sort) once + regroup once + 30 residual passes",
                 "full_iteration_ms": iter_ms,
                 "full_iteration_note": "CostFunctor.value_and_gradient on the resident cloud (fsdf_value_and_gradient: "

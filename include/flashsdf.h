@@ -268,7 +268,10 @@ int fsdf_num_points(const fsdf_ctx* ctx, int64_t* n_out);
  * this exploits: the passes seed each point from its last nearest surface, and
  * a 64-point chunk whose points share one evaluates fewer hulls. Per-point
  * results are unchanged; the cost and wrench sums change in rounding only (the
- * chunks group other points). The resident order changes: re-read
+ * chunks group other points). It pays where the pass is bound by its summed
+ * work — the one-wave grid of clouds above the planned window — and costs where
+ * the planned pass is bound by its heaviest chunk, which grouping makes heavier
+ * (DESIGN.md §7 round 5). The resident order changes: re-read
  * fsdf_get_permutation for FSDF_ORDER_RESIDENT outputs. Requires a sorted
  * (sort_points) or ranged cloud and a pass over it (hull-only scenes of <= 64
  * surfaces); asynchronous on the context stream. */

@@ -244,8 +244,8 @@ void free_sort_scratch(SortScratch& s);
 hipError_t sort_points_spatial(const double* d_src, int64_t n, int precision, void* d_dst, int32_t* d_perm,
                               SortScratch& s, hipStream_t st);
 // Regroup a resident cloud by each point's nearest surface in the last pass
-// (prior[i] < 64) within windows of 4,096 points, keeping the current
-// (Hilbert) order within each group (sort.hip regroup_window_kernel). The
+// (prior[i] < 64), keeping the current (Hilbert) order within each group: a
+// stable counting sort (sort.hip regroup_*_kernel, three launches). The
 // regrouped points replace *d_pts (the old buffer becomes the scratch's:
 // *d_pts / *pts_cap are updated); d_perm and prior are permuted in place.
 // Asynchronous on `st`.

@@ -150,71 +150,146 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const double* __restrict
   for (int j = 0; j < 3; ++j) dst[3 * i + j] = (T)src[3 * o + j];
 }
 
-// regroup_points: one workgroup per window of kRegroupWindow resident points
-// groups the window's points by their last nearest surface (prior < 64),
-// stably — the window's order kept within a group. Sub-chunks of 64 points,
-// one per wave-iteration in order: each lane's rank among the earlier lanes of
-// its key (ballots over the key's 6 bits), the sub-chunk's count per key; then
-// per key an exclusive scan over the sub-chunks, keys in ascending order; then
-// every point moves to window + offset[sub][key] + rank. A window is 64 chunks:
-// their points stay in their window, so the cloud's coarse order is unchanged.
+// regroup_points: a stable counting sort of the resident cloud on each point's
+// last nearest surface (prior < 64), in three launches over windows of
+// kRegroupWindow points: (1) each window's count per surface, (2) one
+// exclusive scan of those counts in surface-major order — the start of every
+// (surface, window) run in the regrouped cloud, (3) each window ranks its
+// points again and moves them there. Ranks: sub-chunks of 64 points, one per
+// wave-iteration in order, a lane's rank among the earlier lanes of its
+// surface from ballots over the surface's 6 bits; per surface an exclusive
+// scan over the window's sub-chunks in LDS. Stable: the previous (Hilbert)
+// order holds within each surface's group.
 constexpr int kRegroupWindow = 4096;
 constexpr int kRegroupSubs = kRegroupWindow / 64;
 constexpr int kRegroupBlock = 256;
-template <typename T>
-__global__ __launch_bounds__(kRegroupBlock) void regroup_window_kernel(const T* __restrict__ pts,
-                                                                    const int32_t* __restrict__ perm,
-                                                                    const uint8_t* __restrict__ prior, int64_t n,
-                                                                    T* __restrict__ dst_pts, int32_t* __restrict__ dst_perm,
-                                                                    uint8_t* __restrict__ dst_prior) {
-  __shared__ uint16_t cnt[kRegroupSubs][64];  // per sub-chunk, per key: count, then offset
-  __shared__ uint16_t tot[64];
+constexpr int kRegroupSubsPerWave = kRegroupSubs / (kRegroupBlock / 64);
+constexpr int kRegroupScanBlock = 1024;
+
+// this lane's surface (-1: past the cloud) and rank among the earlier lanes
+// of its sub-chunk with the same surface; the mask of those lanes
+__device__ __forceinline__ int regroup_rank(int pv, bool valid, int& k, uint64_t& eq) {
+  const int lane = threadIdx.x & 63;
+  k = valid ? (pv & 63) : -1;
+  eq = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < 6; ++b) {
+    const uint64_t m = __ballot(valid && ((k >> b) & 1));
+    eq &= (valid && ((k >> b) & 1)) ? m : ~m;
+  }
+  if (!valid) eq = 0;
+  return __builtin_popcountll(eq & ((1ull << lane) - 1));
+}
+
+__global__ __launch_bounds__(kRegroupBlock) void regroup_count_kernel(const uint8_t* __restrict__ prior, int64_t n,
+                                                                   uint32_t* __restrict__ counts, int nwin) {
+  __shared__ uint32_t cnt[64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t w0 = (int64_t)blockIdx.x * kRegroupWindow;
-  constexpr int kSubsPerWave = kRegroupSubs / (kRegroupBlock / 64);
-  int key[kSubsPerWave], rank[kSubsPerWave];
+  if (threadIdx.x < 64) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  int pv[kRegroupSubsPerWave];  // every load issued before the first ballot
 #pragma unroll
-  for (int j = 0; j < kSubsPerWave; ++j) {
-    const int sub = wave * kSubsPerWave + j;
-    const int64_t i = w0 + 64 * sub + lane;
-    const bool valid = i < n;
-    const int k = valid ? (int)(prior[i] & 63) : 0;
-    uint64_t eq = __ballot(valid);
+  for (int j = 0; j < kRegroupSubsPerWave; ++j) {
+    const int64_t i = w0 + 64 * (wave * kRegroupSubsPerWave + j) + lane;
+    pv[j] = i < n ? prior[i] : 0;
+  }
 #pragma unroll
-    for (int b = 0; b < 6; ++b) {
-      const uint64_t m = __ballot(valid && ((k >> b) & 1));
-      eq &= ((k >> b) & 1) ? m : ~m;
+  for (int j = 0; j < kRegroupSubsPerWave; ++j) {
+    int k;
+    uint64_t eq;
+    const int r = regroup_rank(pv[j], w0 + 64 * (wave * kRegroupSubsPerWave + j) + lane < n, k, eq);
+    if (k >= 0 && r == 0) atomicAdd(&cnt[k], (uint32_t)__builtin_popcountll(eq));
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) counts[(int64_t)threadIdx.x * nwin + blockIdx.x] = cnt[threadIdx.x];
+}
+
+// exclusive prefix sum of counts[0, m) in place (one workgroup): super-tiles
+// of 16 tiles x 1,024 entries, all 16 coalesced loads issued at once (one CU
+// walking 64-B-strided lines was line-rate bound: 16 us for 16 K entries),
+// then per tile in order a wave scan (shuffles) and a scan of the 16 wave
+// totals in LDS
+constexpr int kRegroupScanPer = 16;
+__global__ __launch_bounds__(kRegroupScanBlock) void regroup_scan_kernel(uint32_t* __restrict__ counts, int64_t m) {
+  __shared__ uint32_t wsum[2][kRegroupScanBlock / 64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t carry = 0;
+  for (int64_t base = 0; base < m; base += (int64_t)kRegroupScanPer * kRegroupScanBlock) {
+    uint32_t v[kRegroupScanPer];
+#pragma unroll
+    for (int j = 0; j < kRegroupScanPer; ++j) {
+      const int64_t i = base + (int64_t)j * kRegroupScanBlock + t;
+      v[j] = i < m ? counts[i] : 0u;
     }
-    key[j] = valid ? k : -1;
-    rank[j] = __builtin_popcountll(eq & ((1ull << lane) - 1));
+#pragma unroll
+    for (int j = 0; j < kRegroupScanPer; ++j) {
+      uint32_t x = v[j];  // inclusive wave scan
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(x, off, 64);
+        if (lane >= off) x += o;
+      }
+      uint32_t* ws = wsum[j & 1];  // (alternating: one barrier per tile)
+      if (lane == 63) ws[wave] = x;
+      __syncthreads();
+      uint32_t y = lane < kRegroupScanBlock / 64 ? ws[lane] : 0u;  // every wave scans the 16 totals itself
+#pragma unroll
+      for (int off = 1; off < kRegroupScanBlock / 64; off <<= 1) {
+        const uint32_t o = __shfl_up(y, off, 64);
+        if (lane >= off) y += o;
+      }
+      const uint32_t before = wave ? __shfl(y, wave - 1, 64) : 0u;
+      const uint32_t total = __shfl(y, kRegroupScanBlock / 64 - 1, 64);
+      const int64_t i = base + (int64_t)j * kRegroupScanBlock + t;
+      if (i < m) counts[i] = carry + before + x - v[j];
+      carry += total;
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kRegroupBlock) void regroup_scatter_kernel(const T* __restrict__ pts,
+                                                                     const int32_t* __restrict__ perm,
+                                                                     const uint8_t* __restrict__ prior, int64_t n,
+                                                                     const uint32_t* __restrict__ start, int nwin,
+                                                                     T* __restrict__ dst_pts, int32_t* __restrict__ dst_perm,
+                                                                     uint8_t* __restrict__ dst_prior) {
+  __shared__ uint32_t cnt[kRegroupSubs][64];  // per sub-chunk, per surface: count, then offset in the window's run
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t w0 = (int64_t)blockIdx.x * kRegroupWindow;
+  int key[kRegroupSubsPerWave], rank[kRegroupSubsPerWave];
+#pragma unroll
+  for (int j = 0; j < kRegroupSubsPerWave; ++j) {  // every load issued before the first ballot
+    const int64_t i = w0 + 64 * (wave * kRegroupSubsPerWave + j) + lane;
+    key[j] = i < n ? prior[i] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < kRegroupSubsPerWave; ++j) {
+    const int sub = wave * kRegroupSubsPerWave + j;
+    uint64_t eq;
+    rank[j] = regroup_rank(key[j], w0 + 64 * sub + lane < n, key[j], eq);
     cnt[sub][lane] = 0;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    if (valid && rank[j] == 0) cnt[sub][k] = (uint16_t)__builtin_popcountll(eq);
+    if (key[j] >= 0 && rank[j] == 0) cnt[sub][key[j]] = (uint32_t)__builtin_popcountll(eq);
   }
   __syncthreads();
-  if (threadIdx.x < 64) {  // per key: exclusive scan over the sub-chunks, then over the keys
+  if (threadIdx.x < 64) {  // per surface: exclusive scan over the sub-chunks, from the run's start
     const int k = threadIdx.x;
-    unsigned run = 0;
+    uint32_t run = start[(int64_t)k * nwin + blockIdx.x];
     for (int sub = 0; sub < kRegroupSubs; ++sub) {
-      const unsigned c = cnt[sub][k];
-      cnt[sub][k] = (uint16_t)run;
+      const uint32_t c = cnt[sub][k];
+      cnt[sub][k] = run;
       run += c;
     }
-    unsigned incl = run;  // inclusive wave scan of the keys' totals
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const unsigned o = __shfl_up(incl, off, 64);
-      if (k >= off) incl += o;
-    }
-    tot[k] = (uint16_t)(incl - run);  // the key's group starts here in the window
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kSubsPerWave; ++j) {
+  for (int j = 0; j < kRegroupSubsPerWave; ++j) {
     if (key[j] < 0) continue;
-    const int sub = wave * kSubsPerWave + j;
+    const int sub = wave * kRegroupSubsPerWave + j;
     const int64_t i = w0 + 64 * sub + lane;
-    const int64_t d = w0 + tot[key[j]] + cnt[sub][key[j]] + rank[j];
+    const int64_t d = (int64_t)cnt[sub][key[j]] + rank[j];
 #pragma unroll
     for (int c = 0; c < 3; ++c) dst_pts[3 * d + c] = pts[3 * i + c];
     dst_perm[d] = perm[i];
@@ -294,19 +369,23 @@ hipError_t regroup_points(void** d_pts, int64_t* pts_cap, int64_t n, int precisi
   if (n <= 0) return hipSuccess;
   if (n > INT32_MAX) return hipErrorInvalidValue;
   const size_t tsz = precision == 64 ? sizeof(double) : sizeof(float);
+  const int nwin = (int)((n + kRegroupWindow - 1) / kRegroupWindow);
   hipError_t e;
   if ((e = grow((char**)&s.pts, &s.pts_cap, (size_t)n * 3 * tsz)) != hipSuccess) return e;
-  if ((e = grow(&s.k0, &s.k_cap0, (size_t)n * sizeof(uint32_t))) != hipSuccess) return e;  // perm, then prior
-  if ((e = grow(&s.k1, &s.k_cap1, (size_t)n)) != hipSuccess) return e;
+  if ((e = grow(&s.k0, &s.k_cap0, (size_t)n * sizeof(uint32_t))) != hipSuccess) return e;  // the permutation
+  if ((e = grow(&s.k1, &s.k_cap1, (size_t)n)) != hipSuccess) return e;                     // the priors
+  if ((e = grow(&s.i1, &s.i_cap1, (size_t)64 * nwin * sizeof(int32_t))) != hipSuccess) return e;  // run starts
   int32_t* perm2 = (int32_t*)s.k0;
   uint8_t* prior2 = (uint8_t*)s.k1;
-  const unsigned grid = (unsigned)((n + kRegroupWindow - 1) / kRegroupWindow);
+  uint32_t* start = (uint32_t*)s.i1;
+  hipLaunchKernelGGL(regroup_count_kernel, dim3(nwin), dim3(kRegroupBlock), 0, st, prior, n, start, nwin);
+  hipLaunchKernelGGL(regroup_scan_kernel, dim3(1), dim3(kRegroupScanBlock), 0, st, start, (int64_t)64 * nwin);
   if (precision == 64)
-    hipLaunchKernelGGL(regroup_window_kernel<double>, dim3(grid), dim3(kRegroupBlock), 0, st, (const double*)*d_pts,
-                       d_perm, prior, n, (double*)s.pts, perm2, prior2);
+    hipLaunchKernelGGL(regroup_scatter_kernel<double>, dim3(nwin), dim3(kRegroupBlock), 0, st, (const double*)*d_pts,
+                       d_perm, prior, n, start, nwin, (double*)s.pts, perm2, prior2);
   else
-    hipLaunchKernelGGL(regroup_window_kernel<float>, dim3(grid), dim3(kRegroupBlock), 0, st, (const float*)*d_pts,
-                       d_perm, prior, n, (float*)s.pts, perm2, prior2);
+    hipLaunchKernelGGL(regroup_scatter_kernel<float>, dim3(nwin), dim3(kRegroupBlock), 0, st, (const float*)*d_pts,
+                       d_perm, prior, n, start, nwin, (float*)s.pts, perm2, prior2);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // the regrouped cloud becomes the resident one (the old buffer the scratch)
   void* old = *d_pts;

@@ -566,8 +566,7 @@ def test_prior_seeds_change_no_bits(m64, ctx_factory, n):
 @pytest.mark.parametrize("n", [131077, 530000])
 def test_regroup_points(m64, ctx_factory, n):
     """fsdf_regroup_points: the resident cloud regrouped by each point's nearest
-    surface in the last pass, within windows of 4,096 points (stable: the
-    Hilbert order kept within a group).
+    surface in the last pass (stable: the Hilbert order kept within a group).
     The permutation stays a permutation, the groups are contiguous, and later
     passes give every point's k*, d*, ∇d* bit for bit as an unregrouped
     context does, their sums to rounding; a ranged cloud regroups within its
@@ -600,12 +599,8 @@ def test_regroup_points(m64, ctx_factory, n):
         k_at = np.empty(perm0.max() + 1, np.int32)
         k_at[perm0] = ka
         kg, old = k_at[perm1], pos0[perm1]
-        W = 4096  # sort.hip kRegroupWindow: points stay in their window of the previous order
-        new = np.arange(len(perm1))
-        assert np.array_equal(old // W, new // W)
-        inwin = (new[1:] // W) == (new[:-1] // W)
-        assert np.all(np.diff(kg)[inwin] >= 0)  # contiguous groups, ascending surface, per window
-        same = inwin & (np.diff(kg) == 0)
+        assert np.all(np.diff(kg) >= 0)  # contiguous groups, ascending surface
+        same = np.diff(kg) == 0
         assert np.all(np.diff(old)[same] > 0)  # the previous order within a group
         c1, acc1, (k1, d1, g1) = ctx.eval(pb, per_point=True)
         assert np.array_equal(k1, kb[perm1]) and np.array_equal(d1, db[perm1]) and np.array_equal(g1, gb[perm1])

@@ -1685,7 +1685,9 @@ __global__ __launch_bounds__(NB) __attribute__((
       if (part == 0) ((volatile double*)shb)[lane] = __builtin_huge_val();
       __syncthreads();
     }
-    const int prior = (out.prior_in && valid) ? (int)out.prior_in[i] : -1;
+    // (not in the hull-partitioned tiers: bound by their heaviest chunk's
+    // latency, the prior's load in front of it cost 2^16 0.0501 -> 0.0532 ms)
+    const int prior = (!HPART && out.prior_in && valid) ? (int)out.prior_in[i] : -1;
     scene_eval<T, SLOTS, CULL, RBF, ALIAS, kParts>(px, py, pz, valid, m, ht, smax, stage, out.stats, best, bk, gx, gy,
                                                    gz, cws,
                                                    HPART ? ((kParts == 8 ? 0x0101010101010101ull

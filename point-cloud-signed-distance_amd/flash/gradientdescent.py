@@ -139,6 +139,14 @@ class CostFunctor:
         self.ctx.set_points(self.sensed_points)
         self.manipulator._resident_cloud = self._resident
 
+    def regroup(self):
+        """Once per frame, after its first evaluation: regroup the resident
+        cloud by each point's nearest surface in that pass (fsdf_regroup_points;
+        hull-only scenes). Later evaluations give the same per-point results and
+        sums to rounding, faster on large clouds."""
+        self._ensure_resident()
+        self.ctx.regroup_points()
+
     def _ensure_resident(self):
         if getattr(self.manipulator, "_resident_cloud", None) != self._resident:
             self.ctx.set_points(self.sensed_points)

@@ -612,3 +612,19 @@ def test_regroup_points(m64, ctx_factory, n):
     unsorted.eval(pa)
     with pytest.raises(FlashNativeError):
         unsorted.regroup_points()
+
+
+def test_cost_functor_regroup(irb):
+    """CostFunctor.regroup(): after the frame's first evaluation, later ones
+    give the same cost and gradient to rounding."""
+    from flash import synthetic
+    from flash.gradientdescent import CostFunctor
+    qt, qe = synthetic.perturbed_configuration(irb, 921)
+    pts = synthetic.depth_cloud(irb, qt, 200003, seed=922, order="shuffled")
+    cf = CostFunctor(irb, pts)
+    x = np.asarray(qe, np.float64)
+    c0, g0 = cf.value_and_gradient(x)
+    cf.regroup()
+    c1, g1 = cf.value_and_gradient(x)
+    assert c1 == pytest.approx(c0, rel=1e-12)
+    assert np.allclose(g1, g0, rtol=1e-9, atol=1e-12 * np.abs(g0).max())

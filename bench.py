@@ -354,7 +354,14 @@ def main():
                     ctxs[c].eval_device(poses[0], accums[c][0].data_ptr(), *outs[c])
                 torch.cuda.synchronize()
                 kname = ctx.pass_kernel_name()  # pass_kernel<T, SLOTS, CULL, RBF, ALIAS, HPART, NB, NPART>
-                if not (kname.startswith("pass_kernel<") and kname.split(",")[5].strip() == "false"):
+                one_wave_grid = kname.startswith("pass_kernel<") and kname.split(",")[5].strip() == "false"
+                # (a spatial shard keeps the whole cloud's density: its planned pass
+                # over ~2^19 points gains too — W = 2 max step 0.0678 -> 0.0650 ms —
+                # where W = 4 / 8 shards lose, 0.0575 -> 0.0630 / 0.0564 -> 0.0656,
+                # profiles/r05/regroup/shards_*.jsonl; the bound leaves room for a
+                # rebalanced W = 2 range below 2^19)
+                dense_shard = shard_bounds is not None and world > 1 and ctx.n > 393216
+                if not (one_wave_grid or dense_shard):
                     return None
                 t_r = time.perf_counter()
                 try:

@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--splits", default="slice,spatial,balanced")
     ap.add_argument("--no-plan", action="store_true", help="unplanned pass at every shard size (fsdf_set_plan off)")
+    ap.add_argument("--regroup", action="store_true",
+                    help="fsdf_regroup_points after each shard's first passes (spatial splits)")
     a = ap.parse_args()
     import torch
     import flash
@@ -83,10 +85,15 @@ def main():
                 ctx.set_plan(True, -1.0, -1.0, plan_window(n, len(bounds)))
             ctx.set_points_range_device(d_cloud.data_ptr(), n, b, e)
 
-    def step_rank():
+    def step_rank(regroup=False):
         for i in range(8):  # first pass (tier shape), plan, planned passes
             ctx.eval_device(poses[i & 1], acc.data_ptr(), *outs)
         torch.cuda.synchronize()
+        if regroup:
+            ctx.regroup_points()
+            for i in range(8):  # other chunks: plan anew
+                ctx.eval_device(poses[i & 1], acc.data_ptr(), *outs)
+            torch.cuda.synchronize()
         best = (1e9, 1e9)
         for _ in range(a.rounds):
             ctx.profile_pass(True)
@@ -114,7 +121,7 @@ def main():
             steps, kernels, costs, kinds = [], [], [], []
             for r in range(w):
                 load(split, bounds, r)
-                s, k = step_rank()
+                s, k = step_rank(a.regroup and split != "slice")
                 steps.append(s)
                 kernels.append(k)
                 kinds.append(ctx.pass_kernel_name())
@@ -129,7 +136,7 @@ def main():
             print(json.dumps({"W": w, "split": split, "points": n, "max_step_ms": max(steps),
                               "max_kernel_ms": max(kernels), "step_ms": steps, "kernel_ms": kernels,
                               "bounds": bounds, "heaviest_chunk_us": heavy, "summed_chunk_us": summed,
-                              "kernels": sorted(set(kinds)), "planned": not a.no_plan,
+                              "kernels": sorted(set(kinds)), "planned": not a.no_plan, "regroup": a.regroup,
                               "projected_value": n / (max(steps) / 1e3)}), flush=True)
     return 0
 

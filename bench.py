@@ -644,7 +644,9 @@ def main():
                                  "the timed passes run on it, seeded from the previous pass's k* (per-point results "
                                  "unchanged)" if REGROUP_MS is not None else "not applied (--no-regroup, the "
                                  "planned pass or a hull-partitioned tier, an RBF scene or an unsorted cloud)"),
-                "frame_note": "set_points (H2D-resident copy + Hilbert sort) once + regroup once + 30 residual passes",
+                "frame_note": ("set_points (H2D-resident copy + Hilbert sort) once + regroup once + 30 residual passes "
+                               "at the timed step (a frame's first pass, unseeded and not yet regrouped, runs ~9 us "
+                               "longer at 2^20)"),
                 "full_iteration_ms": iter_ms,
                 "full_iteration_note": "CostFunctor.value_and_gradient on the resident cloud (fsdf_value_and_gradient: "
                                        "host FK + surface poses, pass, accumulator read-back, chain rule; rank 0, "

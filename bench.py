@@ -42,9 +42,13 @@ Rank 0 prints one JSON line (contract in the task description) with:
   cpu_baseline  the C oracle on a bounded sample of the same cloud, on this
                 host's cores: culled (sphere lower bounds, exact) as `value`,
                 brute force (the reference's loop) beside it
-  config        set-points (copy + Hilbert sort) per frame, a 30-iteration frame,
-                and the full CostFunctor iteration (host FK + pass + accumulator
-                read-back + chain rule) measured in the same run
+  config        set-points (copy + Hilbert sort) per frame, a measured track!
+                frame (pinned host cloud -> set_points -> fsdf_descend, 30
+                iterations of estimate_state's default solver; device and host
+                solver loops) and the full CostFunctor iteration (host FK + pass +
+                accumulator read-back + chain rule), measured in the same run
+  telemetry     the GPU's clocks, power and temperatures (sysfs / hipDeviceProp)
+                at the start and end of the timed region
 """
 from __future__ import annotations
 
@@ -69,6 +73,7 @@ ITERS_PER_FRAME = 30           # src/tracking.jl:10-13 default NaiveSolver itera
 SERIAL = {}  # run_cloud's serial re-run of the timed passes (one at a time)
 SIDE_RES = {}  # run_cloud's N = 1 side figures (dependent step, passes in flight)
 REGROUP_MS = None  # run_cloud's per-frame fsdf_regroup_points time (ms per context)
+TELEMETRY = {}  # device_telemetry() at the start and the end of the timed region (first run_cloud)
 
 CONFIGS = {
     # name: (model, default points, scaling, description)
@@ -166,6 +171,67 @@ def cpu_baseline(manip, pts, q_eval, target_s):
                       f"culled on 1 thread: {n1} points, median of 3; host CPU: {model}"}
 
 
+def device_telemetry(device):
+    """The GPU's state where the host can read it: hipDeviceProp (CU count,
+    peak engine / memory clock, PCI bus id) and, for the DRM card at that bus
+    id (every card when it is unknown), the current DPM levels (pp_dpm_sclk /
+    pp_dpm_mclk, the '*' line), power cap / draw and temperatures from hwmon.
+    Fields the box does not expose are left out."""
+    import ctypes
+    import glob
+    out = {}
+    bus = None
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        for name, attr in (("cu_count", 63), ("clock_khz", 5), ("mem_clock_khz", 60)):  # hipDeviceAttribute_t
+            v = ctypes.c_int(0)
+            if hip.hipDeviceGetAttribute(ctypes.byref(v), attr, device) == 0:
+                out[name] = v.value
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, device) == 0:
+            bus = buf.value.decode().lower()
+            out["pci_bus_id"] = bus
+    except OSError:
+        pass
+
+    def read(p):
+        try:
+            with open(p) as f:
+                return f.read().strip()
+        except OSError:
+            return None
+
+    cards = []
+    for dev in sorted(glob.glob("/sys/class/drm/card*/device")):
+        sclk = read(os.path.join(dev, "pp_dpm_sclk"))
+        if sclk is None:
+            continue
+        rec = {"card": dev.split("/")[-2]}
+        if bus is not None:  # this process's GPU only (a node's sysfs lists every card)
+            if not os.path.realpath(dev).lower().endswith(bus):
+                continue
+        for key, fn in (("sclk", "pp_dpm_sclk"), ("mclk", "pp_dpm_mclk")):
+            txt = read(os.path.join(dev, fn)) or ""
+            cur = [ln.split(":", 1)[1].replace("*", "").strip() for ln in txt.splitlines() if ln.endswith("*")]
+            if cur:
+                rec[key] = cur[0]
+        for hw in glob.glob(os.path.join(dev, "hwmon", "hwmon*")):
+            for key, fn, scale in (("power_cap_w", "power1_cap", 1e-6), ("power_w", "power1_average", 1e-6),
+                                   ("power_input_w", "power1_input", 1e-6)):
+                v = read(os.path.join(hw, fn))
+                if v and v.lstrip("-").isdigit():
+                    rec[key] = round(int(v) * scale, 1)
+            for tp in sorted(glob.glob(os.path.join(hw, "temp*_input"))):
+                v = read(tp)
+                lab = read(tp.replace("_input", "_label")) or os.path.basename(tp)
+                if v and v.lstrip("-").isdigit():
+                    rec["temp_" + lab + "_c"] = int(v) / 1000.0
+        cards.append(rec)
+    if cards:
+        out["cards"] = cards
+    return out
+
+
 def full_iteration_ms(manip, ctx, q, iters=20):
     """One CostFunctor.value_and_gradient iteration on the resident cloud, as
     track! runs it for a rigid scene: fsdf_value_and_gradient = native FK +
@@ -180,6 +246,53 @@ def full_iteration_ms(manip, ctx, q, iters=20):
         x = x + 1e-6
         ctx.value_and_gradient(x)
     return (time.perf_counter() - t) / iters * 1e3
+
+
+def measured_frame(manip, ctx, pts_host, q, torch, frames=5):
+    """The reference's unit of tracking work, measured end to end: per frame
+    the sensed cloud from pinned host memory -> fsdf_set_points (H2D + device
+    Hilbert sort) -> fsdf_descend with estimate_state's default solver
+    (NaiveSolver rate 0.1, max_step 0.5, 30 iterations, src/tracking.jl:12-15;
+    tolerance 1e-3, flash/tracking.py) from q over c/N (src/tracking.jl:20);
+    the library regroups after the frame's first pass by its own rule. The
+    device solver loop (every iteration on the GPU, one read-back per frame)
+    and, beside it, the host loop (one synchronisation per iteration). Median
+    of `frames` frames after one untimed (allocations)."""
+    import statistics
+    surf = manip.surfaces
+    ctx.set_mechanism(manip.mechanism, [s.body for s in surf], [s.frame.R for s in surf], [s.frame.t for s in surf])
+    n = len(pts_host)
+    pinned = torch.empty((n, 3), dtype=torch.float64, pin_memory=True)
+    pinned.copy_(torch.from_numpy(np.ascontiguousarray(pts_host, np.float64)))
+    host_pts = pinned.numpy()
+    x0 = np.array(q, np.float64)
+
+    def frame(device_loop):
+        ctx.set_solver(device_loop)
+        t0 = time.perf_counter()
+        ctx.set_points(host_pts)
+        t1 = time.perf_counter()
+        x, f, its = ctx.descend(x0, ITERS_PER_FRAME, 0.1, 0.5, 1e-3, None, float(n))
+        t2 = time.perf_counter()
+        return (t2 - t0) * 1e3, (t1 - t0) * 1e3, its, f, x
+
+    out = {}
+    for name, dev_loop in (("device_loop", True), ("host_loop", False)):
+        frame(dev_loop)
+        rec = [frame(dev_loop) for _ in range(frames)]
+        ms = statistics.median(r[0] for r in rec)
+        sp = statistics.median(r[1] for r in rec)
+        its = rec[0][2]
+        out[name] = {"frame_ms": ms, "set_points_ms": sp, "iterations": its,
+                     "ms_per_iteration": (ms - sp) / max(its, 1),
+                     "tracking_point_evals_per_s": n * its / (ms / 1e3), "f": rec[0][3]}
+    a, b = out["device_loop"], out["host_loop"]
+    out["same_result"] = bool(a["iterations"] == b["iterations"] and a["f"] == b["f"])
+    out["note"] = (f"{n} points, pinned host cloud -> set_points (H2D + sort) -> fsdf_descend(rate 0.1, max_step 0.5, "
+                   f"{ITERS_PER_FRAME} iterations, tolerance 1e-3) from q_eval; median of {frames} frames; "
+                   "device_loop: solver step on the GPU (solver.hip), host_loop: fsdf_set_solver(0)")
+    ctx.set_solver(True)
+    return out
 
 
 def main():
@@ -312,12 +425,22 @@ def main():
         # previous collective completed
         pending = [[None, None] for _ in range(CS)]
 
+        # (no process group — N = 1: no collective to order, and every context
+        # is bound to its own stream by set_stream, so the step is the library
+        # call alone; torch's stream switch cost ~5 us of host time per step,
+        # enough to starve the device between 0.1 ms passes)
+        acc_ptrs = [[accums[c][s_].data_ptr() for s_ in (0, 1)] for c in range(CS)]
+        grouped = dist.is_available() and dist.is_initialized()
+
         def step(i, nctx=C):
             c, s_ = i % nctx, (i // nctx) & 1
+            if not grouped:
+                ctxs[c].eval_device(poses[s_], acc_ptrs[c][s_], *outs[c])
+                return
             with torch.cuda.stream(streams[c]):
                 if pending[c][s_] is not None:
                     pending[c][s_].wait()
-                ctxs[c].eval_device(poses[s_], accums[c][s_].data_ptr(), *outs[c])
+                ctxs[c].eval_device(poses[s_], acc_ptrs[c][s_], *outs[c])
                 pending[c][s_] = allreduce_accum(accums[c][s_], async_op=True)
 
         def drain():
@@ -333,42 +456,37 @@ def main():
                 stream.wait_stream(st)
 
         # once per frame, after its first passes: the resident cloud regrouped by
-        # each point's last nearest surface (fsdf_regroup_points; hull-only
-        # scenes with a permutation — otherwise refused and skipped), timed and
-        # charged to the frame beside set_points; before the settle (and again
-        # after a rebalance's re-upload), so every timed and profiled pass runs
-        # on the regrouped cloud
-        # (only where the pass is bound by its summed work — the one-wave grid
-        # above the planned window: the planned pass and the hull-partitioned
-        # tiers are bound by their heaviest chunks, which grouping makes heavier —
-        # 2^17 step 0.0612 -> 0.0677 ms and worse, profiles/r05/regroup/)
+        # each point's last nearest surface where the library's rule says it
+        # pays (fsdf_regroup_auto: the pass ran one wave per chunk — the grid
+        # above the planned window, bound by its summed work; the planned pass
+        # and the hull-partitioned tiers are bound by their heaviest chunks,
+        # which grouping makes heavier, profiles/r05/regroup/), timed and charged
+        # to the frame beside set_points; before the settle (spatial shards:
+        # after the rebalance, whose chunk costs must be the whole cloud's
+        # Hilbert chunks), so every timed and profiled pass runs on the
+        # regrouped cloud. The track! path (fsdf_descend, value_and_gradient)
+        # applies the same rule by itself (measured_frame below).
         def regroup_all():
             if args.no_regroup:
                 return None
-            ms = None
             # (every context: the same pass, then the same regroup, so that their
             # resident orders — and the in-flight check's accumulators — agree;
-            # the first call also grows the context's scratch, the second is timed)
+            # the first regroup also grows the context's scratch, the second —
+            # an explicit one, the rule having decided — is timed)
+            ms = None
             for rep in range(2):
                 for c in range(CS):
                     ctxs[c].eval_device(poses[0], accums[c][0].data_ptr(), *outs[c])
                 torch.cuda.synchronize()
-                kname = ctx.pass_kernel_name()  # pass_kernel<T, SLOTS, CULL, RBF, ALIAS, HPART, NB, NPART>
-                one_wave_grid = kname.startswith("pass_kernel<") and kname.split(",")[5].strip() == "false"
-                # (a spatial shard keeps the whole cloud's density: its planned pass
-                # over ~2^19 points gains too — W = 2 max step 0.0678 -> 0.0650 ms —
-                # where W = 4 / 8 shards lose, 0.0575 -> 0.0630 / 0.0564 -> 0.0656,
-                # profiles/r05/regroup/shards_*.jsonl; the bound leaves room for a
-                # rebalanced W = 2 range below 2^19)
-                dense_shard = shard_bounds is not None and world > 1 and ctx.n > 393216
-                if not (one_wave_grid or dense_shard):
-                    return None
                 t_r = time.perf_counter()
-                try:
+                if rep == 0:
+                    applied = [cx.regroup_auto() for cx in ctxs]
+                    if not all(applied):
+                        assert not any(applied), "contexts over one cloud disagree on the regroup"
+                        return None
+                else:
                     for cx in ctxs:
                         cx.regroup_points()
-                except FlashNativeError:
-                    return None
                 torch.cuda.synchronize()
                 ms = (time.perf_counter() - t_r) * 1e3 / CS
             for i in range(16 * CS):  # other chunks: their first passes plan and order anew
@@ -378,7 +496,9 @@ def main():
             return ms
 
         global REGROUP_MS
-        REGROUP_MS = regroup_all()
+        spatial = shard_bounds is not None and world > 1
+        if not spatial:
+            REGROUP_MS = regroup_all()
         # settle: untimed passes (no collectives: the ranks' counts differ) until
         # the clocks have ramped, wall-clock bound
         t_settle = time.perf_counter()
@@ -389,12 +509,13 @@ def main():
             i += 1
             if i % 16 == 0:
                 torch.cuda.synchronize()
-        if shard_bounds is not None and world > 1:
+        if spatial:
             # rebalance: the ranks' measured per-chunk durations (the planned
-            # pass's, in the whole cloud's chunk order) all-gathered once; new
-            # ranges at equal summed chunk time, every rank re-uploads its range
+            # pass's, in the whole cloud's chunk order — before any regroup)
+            # all-gathered once; new ranges at equal summed chunk time, every
+            # rank re-uploads its range; then the regroup
             torch.cuda.synchronize()
-            costs = gather_chunk_costs(ctx.chunk_costs())
+            costs = gather_chunk_costs(ctx.chunk_costs(), device=dev)
             if costs.shape[0] == -(-len(pts_host) // 64):
                 shard_bounds[:] = spatial_bounds(len(pts_host), world, costs)
                 for cx in ctxs:
@@ -403,7 +524,7 @@ def main():
                     c = i % C
                     ctxs[c].eval_device(poses[(i // C) & 1], accums[c][(i // C) & 1].data_ptr(), *outs[c])
                 torch.cuda.synchronize()
-                REGROUP_MS = regroup_all()
+            REGROUP_MS = regroup_all()
         del d_pts
         # K passes one at a time on context 0 (no collective), right after the
         # settle: the kernel's own launch duration (the roofline's, as rocprofv3
@@ -427,6 +548,9 @@ def main():
         for cx in ctxs:
             cx.profile_pass(True)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        first_run = not TELEMETRY
+        if first_run:
+            TELEMETRY["timed_start"] = device_telemetry(local)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -434,6 +558,7 @@ def main():
         ev0.record(stream)
         for i in range(args.steps):
             step(i)
+        t_enq = time.perf_counter() - t0  # host time to enqueue the K steps (< the region: device-bound)
         drain()
         join()
         ev1.record(stream)
@@ -441,6 +566,8 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
+        if first_run:
+            TELEMETRY["timed_end"] = device_telemetry(local)
         kernel_ms = pass_ms = 0.0
         launches = 0
         for cx in ctxs:
@@ -453,7 +580,7 @@ def main():
         # waits, every step (what a track! iteration pays besides its host FK and
         # chain rule); (b) SIDE independent passes in flight (aggregate throughput)
         global SIDE_RES
-        SIDE_RES = {}
+        SIDE_RES = {"host_enqueue_ms_per_step": t_enq / args.steps * 1e3}
         if world == 1:
             for i in range(3):
                 ctx.eval_device(poses[i & 1], accums[0][i & 1].data_ptr(), *outs[0])
@@ -543,11 +670,12 @@ def main():
                 "pass_ms": w_pass, "pass_kernel_ms": w_kernel,
                 "note": "weak scaling beside the strong value: every rank its own 2^20-point cloud"}
 
-    iter_ms = None
+    iter_ms = frame_rec = None
     if rank == 0 and world == 1 and not args.no_full_iteration:
         ctx.set_stream(None)
         ctx.set_output_order(False)
         iter_ms = full_iteration_ms(manip, ctx, q_eval)
+        frame_rec = measured_frame(manip, ctx, pts, q_eval, torch)
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -580,7 +708,6 @@ def main():
                 if executed and executed.get("valu_insts_per_launch"):
                     issue = executed["valu_insts_per_launch"] * CYCLES_PER_WAVE_OP / (
                         SIMDS * CLOCK_HZ * kernel_avg_ms / 1e3)
-        frame_ms = set_points_ms + (REGROUP_MS or 0.0) + ITERS_PER_FRAME * ms_per_step
         out = {
             "metric": "SDF+grad point-evals/sec, 1M-pt cloud x 64-prim model (M64)",
             "value": value,
@@ -628,6 +755,7 @@ def main():
                                                  "dependent track! iteration cannot"}
                                         if "inflight_ms_per_pass" in side else None),
                 "serial_step_ms": serial["step_ms"],
+                "host_enqueue_ms_per_step": side.get("host_enqueue_ms_per_step"),
                 "serial_step_note": "K passes one at a time on one context, untimed, before the timed region (no "
                                     "collective, per-point outputs written): one pass's latency",
                 "dependent_step_ms": dependent_ms,
@@ -637,16 +765,14 @@ def main():
                                         "memory + host wait, every step (a track! iteration's device latency; its "
                                         "host FK and chain rule are in full_iteration_ms)"),
                 "set_points_ms_per_frame": set_points_ms,
-                "frame_ms_at_30_iterations": frame_ms,
+                "measured_frame": frame_rec,
                 "regroup_ms_per_frame": REGROUP_MS,
-                "regroup_note": ("fsdf_regroup_points once per frame after its first passes: the resident cloud "
-                                 "grouped by each point's last nearest surface (Hilbert order within a group); "
+                "regroup_note": ("fsdf_regroup_auto once per frame after its first passes (the library's rule: the pass "
+                                 "ran one wave per chunk): the resident cloud grouped by each point's last nearest "
+                                 "surface (Hilbert order within a group); "
                                  "the timed passes run on it, seeded from the previous pass's k* (per-point results "
                                  "unchanged)" if REGROUP_MS is not None else "not applied (--no-regroup, the "
                                  "planned pass or a hull-partitioned tier, an RBF scene or an unsorted cloud)"),
-                "frame_note": ("set_points (H2D-resident copy + Hilbert sort) once + regroup once + 30 residual passes "
-                               "at the timed step (a frame's first pass, unseeded and not yet regrouped, runs ~9 us "
-                               "longer at 2^20)"),
                 "full_iteration_ms": iter_ms,
                 "full_iteration_note": "CostFunctor.value_and_gradient on the resident cloud (fsdf_value_and_gradient: "
                                        "host FK + surface poses, pass, accumulator read-back, chain rule; rank 0, "
@@ -676,6 +802,7 @@ def main():
                                "note": "brute-force F_alg (every plane of every hull, SURVEY.md §8d) per launch / "
                                        "kernel time; culling skips most of it, so the ratio exceeds 1"},
         }
+        out["telemetry"] = TELEMETRY
         if weak is not None:
             out["weak"] = weak
         if world == 1 and not args.no_cpu_baseline:

@@ -21,7 +21,8 @@
  *   EnhancedGJK.NeighborMesh / conv(vertices)   src/models.jl:152
  *                                                     fsdf_convex_hull
  *   transform_to_root(state, frame) src/Flash.jl:248  fsdf_tree_transforms
- *     (RigidBodyDynamics forward kinematics)          (host, per pass)
+ *     (RigidBodyDynamics forward kinematics)          (host, per pass; on the
+ *                                                     device inside fsdf_descend)
  *
  * Conventions
  *   - All host buffers are caller-owned. Nothing is retained past a call
@@ -214,6 +215,15 @@ int fsdf_state_gradient(fsdf_ctx* ctx, const double* x, const double* accum, dou
  * value_out = f of the last evaluation, iterations_out = evaluations made. */
 int fsdf_descend(fsdf_ctx* ctx, double* x, int32_t iteration_limit, double rate, double max_step, double tolerance,
                  const double* divisors, double n_points, double* value_out, int32_t* iterations_out);
+/* Where fsdf_descend iterates for rigid scenes (no RBF skin, no deformation):
+ * device_loop = 1 (default) — every iteration on the device, the frame's
+ * passes and solver steps enqueued up front and read back once (FK, chain rule,
+ * NaiveSolver step in one small workgroup after each pass: the host loop's
+ * arithmetic in the same order, so x, value and iterations are bit-identical
+ * to it; after convergence the remaining launches return at once); 0 — the
+ * host loop around fsdf_value_and_gradient, one synchronization per iteration.
+ * RBF scenes always use the host loop. */
+int fsdf_set_solver(fsdf_ctx* ctx, int32_t device_loop);
 
 /* ---- context ---------------------------------------------------------------- */
 int fsdf_create(fsdf_ctx** out, const fsdf_opts* opts);
@@ -256,7 +266,10 @@ int fsdf_set_points_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n);
  * ranged cloud are always in its resident order, and fsdf_get_permutation names
  * each resident point's index in the whole cloud. fsdf_chunk_costs then reports
  * the range's chunks — the chunks of the whole cloud's order when begin is a
- * multiple of 64 — which is what flash.distributed balances the ranges by. */
+ * multiple of 64 — which is what flash.distributed balances the ranges by; once
+ * the range has been regrouped (fsdf_regroup_points) its chunks are no longer
+ * the whole cloud's and fsdf_chunk_costs refuses (FSDF_ERR_STATE) until the
+ * next set_points. */
 int fsdf_set_points_range(fsdf_ctx* ctx, const double* xyz, int64_t n, int64_t begin, int64_t end);
 int fsdf_set_points_range_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n, int64_t begin, int64_t end);
 int fsdf_num_points(const fsdf_ctx* ctx, int64_t* n_out);
@@ -276,6 +289,20 @@ int fsdf_num_points(const fsdf_ctx* ctx, int64_t* n_out);
  * (sort_points) or ranged cloud and a pass over it (hull-only scenes of <= 64
  * surfaces); asynchronous on the context stream. */
 int fsdf_regroup_points(fsdf_ctx* ctx);
+/* The regroup where it pays, decided by the library: only after a pass that
+ * ran one wave per chunk (the grid above the planned window, bound by its
+ * summed work), on a sorted or ranged cloud not yet regrouped since its
+ * set_points. *applied_out = 1 when it regrouped (NULL allowed).
+ * fsdf_set_regroup: FSDF_REGROUP_AUTO (default) — the iteration entry points
+ * that return no per-point outputs (fsdf_value_and_gradient,
+ * fsdf_eval_state_device, fsdf_descend) apply this rule after a new cloud's
+ * first pass, so track! frames regroup by themselves; FSDF_REGROUP_OFF — only
+ * explicit calls regroup. fsdf_eval / fsdf_eval_device never regroup on their
+ * own (their resident-order outputs index the permutation of the pass). */
+#define FSDF_REGROUP_OFF 0
+#define FSDF_REGROUP_AUTO 1
+int fsdf_regroup_auto(fsdf_ctx* ctx, int32_t* applied_out);
+int fsdf_set_regroup(fsdf_ctx* ctx, int32_t mode);
 
 /* One residual pass over the resident cloud (synchronous, host buffers).
  * poses: [K][12] host. Outputs may be NULL when not wanted:
@@ -385,7 +412,8 @@ int fsdf_set_plan(fsdf_ctx* ctx, int32_t enable, double four_way_share, double t
 /* Diagnostics: the serial-equivalent durations (100 MHz ticks) the last
  * planned pass measured per 64-point chunk of the resident cloud (resident
  * order), as the plan is built from them. *count_out = the chunk count (0
- * before a planned pass); costs_out may be NULL to query it. */
+ * before a planned pass); costs_out may be NULL to query it. FSDF_ERR_STATE
+ * for a ranged cloud that has been regrouped (see fsdf_set_points_range). */
 int fsdf_chunk_costs(fsdf_ctx* ctx, uint32_t* costs_out, int64_t* count_out);
 
 /* Kernel work counters (diagnostics). enable=1 zeroes and starts counting in

@@ -22,6 +22,7 @@
 
 #include "flashsdf.h"
 #include "fsdf_internal.h"
+#include "kin_impl.h"
 
 namespace {
 
@@ -109,6 +110,14 @@ struct fsdf_ctx {
   uint8_t* d_prior = nullptr;        // [n] each resident point's nearest surface in the last pass (seed hint)
   int64_t prior_cap = 0;
   bool prior_ok = false;             // d_prior was written by a pass over the current resident cloud
+  // regroup (fsdf_regroup_points): mode (fsdf_set_regroup), whether the
+  // resident cloud has been regrouped since its set_points, whether its first
+  // iteration pass is still to come (the auto regroup follows that pass), and
+  // the shape of the last resident pass (the auto rule's input)
+  int regroup_mode = FSDF_REGROUP_AUTO;
+  bool regrouped = false;
+  bool regroup_pending = false;
+  int last_pass_shape = 0;           // 0 none, 1 one wave per chunk, 2 hull-partitioned tiers, 3 planned
   int64_t chunk_ws_cap = 0;          // chunks
   fsdf::SortScratch sort;            // per-frame sort scratch (grown only)
   double* d_staging = nullptr;       // host-source clouds land here first
@@ -178,6 +187,18 @@ struct fsdf_ctx {
     std::vector<double> x_pass[2];
     int x_pass_next = 0;
   } mech;
+  // device solver loop of fsdf_descend (solver.hip): the mechanism's device
+  // arrays (built on the first device descend after fsdf_set_mechanism) and
+  // one frame's state; pinned staging for x / divisors in and x, f, flags out
+  int solver_device = 1;             // fsdf_set_solver
+  bool solver_tree_ok = false;
+  fsdf::SolverTree stree;
+  int32_t* d_stree_i = nullptr;
+  double* d_stree_d = nullptr;
+  double* d_solver = nullptr;        // x | div | Rb | tb | poses | f
+  int* d_solver_flags = nullptr;
+  double* h_solver = nullptr;        // pinned: x | div | f | flags (as doubles)
+  size_t solver_cap = 0, h_solver_cap = 0;
 };
 
 static int fail(fsdf_ctx* c, int code, const char* fmt, ...) {
@@ -240,6 +261,9 @@ static void free_model(fsdf_ctx* c) {
   // (the partition tiers are a context setting: they survive a model change)
   const int64_t h4 = c->lm.hpart4_points, h2 = c->lm.hpart2_points;
   c->plan_nc = -1;
+  c->prior_ok = false;        // seeds name surfaces of the old model
+  c->solver_tree_ok = false;  // (its surface list)
+  c->last_pass_shape = 0;
   c->lm = fsdf::LocalModel();
   c->lm.hpart4_points = h4;
   c->lm.hpart2_points = h2;
@@ -311,6 +335,11 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   dfree(c->co.dur);
   dfree(c->d_plan);
   dfree(c->d_plan_order);
+  dfree(c->d_stree_i);
+  dfree(c->d_stree_d);
+  dfree(c->d_solver);
+  dfree(c->d_solver_flags);
+  if (c->h_solver) (void)hipHostFree(c->h_solver);
   for (hipEvent_t e : c->prof_ev) (void)hipEventDestroy(e);
   for (int i = 0; i < kPoseRing; ++i) {
     if (c->pose_ev[i]) (void)hipEventDestroy(c->pose_ev[i]);
@@ -830,6 +859,9 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
     }
   }
   c->prior_ok = false;  // a new cloud: its first pass seeds from the bounds
+  c->regrouped = false;
+  c->regroup_pending = true;  // (the auto regroup follows the new cloud's first iteration pass)
+  c->last_pass_shape = 0;
   // the caller may reuse its buffer once this returns
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   c->n = n;
@@ -879,7 +911,46 @@ extern "C" int fsdf_regroup_points(fsdf_ctx* c) {
   HIPCHECK(c, fsdf::launch_chunk_spheres(c->precision, c->d_pts, c->n, nc, c->d_chunk_ws, c->stream));
   c->plan_nc = -1;       // other chunks: the next planned pass measures anew
   c->order_nblocks = 0;  // and the cost-ordered schedule is rebuilt
+  c->regrouped = true;
+  c->regroup_pending = false;
   return FSDF_OK;
+}
+
+// The auto rule (FSDF_REGROUP_AUTO): regroup where the pass is bound by its
+// summed work — the last resident pass ran one wave per chunk (the grid above
+// the planned window) — and not where the planned pass or a hull-partitioned
+// tier is bound by its heaviest chunk, which grouping makes heavier (2^17 step
+// 0.0612 -> 0.0677 ms and worse). Needs a pass over the
+// cloud (its k* are the groups) and a sorted or ranged cloud.
+static bool regroup_wanted(const fsdf_ctx* c) {
+  return c->n > 0 && c->d_perm && c->prior_ok && !c->regrouped && c->last_pass_shape == 1;
+}
+
+extern "C" int fsdf_regroup_auto(fsdf_ctx* c, int32_t* applied_out) {
+  if (!c) return FSDF_ERR_ARG;
+  if (applied_out) *applied_out = 0;
+  if (!regroup_wanted(c)) return FSDF_OK;
+  const int rc = fsdf_regroup_points(c);
+  if (rc) return rc;
+  if (applied_out) *applied_out = 1;
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_set_regroup(fsdf_ctx* c, int32_t mode) {
+  if (!c) return FSDF_ERR_ARG;
+  if (mode != FSDF_REGROUP_OFF && mode != FSDF_REGROUP_AUTO)
+    return fail(c, FSDF_ERR_ARG, "set_regroup: unknown mode %d", mode);
+  c->regroup_mode = mode;
+  return FSDF_OK;
+}
+
+// after an iteration pass (value_and_gradient, eval_state_device, descend):
+// the new cloud's first one regroups it when the auto rule says so
+static int iteration_regroup(fsdf_ctx* c) {
+  if (!c->regroup_pending) return FSDF_OK;
+  c->regroup_pending = false;
+  if (c->regroup_mode != FSDF_REGROUP_AUTO) return FSDF_OK;
+  return fsdf_regroup_auto(c, nullptr);
 }
 
 static int ensure_partials(fsdf_ctx* c, int nblocks) {
@@ -919,17 +990,24 @@ static int upload_poses(fsdf_ctx* c, const double* poses, hipStream_t st) {
 // buffer index to release with release_posed() after its last reader.
 // Measured: the cross-stream event waits cost more than the overlap saves
 // (+10 us per step on M64), so it is off and the pose kernel runs in order.
-static int pose_model(fsdf_ctx* c, const double* poses, fsdf::PosedModel** out, int* buf) {
+// d_poses_dev (optional): the poses are already on the device (the device
+// solver loop writes them, solver.hip); skip: its done flag.
+static int pose_model(fsdf_ctx* c, const double* poses, fsdf::PosedModel** out, int* buf,
+                      const double* d_poses_dev = nullptr, const int* skip = nullptr) {
   const int b = FSDF_POSE_OVERLAP ? c->pm_next : 0;
   c->pm_next ^= FSDF_POSE_OVERLAP ? 1 : 0;
   fsdf::PosedModel* P = b ? &c->pm_alt : &c->pm;
   P->rbf_rows = c->pm.rbf_rows;  // per-pass RBF rows: one buffer, context-stream ordered
   const hipStream_t ps = FSDF_POSE_OVERLAP ? c->pose_stream : c->stream;
   if (FSDF_POSE_OVERLAP) HIPCHECK(c, hipStreamWaitEvent(ps, c->ev_pm_free[b], 0));
-  int rc = upload_poses(c, poses, ps);
-  if (rc) return rc;
-  HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, c->d_poses, *P, ps,
-                                c->lm.S <= fsdf::kPoseArgMax ? poses : nullptr));
+  if (d_poses_dev) {
+    HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, d_poses_dev, *P, ps, nullptr, skip));
+  } else {
+    int rc = upload_poses(c, poses, ps);
+    if (rc) return rc;
+    HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, c->d_poses, *P, ps,
+                                  c->lm.S <= fsdf::kPoseArgMax ? poses : nullptr));
+  }
   if (FSDF_POSE_OVERLAP) {
     HIPCHECK(c, hipEventRecord(c->ev_pose, ps));
     HIPCHECK(c, hipStreamWaitEvent(c->stream, c->ev_pose, 0));
@@ -1005,7 +1083,7 @@ static void plan_shape(fsdf_ctx* c, int64_t nc, int* n4, int* n2) {
 // plan rebuilt from this pass's chunk durations on the first pass of a cloud
 // and then every kOrderEvery passes.
 static int run_planned(fsdf_ctx* c, const fsdf::PosedModel& P, const void* d_pts, int64_t n, double* d_accum,
-                       fsdf::PassOutputs& out, hipEvent_t* pe) {
+                       fsdf::PassOutputs& out, hipEvent_t* pe, const int* skip) {
   const int64_t nc = (n + 63) / 64;
   int rc = ensure_chunk_outputs(c, nc);
   if (rc) return rc;
@@ -1032,7 +1110,8 @@ static int run_planned(fsdf_ctx* c, const fsdf::PosedModel& P, const void* d_pts
   HIPCHECK(c, fsdf::launch_planned_pass(c->precision, c->cull != 0, c->lm, P, d_pts, n, grid, out, co, c->stream,
                                         pe ? pe[0] : nullptr, pe ? pe[1] : nullptr));
   c->pass_kernel = fsdf::last_pass_kernel();
-  HIPCHECK(c, fsdf::launch_reduce_chunks(co, nc, c->lm.S, c->d_partials, d_accum, c->stream, pe ? pe[2] : nullptr));
+  HIPCHECK(c, fsdf::launch_reduce_chunks(co, nc, c->lm.S, c->d_partials, d_accum, c->stream, pe ? pe[2] : nullptr,
+                                         skip));
   if (!planned || ++c->plan_age >= kOrderEvery) {
     int n4, n2;
     plan_shape(c, nc, &n4, &n2);
@@ -1057,14 +1136,17 @@ static int run_planned(fsdf_ctx* c, const fsdf::PosedModel& P, const void* d_pts
 #endif
 // schedule: resident-cloud passes (repeated over the same cloud) launch their
 // workgroups heaviest-first by the previous pass's durations
+// d_poses_dev / skip: the device solver loop's poses and done flag (pose_model)
 static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t n, double* d_accum,
-                    int32_t* d_kstar, double* d_d, double* d_grad, const int32_t* d_perm, bool schedule) {
+                    int32_t* d_kstar, double* d_d, double* d_grad, const int32_t* d_perm, bool schedule,
+                    const double* d_poses_dev = nullptr, const int* skip = nullptr) {
   if (c->lm.R > 0 && !c->rbf_ready)
     return fail(c, FSDF_ERR_STATE, "eval: the scene has RBF surfaces: call fsdf_set_rbf_params first");
   fsdf::PosedModel* P = nullptr;
   int pbuf = 0;
-  int rc = pose_model(c, poses, &P, &pbuf);
+  int rc = pose_model(c, poses, &P, &pbuf, d_poses_dev, skip);
   if (rc) return rc;
+  const bool resident = d_pts == c->d_pts && n == c->n;
   const int nblocks = fsdf::pass_blocks(n, c->lm);
   rc = ensure_partials(c, nblocks);
   if (rc) return rc;
@@ -1075,14 +1157,16 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
   out.grad = d_grad;
   out.perm = d_perm;
   out.stats = c->stats_on ? c->d_stats : nullptr;
-  out.chunk_ws = FSDF_CHUNK_WS && d_pts == c->d_pts && n == c->n ? c->d_chunk_ws : nullptr;  // resident cloud only
+  out.skip = skip;
+  out.chunk_ws = FSDF_CHUNK_WS && resident ? c->d_chunk_ws : nullptr;  // resident cloud only
   // the previous pass's nearest surfaces as seeds (resident cloud, hull-only
-  // scenes of <= 64 surfaces; fsdf_internal.h PassOutputs::prior_in)
-  const bool prior = FSDF_PRIOR_SEEDS && d_pts == c->d_pts && n == c->n && n > 0 && c->d_prior &&
-                     c->prior_cap >= n && c->lm.R == 0 && c->lm.S <= 64;
+  // scenes of <= 64 surfaces; fsdf_internal.h PassOutputs::prior_in); marked
+  // written (prior_ok) once the pass is launched — stream-ordered, the next
+  // pass reads what this one writes
+  const bool prior = FSDF_PRIOR_SEEDS && resident && n > 0 && c->d_prior && c->prior_cap >= n && c->lm.R == 0 &&
+                     c->lm.S <= 64;
   out.prior_out = prior ? c->d_prior : nullptr;
   out.prior_in = prior && c->prior_ok ? c->d_prior : nullptr;
-  if (prior) c->prior_ok = true;  // (stream-ordered: the next pass reads what this one writes)
   // planned window: (default min, model's default max], or (0, max_points] when set
   const int64_t plan_max = c->plan_max_points >= 0 ? c->plan_max_points : fsdf::planned_default_max_points(c->lm);
   const int64_t plan_min = c->plan_max_points >= 0 ? 0 : fsdf::planned_default_min_points();
@@ -1090,8 +1174,10 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
       fsdf::planned_pass(c->lm, n)) {
     const bool prof = c->profiling && c->prof_used + 3 <= c->prof_ev.size();
     hipEvent_t* pe = prof ? &c->prof_ev[c->prof_used] : nullptr;
-    rc = run_planned(c, *P, d_pts, n, d_accum, out, pe);
+    rc = run_planned(c, *P, d_pts, n, d_accum, out, pe, skip);
     if (rc) return rc;
+    if (prior) c->prior_ok = true;
+    if (resident) c->last_pass_shape = 3;
     if (prof) c->prof_used += 3;
     return release_posed(c, pbuf);
   }
@@ -1111,6 +1197,8 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
     HIPCHECK(c, fsdf::launch_pass(c->precision, c->cull != 0, c->lm, *P, d_pts, n, nblocks, out, c->stream,
                                   pe ? pe[0] : nullptr, pe ? pe[1] : nullptr));
     c->pass_kernel = fsdf::last_pass_kernel();
+    if (prior) c->prior_ok = true;
+    if (resident) c->last_pass_shape = fsdf::hpart_pass(c->lm, n) ? 2 : 1;
     rc = release_posed(c, pbuf);
     if (rc) return rc;
     if (prof) c->prof_used += 3;
@@ -1120,7 +1208,7 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
     const bool rebuild = out.cost && (c->order_nblocks != nblocks || ++c->order_age >= kOrderEvery);
     HIPCHECK(c, fsdf::launch_reduce(c->d_partials, nblocks, accum_len(c), d_accum, c->stream,
                                     rebuild ? out.cost : nullptr, rebuild ? c->d_block_order : nullptr,
-                                    pe ? pe[2] : nullptr));
+                                    pe ? pe[2] : nullptr, skip));
     if (rebuild) {
       c->order_nblocks = nblocks;
       c->order_age = 0;
@@ -1167,6 +1255,11 @@ extern "C" const char* fsdf_pass_kernel_name(const fsdf_ctx* c) { return c ? c->
 
 extern "C" int fsdf_chunk_costs(fsdf_ctx* c, uint32_t* costs_out, int64_t* count_out) {
   if (!c || !count_out) return FSDF_ERR_ARG;
+  // a regrouped range's chunks are no longer the whole cloud's Hilbert chunks:
+  // costs balanced as if they were would place the cut by wrong prefix sums
+  if (c->ranged && c->regrouped)
+    return fail(c, FSDF_ERR_STATE, "chunk_costs: the ranged cloud was regrouped (its chunks are not the whole "
+                                   "cloud's order); gather costs before fsdf_regroup_points");
   const int64_t nc = c->plan_nc > 0 ? c->plan_nc : 0;
   *count_out = nc;
   if (!costs_out || nc == 0) return FSDF_OK;
@@ -1343,6 +1436,7 @@ extern "C" int fsdf_set_mechanism(fsdf_ctx* c, int32_t nb, const int32_t* parent
   M.work.resize(6 * nb);
   M.rbf.clear();  // centre declarations name bodies of the previous tree
   M.x_prepared.clear();
+  c->solver_tree_ok = false;
   return FSDF_OK;
 }
 
@@ -1456,7 +1550,8 @@ static int iteration_prepare(fsdf_ctx* c, const double* x, const char* who, bool
       if (rc) return rc;
     }
   }
-  // surface poses T_world_body · T_body_geometry (identity for surfaces without a body)
+  // surface poses T_world_body · T_body_geometry (identity for surfaces without
+  // a body; kin_impl.h, the device solver's arithmetic too)
   const int S = c->lm.S;
   for (int k = 0; k < S; ++k) {
     double* P = M.poses.data() + 12 * k;
@@ -1465,13 +1560,8 @@ static int iteration_prepare(fsdf_ctx* c, const double* x, const char* who, bool
       for (int i = 0; i < 12; ++i) P[i] = (i % 4 == 0 && i < 9) ? 1.0 : 0.0;
       continue;
     }
-    const double* Rw = M.R.data() + 9 * b;
-    const double* FR = M.frame_R.data() + 9 * k;
-    const double* Ft = M.frame_t.data() + 3 * k;
-    for (int i = 0; i < 3; ++i) {
-      for (int j = 0; j < 3; ++j) P[3 * i + j] = Rw[3 * i] * FR[j] + Rw[3 * i + 1] * FR[3 + j] + Rw[3 * i + 2] * FR[6 + j];
-      P[9 + i] = (Rw[3 * i] * Ft[0] + Rw[3 * i + 1] * Ft[1] + Rw[3 * i + 2] * Ft[2]) + M.t[3 * b + i];
-    }
+    fsdf::kin::surface_pose(M.R.data() + 9 * b, M.t.data() + 3 * b, M.frame_R.data() + 9 * k,
+                            M.frame_t.data() + 3 * k, P);
   }
   M.x_prepared.assign(x, x + M.nq + 3 * M.n_deform);
   return FSDF_OK;
@@ -1542,10 +1632,14 @@ extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cos
   HIPCHECK(c, hipHostGetDevicePointer((void**)&d_acc_host, c->h_acc, 0));
   rc = run_pass(c, M.poses.data(), c->d_pts, c->n, d_acc_host, nullptr, nullptr, nullptr, nullptr, true);
   if (rc) return rc;
+  rc = iteration_regroup(c);  // (stream-ordered after the pass: the sync below covers it)
+  if (rc) return rc;
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   return iteration_finish(c, x, c->h_acc, cost_out, grad_out, "value_and_gradient");
 #else
   rc = run_pass(c, M.poses.data(), c->d_pts, c->n, c->d_accum, nullptr, nullptr, nullptr, nullptr, true);
+  if (rc) return rc;
+  rc = iteration_regroup(c);
   if (rc) return rc;
   M.accum.resize(accum_len(c));
   rc = fetch(c, c->n, nullptr, M.accum.data(), nullptr, nullptr, nullptr, false);
@@ -1558,6 +1652,184 @@ extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cos
 // NaiveSolver restated in flash/tracking.py) around fsdf_value_and_gradient,
 // without a host-language round trip per iteration: f = c/n, g = (∂c/∂x / n)
 // ./ divisors; stop when |g| < tolerance; else x += clamp(-rate g, ±max_step).
+// The device arrays of the mechanism for the solver step (solver.hip) and
+// the level schedules of its parallel FK (bodies by depth) and subtree sums
+// (parents by height, children in descending index: the host's reverse
+// topological loop adds them in that order).
+static int build_solver_tree(fsdf_ctx* c) {
+  auto& M = c->mech;
+  const int nb = M.nb, S = c->lm.S;
+  std::vector<int> depth(nb, 0), height(nb, 0), nchild(nb, 0);
+  for (int b = 1; b < nb; ++b) depth[b] = depth[M.parent[b]] + 1;
+  for (int b = nb - 1; b >= 1; --b) {
+    const int p = M.parent[b];
+    height[p] = std::max(height[p], height[b] + 1);
+    ++nchild[p];
+  }
+  int D = 0, H = 0;
+  for (int b = 1; b < nb; ++b) {
+    D = std::max(D, depth[b]);
+    if (nchild[b]) H = std::max(H, height[b]);
+  }
+  std::vector<int32_t> iv;  // parent | kind | qoff | depth_order | depth_off | height_order | height_off |
+                            // child_off | child_list | surf_off | surf_list | surface_body
+  auto put = [&](const std::vector<int32_t>& v) {
+    const size_t at = iv.size();
+    iv.insert(iv.end(), v.begin(), v.end());
+    return at;
+  };
+  std::vector<int32_t> dord, doff(1, 0), hord, hoff(1, 0), coff(1, 0), clist, soff(1, 0), slist;
+  for (int d = 1; d <= D; ++d) {
+    for (int b = 1; b < nb; ++b)
+      if (depth[b] == d) dord.push_back(b);
+    doff.push_back((int32_t)dord.size());
+  }
+  for (int h = 1; h <= H; ++h) {
+    for (int b = 1; b < nb; ++b)
+      if (nchild[b] && height[b] == h) hord.push_back(b);
+    hoff.push_back((int32_t)hord.size());
+  }
+  for (int p = 0; p < nb; ++p) {
+    for (int b = nb - 1; b > p; --b)
+      if (M.parent[b] == p) clist.push_back(b);
+    coff.push_back((int32_t)clist.size());
+    for (int k = 0; k < S; ++k)
+      if (M.surface_body[k] == p) slist.push_back(k);
+    soff.push_back((int32_t)slist.size());
+  }
+  const size_t o_parent = put(M.parent), o_kind = put(M.kind), o_qoff = put(M.qoff), o_dord = put(dord),
+               o_doff = put(doff), o_hord = put(hord), o_hoff = put(hoff), o_coff = put(coff), o_clist = put(clist),
+               o_soff = put(soff), o_slist = put(slist), o_sb = put(M.surface_body);
+  std::vector<double> dv;
+  auto putd = [&](const std::vector<double>& v) {
+    const size_t at = dv.size();
+    dv.insert(dv.end(), v.begin(), v.end());
+    return at;
+  };
+  const size_t o_axis = putd(M.axis), o_AR = putd(M.AR), o_At = putd(M.At), o_BR = putd(M.BR), o_Bt = putd(M.Bt),
+               o_FR = putd(M.frame_R), o_Ft = putd(M.frame_t);
+  HIPCHECK(c, hipStreamSynchronize(c->stream));  // (a previous frame's steps may still read the old arrays)
+  dfree(c->d_stree_i);
+  dfree(c->d_stree_d);
+  HIPCHECK(c, hipMalloc(&c->d_stree_i, std::max<size_t>(iv.size(), 1) * sizeof(int32_t)));
+  HIPCHECK(c, hipMalloc(&c->d_stree_d, std::max<size_t>(dv.size(), 1) * sizeof(double)));
+  HIPCHECK(c, hipMemcpy(c->d_stree_i, iv.data(), iv.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPCHECK(c, hipMemcpy(c->d_stree_d, dv.data(), dv.size() * sizeof(double), hipMemcpyHostToDevice));
+  fsdf::SolverTree& T = c->stree;
+  const int32_t* I = c->d_stree_i;
+  const double* F = c->d_stree_d;
+  T.nb = nb;
+  T.nx = M.nq;
+  T.S = S;
+  T.D = D;
+  T.H = H;
+  T.parent = I + o_parent;
+  T.kind = I + o_kind;
+  T.qoff = I + o_qoff;
+  T.depth_order = I + o_dord;
+  T.depth_off = I + o_doff;
+  T.height_order = I + o_hord;
+  T.height_off = I + o_hoff;
+  T.child_off = I + o_coff;
+  T.child_list = I + o_clist;
+  T.surf_off = I + o_soff;
+  T.surf_list = I + o_slist;
+  T.surface_body = I + o_sb;
+  T.axis = F + o_axis;
+  T.AR = F + o_AR;
+  T.At = F + o_At;
+  T.BR = F + o_BR;
+  T.Bt = F + o_Bt;
+  T.frame_R = F + o_FR;
+  T.frame_t = F + o_Ft;
+  c->solver_tree_ok = true;
+  return FSDF_OK;
+}
+
+// fsdf_descend for rigid scenes, every iteration on the device: solver_init
+// (FK of x0 -> poses), then per iteration pose -> pass -> reduce -> solver
+// step, all enqueued up front; one read-back of x, f and the count at the end.
+// Bit-identical to the host loop below (solver.hip).
+static int descend_device(fsdf_ctx* c, double* x, int32_t iteration_limit, double rate, double max_step,
+                          double tolerance, const double* divisors, double n_points, double* value_out,
+                          int32_t* iterations_out) {
+  auto& M = c->mech;
+  const int nx = M.nq, nb = M.nb, S = c->lm.S;
+  HIPCHECK(c, hipSetDevice(c->device));
+  if (!c->solver_tree_ok) {
+    const int rc = build_solver_tree(c);
+    if (rc) return rc;
+  }
+  // device: x [nx] | div [nx] | Rb [9 nb] | tb [3 nb] | poses [12 S] | f; flags [4] int
+  const size_t need = (size_t)2 * nx + 12 * (size_t)nb + 12 * (size_t)S + 1;
+  if (c->solver_cap < need) {
+    HIPCHECK(c, hipStreamSynchronize(c->stream));
+    dfree(c->d_solver);
+    c->solver_cap = 0;
+    HIPCHECK(c, hipMalloc(&c->d_solver, need * sizeof(double)));
+    c->solver_cap = need;
+  }
+  if (!c->d_solver_flags) HIPCHECK(c, hipMalloc(&c->d_solver_flags, 4 * sizeof(int)));
+  // pinned: x [nx] | div [nx] | f | flags [4] (as 2 doubles)
+  const size_t hneed = (size_t)2 * nx + 3;
+  if (c->h_solver_cap < hneed) {
+    if (c->h_solver) HIPCHECK(c, hipHostFree(c->h_solver));
+    c->h_solver = nullptr;
+    c->h_solver_cap = 0;
+    HIPCHECK(c, hipHostMalloc((void**)&c->h_solver, hneed * sizeof(double), hipHostMallocDefault));
+    c->h_solver_cap = hneed;
+  }
+  double* h = c->h_solver;
+  HIPCHECK(c, hipStreamSynchronize(c->stream));  // (the pinned staging of an earlier frame is free)
+  memcpy(h, x, (size_t)nx * sizeof(double));
+  if (divisors) memcpy(h + nx, divisors, (size_t)nx * sizeof(double));
+  HIPCHECK(c, hipMemcpyAsync(c->d_solver, h, (size_t)(divisors ? 2 : 1) * nx * sizeof(double),
+                             hipMemcpyHostToDevice, c->stream));
+  fsdf::SolverState st;
+  st.x = c->d_solver;
+  st.div = divisors ? c->d_solver + nx : nullptr;
+  st.Rb = c->d_solver + 2 * nx;
+  st.tb = st.Rb + 9 * nb;
+  st.poses = st.tb + 3 * nb;
+  st.f = st.poses + 12 * S;
+  st.flags = c->d_solver_flags;
+  st.rate = rate;
+  st.max_step = max_step;
+  st.tol = tolerance;
+  st.n_points = n_points;
+  st.weight = M.weight;
+  st.limit = iteration_limit;
+  HIPCHECK(c, fsdf::launch_solver_init(c->stree, st, c->stream));
+  for (int it = 0; it < iteration_limit; ++it) {
+    int rc = run_pass(c, nullptr, c->d_pts, c->n, c->d_accum, nullptr, nullptr, nullptr, nullptr, true, st.poses,
+                      st.flags);
+    if (rc) return rc;
+    if (it == 0) {
+      rc = iteration_regroup(c);
+      if (rc) return rc;
+    }
+    HIPCHECK(c, fsdf::launch_solver_step(c->stree, st, c->d_accum, c->stream));
+  }
+  HIPCHECK(c, hipMemcpyAsync(h, st.x, (size_t)nx * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(c, hipMemcpyAsync(h + 2 * nx, st.f, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(c, hipMemcpyAsync(h + 2 * nx + 1, st.flags, 4 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  int flags[4];
+  memcpy(flags, h + 2 * nx + 1, sizeof flags);
+  memcpy(x, h, (size_t)nx * sizeof(double));
+  if (iterations_out) *iterations_out = flags[1];
+  if (flags[2] == 2) return fail(c, FSDF_ERR_ARG, "descend: poses not finite (configuration diverged)");
+  if (flags[2]) return fail(c, FSDF_ERR_ARG, "descend: forward kinematics / chain rule (bad configuration)");
+  if (value_out) *value_out = h[2 * nx];
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_set_solver(fsdf_ctx* c, int32_t device_loop) {
+  if (!c) return FSDF_ERR_ARG;
+  c->solver_device = device_loop != 0;
+  return FSDF_OK;
+}
+
 extern "C" int fsdf_descend(fsdf_ctx* c, double* x, int32_t iteration_limit, double rate, double max_step,
                             double tolerance, const double* divisors, double n_points, double* value_out,
                             int32_t* iterations_out) {
@@ -1566,6 +1838,14 @@ extern "C" int fsdf_descend(fsdf_ctx* c, double* x, int32_t iteration_limit, dou
   if (!x || iteration_limit < 0 || !(n_points > 0.0) || !std::isfinite(rate) || !(max_step >= 0.0))
     return fail(c, FSDF_ERR_ARG, "descend: bad arguments");
   if (c->mech.nb == 0) return fail(c, FSDF_ERR_STATE, "descend: no mechanism (call fsdf_set_mechanism)");
+  const auto& Mc = c->mech;
+  if ((int)Mc.surface_body.size() != c->lm.S || (int)Mc.poses.size() != 12 * c->lm.S)
+    return fail(c, FSDF_ERR_STATE, "descend: mechanism registered for another surface list (call fsdf_set_mechanism)");
+  // rigid scenes (no RBF skin, no deformation) iterate on the device
+  if (c->solver_device && iteration_limit > 0 && c->lm.R == 0 && Mc.n_deform == 0 && c->n > 0 &&
+      fsdf::solver_fits(Mc.nb, Mc.nq))
+    return descend_device(c, x, iteration_limit, rate, max_step, tolerance, divisors, n_points, value_out,
+                          iterations_out);
   const int ns = c->mech.nq + 3 * c->mech.n_deform;
   std::vector<double> g(ns);
   double f = 0.0;
@@ -1597,6 +1877,8 @@ extern "C" int fsdf_eval_state_device(fsdf_ctx* c, const double* x, double* d_ac
   int rc = iteration_prepare(c, x, "eval_state_device");
   if (rc) return rc;
   rc = run_pass(c, c->mech.poses.data(), c->d_pts, c->n, d_accum, nullptr, nullptr, nullptr, nullptr, true);
+  if (rc) return rc;
+  rc = iteration_regroup(c);
   if (rc) return rc;
   auto& M = c->mech;
   M.x_pass[M.x_pass_next] = M.x_prepared;

@@ -143,6 +143,9 @@ struct PassOutputs {
   // this pass. prior_in is null on a cloud's first pass.
   const uint8_t* prior_in = nullptr;
   uint8_t* prior_out = nullptr;
+  // optional device flag: set, the launch returns at once (the passes a
+  // converged device solver loop still has queued, solver.hip)
+  const int* skip = nullptr;
 };
 
 // Planned pass (sdf_kernels.hip planned_pass_kernel): per-chunk partial rows
@@ -180,7 +183,7 @@ hipError_t launch_planned_pass(int precision, bool cull, const LocalModel& lm, c
 // the unplanned pass's tile reduce over them
 int64_t reduce_chunk_groups(int64_t nc);
 hipError_t launch_reduce_chunks(const ChunkOutputs& co, int64_t nc, int S, double* partials, double* d_accum,
-                                hipStream_t s, hipEvent_t ev_stop = nullptr);
+                                hipStream_t s, hipEvent_t ev_stop = nullptr, const int* skip = nullptr);
 // the plan of the next passes from the chunk durations of this one
 hipError_t launch_plan(const uint32_t* dur, int64_t nc, int n4, int n2, int32_t* order, int32_t* plan, hipStream_t s);
 
@@ -194,7 +197,8 @@ struct PoseArgs {
 // precision: 64 or 32. Points are AoS of the matching precision. h_poses (host,
 // S <= kPoseArgMax) are passed by value in the launch; otherwise d_poses is read.
 hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_poses,
-                       const PosedModel& pm, hipStream_t s, const double* h_poses = nullptr);
+                       const PosedModel& pm, hipStream_t s, const double* h_poses = nullptr,
+                       const int* skip = nullptr);
 
 // ev_start / ev_stop (optional): timing events stamped by the pass kernel's
 // dispatch itself (hipExtLaunchKernel), not by packets of their own
@@ -210,7 +214,7 @@ hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const 
 // blocks first) from this pass's costs, for the next pass of the same grid.
 hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum,
                          hipStream_t s, const uint32_t* cost = nullptr, int32_t* order = nullptr,
-                         hipEvent_t ev_stop = nullptr);
+                         hipEvent_t ev_stop = nullptr, const int* skip = nullptr);
 
 hipError_t launch_to_f32(const double* src, float* dst, int64_t count, hipStream_t s);
 
@@ -251,6 +255,41 @@ hipError_t sort_points_spatial(const double* d_src, int64_t n, int precision, vo
 // Asynchronous on `st`.
 hipError_t regroup_points(void** d_pts, int64_t* pts_cap, int64_t n, int precision, int32_t* d_perm, uint8_t* prior,
                           SortScratch& s, hipStream_t st);
+// ---- device solver iteration (solver.hip) ------------------------------------
+// The mechanism of a rigid scene, device arrays built by the context from
+// fsdf_set_mechanism (capi.hip descend_device), with the level schedules of
+// the parallel FK and chain rule:
+struct SolverTree {
+  int nb = 0, nx = 0, S = 0;
+  int D = 0;  // depth levels of bodies >= 1: depth_order[depth_off[d] .. depth_off[d+1]) at depth d+1
+  int H = 0;  // height levels of bodies with children: height_order[height_off[h] .. ) at height h+1
+  const int32_t *parent = nullptr, *kind = nullptr, *qoff = nullptr;
+  const int32_t *depth_order = nullptr, *depth_off = nullptr, *height_order = nullptr, *height_off = nullptr;
+  const int32_t *child_off = nullptr, *child_list = nullptr;  // [nb+1], children in descending index
+  const int32_t *surf_off = nullptr, *surf_list = nullptr;    // [nb+1], surfaces in ascending index
+  const int32_t* surface_body = nullptr;                      // [S]
+  const double *axis = nullptr, *AR = nullptr, *At = nullptr, *BR = nullptr, *Bt = nullptr;
+  const double *frame_R = nullptr, *frame_t = nullptr;        // [S][9], [S][3]
+};
+// One frame's solver state (device): x [nx], optional divisors [nx], the joint
+// frames of the last FK (Rb [nb][9], tb [nb][3]), the poses the next pass reads
+// [S][12], f = the last evaluation's cost / n_points, flags [3] = (done — the
+// skip flag of the frame's launches —, iterations, error: 1 FK / chain rule,
+// 2 a non-finite pose).
+struct SolverState {
+  double* x = nullptr;
+  const double* div = nullptr;
+  double *Rb = nullptr, *tb = nullptr, *poses = nullptr, *f = nullptr;
+  int* flags = nullptr;
+  double rate = 0.0, max_step = 0.0, tol = 0.0, n_points = 1.0, weight = 0.0;
+  int limit = 0;
+};
+bool solver_fits(int nb, int nx);  // the step's LDS carve fits one workgroup
+// FK of st.x -> poses, Rb, tb; flags = (error != 0, 0, error)
+hipError_t launch_solver_init(const SolverTree& T, const SolverState& st, hipStream_t s);
+// one NaiveSolver iteration from the pass's accumulator (skips once flags[0] is set)
+hipError_t launch_solver_step(const SolverTree& T, const SolverState& st, const double* d_accum, hipStream_t s);
+
 // d_out[i] = d_perm[i] as int64 (fsdf_get_permutation's layout)
 hipError_t widen_permutation(const int32_t* d_perm, int64_t n, int64_t* d_out, hipStream_t st);
 

@@ -190,11 +190,15 @@ __device__ __forceinline__ void pose_body(const LocalModel& lm, const double* __
 // surfaces — straight from the kernel arguments: the launch carries the 12·S
 // doubles, each workgroup copies them into LDS, and the per-pass host-to-device
 // copy (a blit kernel of its own) disappears from the step.
+// skip (optional): a device flag; set, the launch does nothing (the device
+// solver loop's passes after convergence, solver.hip)
 template <typename T>
 __global__ __launch_bounds__(kBlock) void pose_kernel(LocalModel lm, const double* __restrict__ poses,
                                                       T* __restrict__ planes_w, float* __restrict__ spheres_w,
                                                       T* __restrict__ verts_w, T* __restrict__ hscale_w,
-                                                      float* __restrict__ screen_w, I4* __restrict__ image_w) {
+                                                      float* __restrict__ screen_w, I4* __restrict__ image_w,
+                                                      const int* __restrict__ skip) {
+  if (skip && *skip) return;
   pose_body<T>(lm, poses, planes_w, spheres_w, verts_w, hscale_w, screen_w, image_w);
 }
 template <typename T>
@@ -1608,6 +1612,7 @@ template <typename T, int SLOTS, bool CULL, bool RBF, bool ALIAS = false, bool H
 __global__ __launch_bounds__(NB) __attribute__((
     amdgpu_waves_per_eu((SLOTS == 1 ? kPassWavesPerSimd : (SLOTS == 2 ? 3 : 2)) - (RBF ? 1 : 0)))) void pass_kernel(
     const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out) {
+  if (out.skip && *out.skip) return;  // (uniform: a converged device solver loop)
   static_assert(!ALIAS || (SLOTS == 1 && !RBF), "aliased wrench rows: hull-only, <= 64 surfaces");
   static_assert(!HPART || ALIAS, "the hull-partitioned pass is an aliased pass");
   constexpr int kParts = HPART ? NPART : 1;
@@ -1873,6 +1878,7 @@ template <typename T, bool CULL>
 __global__ __launch_bounds__(kPassBlock) __attribute__((amdgpu_waves_per_eu(kPassWavesPerSimd))) void planned_pass_kernel(
     const T* __restrict__ pts, int64_t n, PassModel<T> m, PassOutputs out, ChunkOutputs co) {
   static_assert(kPassBlock == 256, "the planned pass runs 4-wave workgroups");
+  if (out.skip && *out.skip) return;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   HullRow* ht = (HullRow*)fsdf_lds;
@@ -1976,7 +1982,9 @@ __global__ __launch_bounds__(kGroupBlock) void chunk_groups_kernel(const I4* __r
                                                                    const double* __restrict__ ent,
                                                                    const double* __restrict__ csum,
                                                                    const double* __restrict__ dense, int nc, int S,
-                                                                   double* __restrict__ partials, int ngroups) {
+                                                                   double* __restrict__ partials, int ngroups,
+                                                                   const int* __restrict__ skip) {
+  if (skip && *skip) return;
   const int len = 1 + 6 * S;
   const int g = blockIdx.x, tid = threadIdx.x;
   const int c0 = g * kGroupChunks;
@@ -2204,7 +2212,9 @@ __device__ void build_order(const uint32_t* __restrict__ cost, int nb, int32_t* 
 // (deterministic). The schedule rebuild is a launch of its own (order_kernel).
 constexpr int kTileBlock = 1024;
 __global__ __launch_bounds__(kTileBlock) void reduce_tiles_kernel(const double* __restrict__ partials, int nblocks,
-                                                                  int len, double* __restrict__ accum) {
+                                                                  int len, double* __restrict__ accum,
+                                                                  const int* __restrict__ skip) {
+  if (skip && *skip) return;
   const int x = blockIdx.x;
   typedef double D2 __attribute__((ext_vector_type(2)));
   const D2* tile = (const D2*)(partials + (int64_t)x * nblocks * 8);
@@ -2322,7 +2332,7 @@ int pass_blocks(int64_t n, const LocalModel& lm) {
 }
 
 hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_poses, const PosedModel& pm,
-                       hipStream_t s, const double* h_poses) {
+                       hipStream_t s, const double* h_poses, const int* skip) {
   const int total = ((lm.F + lm.V + 63) & ~63) + 64 * lm.K;
   if (total == 0) return hipSuccess;  // RBF-only scene: nothing to pose
   const int grid = (total + kBlock - 1) / kBlock;
@@ -2340,10 +2350,10 @@ hipError_t launch_pose(int precision, const LocalModel& lm, const double* d_pose
   if (precision == 64) {
     hipLaunchKernelGGL(pose_kernel<double>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses,
                        (double*)pm.planes_w, pm.spheres_w, (double*)pm.verts_w, (double*)pm.hscale_w,
-                       pm.screen_w, (I4*)pm.image_w);
+                       pm.screen_w, (I4*)pm.image_w, skip);
   } else {
     hipLaunchKernelGGL(pose_kernel<float>, dim3(grid), dim3(kBlock), 0, s, lm, d_poses, (float*)pm.planes_w,
-                       pm.spheres_w, (float*)pm.verts_w, (float*)pm.hscale_w, (float*)nullptr, (I4*)nullptr);
+                       pm.spheres_w, (float*)pm.verts_w, (float*)pm.hscale_w, (float*)nullptr, (I4*)nullptr, skip);
   }
   return hipGetLastError();
 }
@@ -2539,13 +2549,13 @@ hipError_t launch_raycast(int precision, bool cull, const LocalModel& lm, const 
 }
 
 hipError_t launch_reduce(const double* partials, int nblocks, int len, double* d_accum, hipStream_t s,
-                         const uint32_t* cost, int32_t* order, hipEvent_t ev_stop) {
+                         const uint32_t* cost, int32_t* order, hipEvent_t ev_stop, const int* skip) {
   if (ev_stop)
     hipExtLaunchKernelGGL(reduce_tiles_kernel, dim3((len + 7) / 8), dim3(kTileBlock), 0u, s, nullptr, ev_stop, 0u,
-                          partials, nblocks, len, d_accum);
+                          partials, nblocks, len, d_accum, skip);
   else
     hipLaunchKernelGGL(reduce_tiles_kernel, dim3((len + 7) / 8), dim3(kTileBlock), 0, s, partials, nblocks, len,
-                       d_accum);
+                       d_accum, skip);
   if (cost) hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kBlock), 0, s, cost, nblocks, order);
   return hipGetLastError();
 }
@@ -2587,13 +2597,13 @@ hipError_t launch_planned_pass(int precision, bool cull, const LocalModel& lm, c
 }
 
 hipError_t launch_reduce_chunks(const ChunkOutputs& co, int64_t nc, int S, double* partials, double* d_accum,
-                                hipStream_t s, hipEvent_t ev_stop) {
+                                hipStream_t s, hipEvent_t ev_stop, const int* skip) {
   const int len = 1 + 6 * S;
   const int ngroups = (int)reduce_chunk_groups(nc);
   const size_t lds = (size_t)kGroupChunks * len * sizeof(double) + kGroupChunks * sizeof(I4);
   hipLaunchKernelGGL(chunk_groups_kernel, dim3(ngroups), dim3(kGroupBlock), lds, s, (const I4*)co.hdr, co.ent, co.csum,
-                     co.dense, (int)nc, S, partials, ngroups);
-  return launch_reduce(partials, ngroups, len, d_accum, s, nullptr, nullptr, ev_stop);
+                     co.dense, (int)nc, S, partials, ngroups, skip);
+  return launch_reduce(partials, ngroups, len, d_accum, s, nullptr, nullptr, ev_stop, skip);
 }
 
 int64_t reduce_chunk_groups(int64_t nc) { return (nc + kGroupChunks - 1) / kGroupChunks; }

@@ -66,6 +66,9 @@ _PROTOS = {
     "fsdf_set_points_range": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_int64]),
     "fsdf_set_points_range_device": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_int64]),
     "fsdf_regroup_points": (c_int32, [c_void_p]),
+    "fsdf_regroup_auto": (c_int32, [c_void_p, POINTER(c_int32)]),
+    "fsdf_set_regroup": (c_int32, [c_void_p, c_int32]),
+    "fsdf_set_solver": (c_int32, [c_void_p, c_int32]),
     "fsdf_num_points": (c_int32, [c_void_p, POINTER(c_int64)]),
     "fsdf_eval": (c_int32, [c_void_p, c_void_p, POINTER(c_double), c_void_p, c_void_p, c_void_p, c_void_p]),
     "fsdf_eval_device": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -249,6 +252,27 @@ class Context:
         check(self._lib.fsdf_set_points_range(self._ctx, ptr(pts), pts.shape[0], int(begin), int(end)), self._ctx,
               "set_points_range")
         self.n = int(end) - int(begin)
+
+    def regroup_auto(self) -> bool:
+        """fsdf_regroup_auto: regroup only where the library's rule says it pays
+        (the last pass ran one wave per chunk); True when it regrouped."""
+        applied = c_int32(0)
+        check(self._lib.fsdf_regroup_auto(self._ctx, ctypes.byref(applied)), self._ctx, "regroup_auto")
+        return bool(applied.value)
+
+    REGROUP_OFF, REGROUP_AUTO = 0, 1
+
+    def set_regroup(self, auto: bool):
+        """fsdf_set_regroup: the iteration entry points (value_and_gradient,
+        eval_state_device, descend) regroup a new cloud after its first pass by
+        the auto rule (default), or never on their own."""
+        check(self._lib.fsdf_set_regroup(self._ctx, self.REGROUP_AUTO if auto else self.REGROUP_OFF), self._ctx,
+              "set_regroup")
+
+    def set_solver(self, device_loop: bool):
+        """fsdf_set_solver: descend's iterations on the device (rigid scenes;
+        default) or the host loop around value_and_gradient."""
+        check(self._lib.fsdf_set_solver(self._ctx, int(bool(device_loop))), self._ctx, "set_solver")
 
     def regroup_points(self):
         """Regroup the resident cloud by each point's nearest surface in the

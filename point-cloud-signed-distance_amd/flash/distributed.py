@@ -25,6 +25,8 @@ from __future__ import annotations
 
 import numpy as np
 
+from ._lib import FlashNativeError
+
 from .core import ConvexGeometry, Manipulator, ManipulatorState, prepare_pass
 from .gradientdescent import (_regularizer, default_deformation_cost_weight, gradient_from_accum, native_capable,
                               normalize, register_native, unflatten)
@@ -87,17 +89,21 @@ def spatial_bounds(n: int, world: int, chunk_costs=None) -> list[tuple[int, int]
     return [(min(CHUNK * a, n), min(CHUNK * b, n)) for a, b in zip(cuts[:-1], cuts[1:])]
 
 
-def gather_chunk_costs(local_costs, group=None) -> np.ndarray:
+def gather_chunk_costs(local_costs, group=None, device=None) -> np.ndarray:
     """The ranks' per-chunk costs concatenated in rank order (the whole cloud's
     chunk order when the shards are spatial_bounds ranges): one all_gather of
-    the padded arrays — a control-path collective, once per rebalance."""
+    the padded arrays — a control-path collective, once per rebalance. device:
+    the rank's GPU for an RCCL group (default: the current device)."""
     import torch
     import torch.distributed as dist
     local = np.asarray(local_costs, np.float64).reshape(-1)
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return local
     world = dist.get_world_size(group)
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
     cnt = torch.tensor([local.shape[0]], dtype=torch.int64, device=dev)
     cnts = [torch.zeros_like(cnt) for _ in range(world)]
     dist.all_gather(cnts, cnt, group=group)
@@ -297,7 +303,12 @@ class ShardedCostFunctor:
         ranges. Returns the new bounds."""
         if not self.spatial:
             raise ValueError("rebalance: not a spatial shard")
-        costs = gather_chunk_costs(self.ctx.chunk_costs(), self.group)
+        try:
+            local = self.ctx.chunk_costs()
+        except FlashNativeError:  # a regrouped range (its chunks are not the whole cloud's): keep the ranges
+            local = np.zeros(0)
+        # (every rank joins the all-gather; a short list on any rank keeps every rank's ranges)
+        costs = gather_chunk_costs(local, self.group, device=None if self.dev.type == "cpu" else self.dev)
         nc = -(-self.cloud_n // CHUNK)
         if costs.shape[0] != nc:  # (no planned pass measured every chunk: keep the ranges)
             return self.bounds

@@ -27,6 +27,9 @@
 #                   irb140 | arm_grid, SIZES and EXTRA arguments comma-separated) -> hpart_sweep_MODEL*.jsonl
 #   inflight:SIZES[:EXTRA]  independent passes in flight (tools/inflight_probe.py)  -> inflight.jsonl
 #   split:MODEL:N   speed-up of 2- / 4-wave chunk splits at N points (tools/split_speedup.py) -> split_speedup.jsonl
+#   abdriver        the driver's exact bench command, interleaved twice: HEAD, round 4 (abr/r04, an extracted
+#                   1ef061e tree built in-tree), HEAD --no-regroup; device telemetry around each; then the
+#                   rocprofv3 kernel trace of the same command at HEAD                  -> abdriver/
 #   c5sweep         BASELINE C5 precision sweep on the reference cloud (tools/precision_sweep.py) -> c5_sweep.json
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -166,6 +169,30 @@ for l in open('$O/hpart_sweep_$N.jsonl'):
       timeout -k 10 300 python tools/split_speedup.py --model $M --points $P >> $O/split_speedup.jsonl \
         2>> $O/split_speedup.err || { echo SPLIT FAILED; tail $O/split_speedup.err; exit 1; }
       tail -1 $O/split_speedup.jsonl | cut -c1-600 ;;
+    abdriver)
+      D=$O/abdriver; mkdir -p $D
+      CMD="python3 bench.py --gpus 1 --steps 20 --warmup 5"
+      TEL="import bench, json; print(json.dumps(bench.device_telemetry(0)))"
+      for rep in 1 2; do
+        timeout -k 10 300 $CMD > $D/head_$rep.json 2> $D/head_$rep.err || { echo AB HEAD FAILED; tail $D/head_$rep.err; exit 1; }
+        ( timeout -k 10 60 python3 -c "$TEL" > $D/r04_${rep}_tel0.json && cd abr/r04 && timeout -k 10 300 $CMD ) \
+          > $D/r04_$rep.json 2> $D/r04_$rep.err || { echo AB R04 FAILED; tail $D/r04_$rep.err; exit 1; }
+        timeout -k 10 60 python3 -c "$TEL" > $D/r04_${rep}_tel1.json || exit 1
+        timeout -k 10 300 $CMD --no-regroup > $D/noregroup_$rep.json 2> $D/noregroup_$rep.err \
+          || { echo AB NOREGROUP FAILED; tail $D/noregroup_$rep.err; exit 1; }
+        for f in head r04 noregroup; do python3 -c "
+import json; d = json.load(open('$D/${f}_$rep.json')); c = d['config']; r = d['roofline']
+print('$f $rep', round(d['value'] / 1e9, 3), 'G', round(d['ms_per_step'], 5), 'serial', round(c['serial_step_ms'], 5),
+      'kernel', round(r['kernel_ms'], 5), 'frac', round(r['frac'], 4))"; done
+      done
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d $GRAFT_REPO_ROOT/$D/ktrace -o run -- python3 $GRAFT_REPO_ROOT/bench.py --gpus 1 --steps 20 --warmup 5 \
+          > $GRAFT_REPO_ROOT/$D/ktrace.json 2> $GRAFT_REPO_ROOT/$D/ktrace.err ) || { echo AB KTRACE FAILED; tail $D/ktrace.err; exit 1; }
+      python3 -c "
+import csv, glob
+f = glob.glob('$D/ktrace/**/run_kernel_stats.csv', recursive=True)[0]
+for r in list(csv.DictReader(open(f)))[:4]:
+    print('ktrace', r['Name'][:70], r['Calls'], round(float(r['AverageNs']) / 1e3, 3), 'us')" ;;
     c5sweep)
       timeout -k 10 300 python tools/precision_sweep.py --json $O/c5_sweep.json > $O/c5_sweep.log 2>&1 \
         || { echo C5 SWEEP FAILED; tail $O/c5_sweep.log; exit 1; }

@@ -273,6 +273,23 @@ int fsdf_set_points_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n);
 int fsdf_set_points_range(fsdf_ctx* ctx, const double* xyz, int64_t n, int64_t begin, int64_t end);
 int fsdf_set_points_range_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n, int64_t begin, int64_t end);
 int fsdf_num_points(const fsdf_ctx* ctx, int64_t* n_out);
+/* Spatial shards with O(N/W) ingest per rank (flash.distributed.exchange_points):
+ * each rank uploads only its 1/W slice of the sensed cloud; the ranks agree on
+ * the whole cloud's bounding box (fsdf_cloud_box_device of each slice, then a
+ * 6-double all-reduce), compute each point's 30-bit Hilbert key in it
+ * (fsdf_curve_keys_device: the keys fsdf_set_points orders by), split the key
+ * range into W contiguous ranges from an all-reduced key histogram, move every
+ * point to the rank owning its key over one all-to-all, and each rank makes its
+ * received points resident (fsdf_set_points_keyed_device): ordered by (key,
+ * whole-cloud index) — exactly the whole cloud's sorted order restricted to its
+ * key range — with the whole-cloud indices as the permutation (FSDF_ORDER_RESIDENT
+ * outputs, like fsdf_set_points_range; indices < 2^31). Per-point results are
+ * those of a single context over the whole cloud, bit for bit. box: host
+ * [6] = (lo xyz, hi xyz); all calls synchronous. */
+int fsdf_cloud_box_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n, double* box_out);
+int fsdf_curve_keys_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n, const double* box, uint32_t* d_keys);
+int fsdf_set_points_keyed_device(fsdf_ctx* ctx, const double* d_xyz, const uint32_t* d_keys, const int64_t* d_index,
+                                 int64_t n);
 /* Regroup the resident cloud by each point's nearest surface in the last pass
  * over it, keeping the current (Hilbert) order within each surface's group: a
  * stable device sort, once per frame after its first pass. The reference has no

@@ -193,8 +193,7 @@ struct fsdf_ctx {
   int solver_device = 1;             // fsdf_set_solver
   bool solver_tree_ok = false;
   fsdf::SolverTree stree;
-  int32_t* d_stree_i = nullptr;
-  double* d_stree_d = nullptr;
+  double* d_stree_d = nullptr;       // the tree blob (fsdf::SolverTree::blob)
   double* d_solver = nullptr;        // x | div | Rb | tb | poses | f
   int* d_solver_flags = nullptr;
   double* h_solver = nullptr;        // pinned: x | div | f | flags (as doubles)
@@ -335,7 +334,6 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   dfree(c->co.dur);
   dfree(c->d_plan);
   dfree(c->d_plan_order);
-  dfree(c->d_stree_i);
   dfree(c->d_stree_d);
   dfree(c->d_solver);
   dfree(c->d_solver_flags);
@@ -747,6 +745,8 @@ static int adopt_points_device(fsdf_ctx* c, const double* d_src, int64_t n, void
   return FSDF_OK;
 }
 
+static int finish_resident(fsdf_ctx* c, int64_t n, bool ranged);
+
 // [begin, end): the resident cloud is that range of the whole cloud's order
 // (the Hilbert order of all n points with sort_points, else the caller's);
 // the permutation then holds the points' indices in the whole cloud
@@ -838,7 +838,12 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
     int rc = adopt_points_device(c, d_src, n, &c->d_pts, &c->pts_cap);
     if (rc) return rc;
   }
-  n = nr;  // from here on: the resident cloud
+  return finish_resident(c, nr, ranged || range_call);
+}
+
+// the per-cloud state of a new resident cloud of n points (d_pts / d_perm
+// written, stream-ordered): chunk spheres, seed buffer, plan and regroup state
+static int finish_resident(fsdf_ctx* c, int64_t n, bool ranged) {
   if (n > 0) {  // per-chunk bounding spheres of the resident order (pose-independent)
     // (padded to whole 4-chunk pass workgroups: every wave of a hull-partitioned
     // pass reads its chunk's row, also past the cloud's end)
@@ -867,9 +872,78 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
   c->n = n;
   // (a range call keeps resident-order outputs even when its range is the
   // whole cloud: the caller indexes them through the permutation)
-  c->ranged = ranged || range_call;
+  c->ranged = ranged;
   c->plan_nc = -1;  // a new cloud: its first planned pass runs the default shape and measures
   return FSDF_OK;
+}
+
+// ---- exchanged spatial shards (O(N/W) ingest per rank) ------------------------
+extern "C" int fsdf_cloud_box_device(fsdf_ctx* c, const double* d_xyz, int64_t n, double* box_out) {
+  if (!c) return FSDF_ERR_ARG;
+  if (n < 0 || (n > 0 && !d_xyz) || !box_out) return fail(c, FSDF_ERR_ARG, "cloud_box_device: bad arguments");
+  HIPCHECK(c, hipSetDevice(c->device));
+  if (n == 0) {
+    for (int j = 0; j < 3; ++j) {
+      box_out[j] = HUGE_VAL;
+      box_out[3 + j] = -HUGE_VAL;
+    }
+    return FSDF_OK;
+  }
+  double* d_box = nullptr;
+  hipError_t e = fsdf::cloud_box(d_xyz, n, c->sort, c->stream, &d_box);
+  if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "cloud_box_device: %s", hipGetErrorString(e));
+  HIPCHECK(c, hipMemcpyAsync(box_out, d_box, 6 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_curve_keys_device(fsdf_ctx* c, const double* d_xyz, int64_t n, const double* box,
+                                      uint32_t* d_keys) {
+  if (!c) return FSDF_ERR_ARG;
+  if (n < 0 || (n > 0 && (!d_xyz || !d_keys)) || !box) return fail(c, FSDF_ERR_ARG, "curve_keys_device: bad arguments");
+  for (int j = 0; j < 6; ++j)
+    if (!std::isfinite(box[j])) return fail(c, FSDF_ERR_ARG, "curve_keys_device: box not finite");
+  HIPCHECK(c, hipSetDevice(c->device));
+  if (n == 0) return FSDF_OK;
+  double* d_box = nullptr;  // (the scratch's box slot, filled from the host)
+  hipError_t e = fsdf::cloud_box(d_xyz, 0, c->sort, c->stream, &d_box);
+  if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "curve_keys_device: %s", hipGetErrorString(e));
+  HIPCHECK(c, hipStreamSynchronize(c->stream));  // (an earlier sort may still read the slot)
+  HIPCHECK(c, hipMemcpy(d_box, box, 6 * sizeof(double), hipMemcpyHostToDevice));
+  e = fsdf::curve_keys(d_xyz, n, d_box, d_keys, c->stream);
+  if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "curve_keys_device: %s", hipGetErrorString(e));
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_set_points_keyed_device(fsdf_ctx* c, const double* d_xyz, const uint32_t* d_keys,
+                                            const int64_t* d_index, int64_t n) {
+  if (!c) return FSDF_ERR_ARG;
+  if (n < 0 || (n > 0 && (!d_xyz || !d_keys || !d_index)))
+    return fail(c, FSDF_ERR_ARG, "set_points_keyed_device: bad arguments");
+  if (n > INT32_MAX) return fail(c, FSDF_ERR_ARG, "set_points_keyed_device: < 2^31 points per shard");
+  HIPCHECK(c, hipSetDevice(c->device));
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  c->n = 0;
+  const size_t tsz = c->precision == 64 ? sizeof(double) : sizeof(float);
+  if (c->pts_cap < n || !c->d_pts) {
+    dfree(c->d_pts);
+    c->pts_cap = 0;
+    HIPCHECK(c, hipMalloc(&c->d_pts, (size_t)std::max<int64_t>(n, 1) * 3 * tsz));
+    c->pts_cap = std::max<int64_t>(n, 1);
+  }
+  if (c->perm_cap < n || !c->d_perm) {
+    dfree(c->d_perm);
+    c->perm_cap = 0;
+    HIPCHECK(c, hipMalloc(&c->d_perm, (size_t)std::max<int64_t>(n, 1) * sizeof(int32_t)));
+    c->perm_cap = std::max<int64_t>(n, 1);
+  }
+  if (n > 0) {
+    hipError_t e = fsdf::sort_points_keyed(d_xyz, d_keys, d_index, n, c->precision, c->d_pts, c->d_perm, c->sort,
+                                           c->stream);
+    if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "set_points_keyed_device (sort): %s", hipGetErrorString(e));
+  }
+  return finish_resident(c, n, true);
 }
 
 extern "C" int fsdf_set_points(fsdf_ctx* c, const double* xyz, int64_t n) {
@@ -1709,39 +1783,43 @@ static int build_solver_tree(fsdf_ctx* c) {
   const size_t o_axis = putd(M.axis), o_AR = putd(M.AR), o_At = putd(M.At), o_BR = putd(M.BR), o_Bt = putd(M.Bt),
                o_FR = putd(M.frame_R), o_Ft = putd(M.frame_t);
   HIPCHECK(c, hipStreamSynchronize(c->stream));  // (a previous frame's steps may still read the old arrays)
-  dfree(c->d_stree_i);
   dfree(c->d_stree_d);
-  HIPCHECK(c, hipMalloc(&c->d_stree_i, std::max<size_t>(iv.size(), 1) * sizeof(int32_t)));
-  HIPCHECK(c, hipMalloc(&c->d_stree_d, std::max<size_t>(dv.size(), 1) * sizeof(double)));
-  HIPCHECK(c, hipMemcpy(c->d_stree_i, iv.data(), iv.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-  HIPCHECK(c, hipMemcpy(c->d_stree_d, dv.data(), dv.size() * sizeof(double), hipMemcpyHostToDevice));
+  const size_t bytes = dv.size() * sizeof(double) + iv.size() * sizeof(int32_t);
+  const size_t chunks = (bytes + 15) / 16;
+  std::vector<char> blob(chunks * 16, 0);
+  memcpy(blob.data(), dv.data(), dv.size() * sizeof(double));
+  memcpy(blob.data() + dv.size() * sizeof(double), iv.data(), iv.size() * sizeof(int32_t));
+  HIPCHECK(c, hipMalloc(&c->d_stree_d, std::max<size_t>(blob.size(), 16)));
+  HIPCHECK(c, hipMemcpy(c->d_stree_d, blob.data(), blob.size(), hipMemcpyHostToDevice));
   fsdf::SolverTree& T = c->stree;
-  const int32_t* I = c->d_stree_i;
-  const double* F = c->d_stree_d;
   T.nb = nb;
   T.nx = M.nq;
   T.S = S;
   T.D = D;
   T.H = H;
-  T.parent = I + o_parent;
-  T.kind = I + o_kind;
-  T.qoff = I + o_qoff;
-  T.depth_order = I + o_dord;
-  T.depth_off = I + o_doff;
-  T.height_order = I + o_hord;
-  T.height_off = I + o_hoff;
-  T.child_off = I + o_coff;
-  T.child_list = I + o_clist;
-  T.surf_off = I + o_soff;
-  T.surf_list = I + o_slist;
-  T.surface_body = I + o_sb;
-  T.axis = F + o_axis;
-  T.AR = F + o_AR;
-  T.At = F + o_At;
-  T.BR = F + o_BR;
-  T.Bt = F + o_Bt;
-  T.frame_R = F + o_FR;
-  T.frame_t = F + o_Ft;
+  T.blob = c->d_stree_d;
+  T.ni = (int)iv.size();
+  T.nd = (int)dv.size();
+  T.chunks16 = (int)chunks;
+  T.parent = (int)o_parent;
+  T.kind = (int)o_kind;
+  T.qoff = (int)o_qoff;
+  T.depth_order = (int)o_dord;
+  T.depth_off = (int)o_doff;
+  T.height_order = (int)o_hord;
+  T.height_off = (int)o_hoff;
+  T.child_off = (int)o_coff;
+  T.child_list = (int)o_clist;
+  T.surf_off = (int)o_soff;
+  T.surf_list = (int)o_slist;
+  T.surface_body = (int)o_sb;
+  T.axis = (int)o_axis;
+  T.AR = (int)o_AR;
+  T.At = (int)o_At;
+  T.BR = (int)o_BR;
+  T.Bt = (int)o_Bt;
+  T.frame_R = (int)o_FR;
+  T.frame_t = (int)o_Ft;
   c->solver_tree_ok = true;
   return FSDF_OK;
 }
@@ -1816,6 +1894,15 @@ static int descend_device(fsdf_ctx* c, double* x, int32_t iteration_limit, doubl
   HIPCHECK(c, hipStreamSynchronize(c->stream));
   int flags[4];
   memcpy(flags, h + 2 * nx + 1, sizeof flags);
+#ifdef FSDF_SOLVER_TIMES
+  {
+    unsigned long long tt[16];
+    fsdf::solver_times(tt);
+    fprintf(stderr, "solver step phases (10 ns):");
+    for (int i = 1; i < 10; ++i) fprintf(stderr, " %lld", (long long)(tt[i] - tt[0]));
+    fprintf(stderr, "\n");
+  }
+#endif
   memcpy(x, h, (size_t)nx * sizeof(double));
   if (iterations_out) *iterations_out = flags[1];
   if (flags[2] == 2) return fail(c, FSDF_ERR_ARG, "descend: poses not finite (configuration diverged)");
@@ -1841,9 +1928,12 @@ extern "C" int fsdf_descend(fsdf_ctx* c, double* x, int32_t iteration_limit, dou
   const auto& Mc = c->mech;
   if ((int)Mc.surface_body.size() != c->lm.S || (int)Mc.poses.size() != 12 * c->lm.S)
     return fail(c, FSDF_ERR_STATE, "descend: mechanism registered for another surface list (call fsdf_set_mechanism)");
-  // rigid scenes (no RBF skin, no deformation) iterate on the device
+  // rigid scenes (no RBF skin, no deformation) iterate on the device when the
+  // mechanism fits the step's LDS (at most 8 + 2S + depth + height + 4 ints and
+  // 69 nb + 18 S + 3 nx + 1 doubles: M64's 65 bodies take 49 KB)
+  const int ni_max = 8 * Mc.nb + 2 * c->lm.S + 2 * Mc.nb + 4;
   if (c->solver_device && iteration_limit > 0 && c->lm.R == 0 && Mc.n_deform == 0 && c->n > 0 &&
-      fsdf::solver_fits(Mc.nb, Mc.nq))
+      fsdf::solver_fits(Mc.nb, Mc.nq, c->lm.S, ni_max))
     return descend_device(c, x, iteration_limit, rate, max_step, tolerance, divisors, n_points, value_out,
                           iterations_out);
   const int ns = c->mech.nq + 3 * c->mech.n_deform;

@@ -238,7 +238,9 @@ struct SortScratch {
   int32_t* i1 = nullptr;   // alternate index buffer
   void* tmp = nullptr;     // rocPRIM temporary storage
   void* pts = nullptr;     // (regroup_points) the cloud buffer the regrouped points go to
-  size_t part_cap = 0, k_cap0 = 0, k_cap1 = 0, i_cap1 = 0, tmp_cap = 0, pts_cap = 0;
+  uint64_t* q0 = nullptr;  // (sort_points_keyed) composite keys, double-buffered
+  uint64_t* q1 = nullptr;
+  size_t part_cap = 0, k_cap0 = 0, k_cap1 = 0, i_cap1 = 0, tmp_cap = 0, pts_cap = 0, q_cap0 = 0, q_cap1 = 0;
 };
 void free_sort_scratch(SortScratch& s);
 
@@ -256,20 +258,26 @@ hipError_t sort_points_spatial(const double* d_src, int64_t n, int precision, vo
 hipError_t regroup_points(void** d_pts, int64_t* pts_cap, int64_t n, int precision, int32_t* d_perm, uint8_t* prior,
                           SortScratch& s, hipStream_t st);
 // ---- device solver iteration (solver.hip) ------------------------------------
-// The mechanism of a rigid scene, device arrays built by the context from
-// fsdf_set_mechanism (capi.hip descend_device), with the level schedules of
-// the parallel FK and chain rule:
+// The mechanism of a rigid scene as two device buffers built by the context
+// from fsdf_set_mechanism (capi.hip build_solver_tree) — integers and doubles,
+// each array at an offset — with the level schedules of the parallel FK and
+// chain rule. The solver kernels copy both buffers into LDS first, so every
+// later access in their level loops is an LDS access.
 struct SolverTree {
   int nb = 0, nx = 0, S = 0;
   int D = 0;  // depth levels of bodies >= 1: depth_order[depth_off[d] .. depth_off[d+1]) at depth d+1
   int H = 0;  // height levels of bodies with children: height_order[height_off[h] .. ) at height h+1
-  const int32_t *parent = nullptr, *kind = nullptr, *qoff = nullptr;
-  const int32_t *depth_order = nullptr, *depth_off = nullptr, *height_order = nullptr, *height_off = nullptr;
-  const int32_t *child_off = nullptr, *child_list = nullptr;  // [nb+1], children in descending index
-  const int32_t *surf_off = nullptr, *surf_list = nullptr;    // [nb+1], surfaces in ascending index
-  const int32_t* surface_body = nullptr;                      // [S]
-  const double *axis = nullptr, *AR = nullptr, *At = nullptr, *BR = nullptr, *Bt = nullptr;
-  const double *frame_R = nullptr, *frame_t = nullptr;        // [S][9], [S][3]
+  // one blob: the doubles [nd], then the ints [ni], padded to 16 B — copied into
+  // LDS with one batch of 16-B loads per thread (one memory latency)
+  const void* blob = nullptr;
+  int ni = 0, nd = 0, chunks16 = 0;
+  // offsets into the ints
+  int parent = 0, kind = 0, qoff = 0, depth_order = 0, depth_off = 0, height_order = 0, height_off = 0;
+  int child_off = 0, child_list = 0;  // [nb+1], children in descending index
+  int surf_off = 0, surf_list = 0;    // [nb+1], surfaces in ascending index
+  int surface_body = 0;               // [S]
+  // offsets into the doubles
+  int axis = 0, AR = 0, At = 0, BR = 0, Bt = 0, frame_R = 0, frame_t = 0;  // frames: [S][9], [S][3]
 };
 // One frame's solver state (device): x [nx], optional divisors [nx], the joint
 // frames of the last FK (Rb [nb][9], tb [nb][3]), the poses the next pass reads
@@ -284,11 +292,25 @@ struct SolverState {
   double rate = 0.0, max_step = 0.0, tol = 0.0, n_points = 1.0, weight = 0.0;
   int limit = 0;
 };
-bool solver_fits(int nb, int nx);  // the step's LDS carve fits one workgroup
+// the step's LDS (the tree, the accumulator and the work arrays) fits one workgroup
+bool solver_fits(int nb, int nx, int S, int ni);
+// diagnostic builds (-DFSDF_SOLVER_TIMES=1): the last step's phase clocks (16, 100 MHz)
+void solver_times(unsigned long long* out);
 // FK of st.x -> poses, Rb, tb; flags = (error != 0, 0, error)
 hipError_t launch_solver_init(const SolverTree& T, const SolverState& st, hipStream_t s);
 // one NaiveSolver iteration from the pass's accumulator (skips once flags[0] is set)
 hipError_t launch_solver_step(const SolverTree& T, const SolverState& st, const double* d_accum, hipStream_t s);
+
+// Exchanged spatial shards (fsdf_set_points_keyed_device): the bounding box
+// (lo xyz, hi xyz; a device pointer into the scratch) of a device f64 cloud,
+// the 30-bit curve keys of a cloud in a given device box (the keys
+// sort_points_spatial orders by), and a resident cloud ordered by (key,
+// whole-cloud index) with perm = those indices (< 2^31) — the order a shard of
+// the whole cloud's sort_points_spatial order has. Asynchronous on `st`.
+hipError_t cloud_box(const double* d_src, int64_t n, SortScratch& s, hipStream_t st, double** d_box);
+hipError_t curve_keys(const double* d_src, int64_t n, const double* d_box, uint32_t* d_keys, hipStream_t st);
+hipError_t sort_points_keyed(const double* d_src, const uint32_t* d_keys, const int64_t* d_index, int64_t n,
+                             int precision, void* d_dst, int32_t* d_perm, SortScratch& s, hipStream_t st);
 
 // d_out[i] = d_perm[i] as int64 (fsdf_get_permutation's layout)
 hipError_t widen_permutation(const int32_t* d_perm, int64_t n, int64_t* d_out, hipStream_t st);

@@ -26,64 +26,174 @@
 #include "fsdf_internal.h"
 #include "kin_impl.h"
 
+#ifndef FSDF_SOLVER_TIMES
+#define FSDF_SOLVER_TIMES 0  // diagnostic builds: per-phase clocks of the step (capi.hip prints them)
+#endif
+
 namespace fsdf {
 
 namespace {
 
 constexpr int kSolverBlock = 256;
 
-// LDS carve of one step: sub [6 nb] | LR [9 nb] | Lt [3 nb] | R [9 nb] | t [3 nb]
-// | Rb [9 nb] | tb [3 nb] | x [nx] | g [nx]
-__device__ __forceinline__ void carve(double* lds, int nb, int nx, double** sub, double** LR, double** Lt, double** R,
-                                      double** t, double** Rb, double** tb, double** x, double** g) {
-  *sub = lds;
-  *LR = *sub + 6 * nb;
-  *Lt = *LR + 9 * nb;
-  *R = *Lt + 3 * nb;
-  *t = *R + 9 * nb;
-  *Rb = *t + 3 * nb;
-  *tb = *Rb + 9 * nb;
-  *x = *tb + 3 * nb;
-  *g = *x + nx;
+#if FSDF_SOLVER_TIMES
+__device__ unsigned long long g_solver_times[64];
+#define STAMP(i) \
+  if (threadIdx.x == 0 && it0 == 5) g_solver_times[i] = wall_clock64()
+#else
+#define STAMP(i)
+#endif
+
+// The step's LDS: the tree blob (doubles [nd], ints [ni], padded to 16 B) |
+// the accumulator [1+6S] | Rb [9nb] | tb [3nb] (the last FK's joint frames:
+// read by the chain rule, then overwritten by this step's FK) | x [nx] |
+// div [nx] | sub [6nb] | LR [9nb] | Lt [3nb] | R [9nb] | t [3nb] | g [nx].
+// Every array the level loops touch is here: a level costs LDS latency and a
+// barrier, not a global-memory round trip.
+struct Lds {
+  const double *axis, *AR, *At, *BR, *Bt, *FR, *Ft;
+  double *acc, *Rb, *tb, *sub, *LR, *Lt, *R, *t, *x, *g, *div;
+  const int32_t *parent, *kind, *qoff, *dord, *doff, *hord, *hoff, *coff, *clist, *soff, *slist, *sbody;
+};
+
+// the doubles after the blob: acc | Rb | tb | x | div | sub | LR | Lt | R | t | g
+__host__ __device__ inline size_t work_doubles(int nb, int nx, int S) {
+  return 1 + 6 * (size_t)S + 42 * (size_t)nb + 3 * (size_t)nx;
 }
 
-// FK of the LDS configuration x into LDS R, t, Rb, tb; then the surface poses
-// (global) and Rb, tb (global, for the next chain rule). Returns through
-// *bad: 1 a zero quaternion / unknown joint, 2 a non-finite pose.
-__device__ void fk_and_poses(const SolverTree& T, const SolverState& st, const double* x, double* LR, double* Lt,
-                             double* R, double* t, double* Rb, double* tb, int* bad) {
-  const int tid = threadIdx.x;
-  for (int b = 1 + tid; b < T.nb; b += kSolverBlock) {
-    const int k = T.kind[b];
-    if (!kin::joint_local(k, T.axis + 3 * b, T.AR + 9 * b, T.At + 3 * b, T.BR + 9 * b, T.Bt + 3 * b,
-                          k ? x + T.qoff[b] : x, LR + 9 * b, Lt + 3 * b))
+// The tree blob, the accumulator (optional), Rb / tb and x (+ divisors) into
+// LDS: every thread issues all of its loads before its first store, so the
+// staging costs one memory latency (the blob is ~23 KB for M64: 6 16-B chunks
+// per thread). A copy loop that stores each load before the next one waits a
+// full memory round trip (~1-2 us) per element per thread — measured 28 us per
+// step that way.
+constexpr int kBlobPer = 8;   // 16-B blob chunks per thread: blobs up to 32 KB
+constexpr int kDynPer = 8;    // dynamic doubles per thread (accum, Rb|tb, x, div): up to 2,048
+
+__device__ Lds stage(const SolverTree& T, const SolverState& st, double* lds, const double* accum) {
+  const int tid = threadIdx.x, nb = T.nb, nx = T.nx, S = T.S;
+  typedef double D2 __attribute__((ext_vector_type(2)));
+  // loads: blob chunks, then the dynamic doubles (a flat index over accum | Rb tb | x | div)
+  const D2* blob = (const D2*)T.blob;
+  D2 bv[kBlobPer];
+#pragma unroll
+  for (int u = 0; u < kBlobPer; ++u) {
+    const int i = tid + u * kSolverBlock;
+    bv[u] = i < T.chunks16 ? blob[i] : D2{0.0, 0.0};
+  }
+  const int na = accum ? 1 + 6 * S : 0, nr = accum ? 12 * nb : 0, nd_ = st.div ? nx : 0;
+  const int ndyn = na + nr + nx + nd_;
+  double dv[kDynPer];
+#pragma unroll
+  for (int u = 0; u < kDynPer; ++u) {
+    const int i = tid + u * kSolverBlock;
+    double v = 0.0;
+    if (i < na) v = accum[i];
+    else if (i < na + nr) v = st.Rb[i - na];  // (Rb | tb adjacent in the state buffer)
+    else if (i < na + nr + nx) v = st.x[i - na - nr];
+    else if (i < ndyn) v = st.div[i - na - nr - nx];
+    dv[u] = v;
+  }
+  Lds L;
+  double* d = lds;
+  D2* l2 = (D2*)lds;
+#pragma unroll
+  for (int u = 0; u < kBlobPer; ++u) {
+    const int i = tid + u * kSolverBlock;
+    if (i < T.chunks16) l2[i] = bv[u];
+  }
+  L.axis = d + T.axis;
+  L.AR = d + T.AR;
+  L.At = d + T.At;
+  L.BR = d + T.BR;
+  L.Bt = d + T.Bt;
+  L.FR = d + T.frame_R;
+  L.Ft = d + T.frame_t;
+  const int32_t* iv = (const int32_t*)(d + T.nd);
+  L.parent = iv + T.parent;
+  L.kind = iv + T.kind;
+  L.qoff = iv + T.qoff;
+  L.dord = iv + T.depth_order;
+  L.doff = iv + T.depth_off;
+  L.hord = iv + T.height_order;
+  L.hoff = iv + T.height_off;
+  L.coff = iv + T.child_off;
+  L.clist = iv + T.child_list;
+  L.soff = iv + T.surf_off;
+  L.slist = iv + T.surf_list;
+  L.sbody = iv + T.surface_body;
+  d += 2 * T.chunks16;  // (the blob, padded to 16 B)
+  L.acc = d;
+  d += 1 + 6 * S;
+  L.Rb = d;
+  d += 9 * nb;
+  L.tb = d;
+  d += 3 * nb;
+  L.x = d;
+  d += nx;
+  L.div = st.div ? d : nullptr;
+  d += nx;
+  L.sub = d;
+  d += 6 * nb;
+  L.LR = d;
+  d += 9 * nb;
+  L.Lt = d;
+  d += 3 * nb;
+  L.R = d;
+  d += 9 * nb;
+  L.t = d;
+  d += 3 * nb;
+  L.g = d;
+  // the dynamic doubles land at acc (accum | Rb tb | x | div are contiguous
+  // there too; without an accumulator x lands at L.x)
+#pragma unroll
+  for (int u = 0; u < kDynPer; ++u) {
+    const int i = tid + u * kSolverBlock;
+    if (i < na + nr) L.acc[i] = dv[u];
+    else if (i < ndyn) L.x[i - na - nr] = dv[u];
+  }
+  for (int i = tid; i < nx; i += kSolverBlock) L.g[i] = 0.0;
+  return L;
+}
+
+// FK of L.x into L.R, t, Rb, tb; then the surface poses (global) and Rb, tb
+// (global, for the next chain rule). *bad: 1 a zero quaternion / unknown
+// joint, 2 a non-finite pose.
+__device__ void fk_and_poses(const SolverTree& T, const SolverState& st, const Lds& L, int* bad, int it0 = -1) {
+  const int tid = threadIdx.x, nb = T.nb;
+  for (int b = 1 + tid; b < nb; b += kSolverBlock) {
+    const int k = L.kind[b];
+    if (!kin::joint_local(k, L.axis + 3 * b, L.AR + 9 * b, L.At + 3 * b, L.BR + 9 * b, L.Bt + 3 * b,
+                          k ? L.x + L.qoff[b] : L.x, L.LR + 9 * b, L.Lt + 3 * b))
       atomicOr(bad, 1);
   }
+  STAMP(5);
   if (tid < 9) {
     const double v = (tid % 4 == 0) ? 1.0 : 0.0;
-    R[tid] = v;
-    Rb[tid] = v;
+    L.R[tid] = v;
+    L.Rb[tid] = v;
   } else if (tid < 12) {
-    t[tid - 9] = 0.0;
-    tb[tid - 9] = 0.0;
+    L.t[tid - 9] = 0.0;
+    L.tb[tid - 9] = 0.0;
   }
   __syncthreads();
   for (int d = 0; d < T.D; ++d) {
-    const int a = T.depth_off[d], e = T.depth_off[d + 1];
+    const int a = L.doff[d], e = L.doff[d + 1];
     for (int i = a + tid; i < e; i += kSolverBlock) {
-      const int b = T.depth_order[i], p = T.parent[b];
-      kin::compose(R + 9 * p, t + 3 * p, LR + 9 * b, Lt + 3 * b, T.AR + 9 * b, T.At + 3 * b, R + 9 * b, t + 3 * b,
-                   Rb + 9 * b, tb + 3 * b);
+      const int b = L.dord[i], p = L.parent[b];
+      kin::compose(L.R + 9 * p, L.t + 3 * p, L.LR + 9 * b, L.Lt + 3 * b, L.AR + 9 * b, L.At + 3 * b, L.R + 9 * b,
+                   L.t + 3 * b, L.Rb + 9 * b, L.tb + 3 * b);
     }
     __syncthreads();
   }
+  STAMP(6);
   for (int k = tid; k < T.S; k += kSolverBlock) {
     double P[12];
-    const int b = T.surface_body[k];
+    const int b = L.sbody[k];
     if (b < 0) {
       for (int i = 0; i < 12; ++i) P[i] = (i % 4 == 0 && i < 9) ? 1.0 : 0.0;
     } else {
-      kin::surface_pose(R + 9 * b, t + 3 * b, T.frame_R + 9 * k, T.frame_t + 3 * k, P);
+      kin::surface_pose(L.R + 9 * b, L.t + 3 * b, L.FR + 9 * k, L.Ft + 3 * k, P);
     }
     bool fin = true;
     for (int i = 0; i < 12; ++i) {
@@ -92,20 +202,20 @@ __device__ void fk_and_poses(const SolverTree& T, const SolverState& st, const d
     }
     if (!fin) atomicOr(bad, 2);
   }
-  for (int i = tid; i < 9 * T.nb; i += kSolverBlock) st.Rb[i] = Rb[i];
-  for (int i = tid; i < 3 * T.nb; i += kSolverBlock) st.tb[i] = tb[i];
+  STAMP(7);
+  for (int i = tid; i < 9 * nb; i += kSolverBlock) st.Rb[i] = L.Rb[i];
+  for (int i = tid; i < 3 * nb; i += kSolverBlock) st.tb[i] = L.tb[i];
+  STAMP(8);
 }
 
 __global__ __launch_bounds__(kSolverBlock) void solver_init_kernel(SolverTree T, SolverState st) {
   extern __shared__ double lds[];
   __shared__ int bad;
-  double *sub, *LR, *Lt, *R, *t, *Rb, *tb, *x, *g;
-  carve(lds, T.nb, T.nx, &sub, &LR, &Lt, &R, &t, &Rb, &tb, &x, &g);
   const int tid = threadIdx.x;
   if (tid == 0) bad = 0;
-  for (int i = tid; i < T.nx; i += kSolverBlock) x[i] = st.x[i];
+  const Lds L = stage(T, st, lds, nullptr);
   __syncthreads();
-  fk_and_poses(T, st, x, LR, Lt, R, t, Rb, tb, &bad);
+  fk_and_poses(T, st, L, &bad);
   __syncthreads();
   if (tid == 0) {
     st.flags[1] = 0;
@@ -120,50 +230,54 @@ __global__ __launch_bounds__(kSolverBlock) void solver_step_kernel(SolverTree T,
   if (st.flags[0]) return;  // converged (or failed): the frame's remaining steps are no-ops
   extern __shared__ double lds[];
   __shared__ int bad, verdict;
-  double *sub, *LR, *Lt, *R, *t, *Rb, *tb, *x, *g;
-  carve(lds, T.nb, T.nx, &sub, &LR, &Lt, &R, &t, &Rb, &tb, &x, &g);
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, nb = T.nb, nx = T.nx;
+#if FSDF_SOLVER_TIMES
+  const int it0 = st.flags[1];
+#endif
+  STAMP(0);
   if (tid == 0) bad = 0;
-  for (int i = tid; i < T.nx; i += kSolverBlock) {
-    x[i] = st.x[i];
-    g[i] = 0.0;
-  }
+  const Lds L = stage(T, st, lds, accum);
+  __syncthreads();
+  STAMP(1);
   // body wrenches: each body's surfaces in index order (fsdf_config_gradient)
-  for (int i = tid; i < 6 * T.nb; i += kSolverBlock) {
+  for (int i = tid; i < 6 * nb; i += kSolverBlock) {
     const int b = i / 6, j = i - 6 * b;
     double s = 0.0;
-    for (int q = T.surf_off[b]; q < T.surf_off[b + 1]; ++q) s += accum[1 + 6 * T.surf_list[q] + j];
-    sub[i] = s;
+    for (int q = L.soff[b]; q < L.soff[b + 1]; ++q) s += L.acc[1 + 6 * L.slist[q] + j];
+    L.sub[i] = s;
   }
   __syncthreads();
   // subtree sums: parents by height, each adding its children in descending index
   for (int h = 0; h < T.H; ++h) {
-    const int a = T.height_off[h], e = T.height_off[h + 1];
+    const int a = L.hoff[h], e = L.hoff[h + 1];
     for (int i = tid; i < 6 * (e - a); i += kSolverBlock) {
-      const int p = T.height_order[a + i / 6], j = i % 6;
-      double s = sub[6 * p + j];
-      for (int q = T.child_off[p]; q < T.child_off[p + 1]; ++q) s += sub[6 * T.child_list[q] + j];
-      sub[6 * p + j] = s;
+      const int p = L.hord[a + i / 6], j = i % 6;
+      double s = L.sub[6 * p + j];
+      for (int q = L.coff[p]; q < L.coff[p + 1]; ++q) s += L.sub[6 * L.clist[q] + j];
+      L.sub[6 * p + j] = s;
     }
     __syncthreads();
   }
-  for (int b = 1 + tid; b < T.nb; b += kSolverBlock) {
-    const int k = T.kind[b];
-    if (k && !kin::joint_gradient(k, T.axis + 3 * b, st.Rb + 9 * b, st.tb + 3 * b, x + T.qoff[b], sub + 6 * b,
-                                  g + T.qoff[b]))
+  STAMP(2);
+  for (int b = 1 + tid; b < nb; b += kSolverBlock) {
+    const int k = L.kind[b];
+    if (k && !kin::joint_gradient(k, L.axis + 3 * b, L.Rb + 9 * b, L.tb + 3 * b, L.x + L.qoff[b], L.sub + 6 * b,
+                                  L.g + L.qoff[b]))
       atomicOr(&bad, 1);
   }
   __syncthreads();
-  for (int i = tid; i < T.nx; i += kSolverBlock) {
-    double gi = g[i] / st.n_points;
-    if (st.div) gi = gi / st.div[i];
-    g[i] = gi;
+  for (int i = tid; i < nx; i += kSolverBlock) {
+    double gi = L.g[i] / st.n_points;
+    if (L.div) gi = gi / L.div[i];
+    L.g[i] = gi;
   }
   __syncthreads();
+  STAMP(3);
   if (tid == 0) {
     double nrm2 = 0.0;  // in index order, as the host sums it
-    for (int i = 0; i < T.nx; ++i) nrm2 += g[i] * g[i];
-    const double cost = accum[0] + st.weight * 0.0;  // (rigid: the regularizer's sum is 0.0)
+#pragma unroll 8
+    for (int i = 0; i < nx; ++i) nrm2 += L.g[i] * L.g[i];
+    const double cost = L.acc[0] + st.weight * 0.0;  // (rigid: the regularizer's sum is 0.0)
     const int it = st.flags[1] + 1;
     st.flags[1] = it;
     *st.f = cost / st.n_points;
@@ -178,9 +292,9 @@ __global__ __launch_bounds__(kSolverBlock) void solver_step_kernel(SolverTree T,
     }
     return;
   }
-  for (int i = tid; i < T.nx; i += kSolverBlock) {
-    const double xi = x[i] + kin::clipped_step(st.rate, g[i], st.max_step);
-    x[i] = xi;
+  for (int i = tid; i < nx; i += kSolverBlock) {
+    const double xi = L.x[i] + kin::clipped_step(st.rate, L.g[i], st.max_step);
+    L.x[i] = xi;
     st.x[i] = xi;
   }
   if (v == 2) {  // the last iteration: no pass follows
@@ -188,23 +302,46 @@ __global__ __launch_bounds__(kSolverBlock) void solver_step_kernel(SolverTree T,
     return;
   }
   __syncthreads();
-  fk_and_poses(T, st, x, LR, Lt, R, t, Rb, tb, &bad);
+  STAMP(4);
+#if FSDF_SOLVER_TIMES
+  fk_and_poses(T, st, L, &bad, it0);
+#else
+  fk_and_poses(T, st, L, &bad);
+#endif
   __syncthreads();
+  STAMP(9);
   if (tid == 0 && bad) {
     st.flags[2] = bad;
     st.flags[0] = 1;
   }
 }
 
-size_t solver_lds_bytes(const SolverTree& T) { return (size_t)(42 * T.nb + 2 * T.nx) * sizeof(double); }
+size_t solver_lds_bytes(const SolverTree& T) {
+  return (size_t)T.chunks16 * 16 + work_doubles(T.nb, T.nx, T.S) * sizeof(double);
+}
 
 }  // namespace
 
-bool solver_fits(int nb, int nx) { return nb >= 1 && (size_t)(42 * nb + 2 * nx) * sizeof(double) <= 65536; }
+// the blob (27 nb + 12 S doubles + ni ints) within kBlobPer chunks per thread,
+// the dynamic loads within kDynPer, the whole carve within 64 KB of LDS
+bool solver_fits(int nb, int nx, int S, int ni) {
+  const size_t blob = ((27 * (size_t)nb + 12 * (size_t)S) * 8 + (size_t)ni * 4 + 15) / 16;
+  const size_t dyn = 1 + 6 * (size_t)S + 12 * (size_t)nb + 2 * (size_t)nx;
+  return nb >= 1 && blob <= (size_t)kBlobPer * kSolverBlock && dyn <= (size_t)kDynPer * kSolverBlock &&
+         blob * 16 + work_doubles(nb, nx, S) * 8 <= 65536;
+}
 
 hipError_t launch_solver_init(const SolverTree& T, const SolverState& st, hipStream_t s) {
   hipLaunchKernelGGL(solver_init_kernel, dim3(1), dim3(kSolverBlock), solver_lds_bytes(T), s, T, st);
   return hipGetLastError();
+}
+
+void solver_times(unsigned long long* out) {
+#if FSDF_SOLVER_TIMES
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_solver_times), 16 * sizeof(unsigned long long));
+#else
+  for (int i = 0; i < 16; ++i) out[i] = 0;
+#endif
 }
 
 hipError_t launch_solver_step(const SolverTree& T, const SolverState& st, const double* d_accum, hipStream_t s) {

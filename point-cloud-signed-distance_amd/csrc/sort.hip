@@ -137,7 +137,32 @@ __global__ __launch_bounds__(kBlock) void curve_key_kernel(const double* __restr
 #else
   keys[i] = spread10(q[0]) | (spread10(q[1]) << 1) | (spread10(q[2]) << 2);
 #endif
-  idx[i] = (int32_t)i;
+  if (idx) idx[i] = (int32_t)i;
+}
+
+// composite (30-bit curve key, int31 whole-cloud index) keys and positions for
+// the keyed resident order (sort_points_keyed)
+__global__ __launch_bounds__(kBlock) void composite_key_kernel(const uint32_t* __restrict__ keys,
+                                                            const int64_t* __restrict__ index, int64_t n,
+                                                            uint64_t* __restrict__ out, int32_t* __restrict__ pos) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  out[i] = ((uint64_t)(keys[i] & 0x3fffffffu) << 31) | (uint64_t)(index[i] & 0x7fffffff);
+  pos[i] = (int32_t)i;
+}
+
+// resident i <- source pos[i]: the point (context precision) and its whole-cloud index
+template <typename T>
+__global__ __launch_bounds__(kBlock) void gather_keyed_kernel(const double* __restrict__ src,
+                                                           const int64_t* __restrict__ index, int64_t n,
+                                                           const int32_t* __restrict__ pos, T* __restrict__ dst,
+                                                           int32_t* __restrict__ perm) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int64_t o = pos[i];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) dst[3 * i + j] = (T)src[3 * o + j];
+  perm[i] = (int32_t)index[o];
 }
 
 template <typename T>
@@ -326,6 +351,8 @@ void free_sort_scratch(SortScratch& s) {
   if (s.i1) (void)hipFree(s.i1);
   if (s.tmp) (void)hipFree(s.tmp);
   if (s.pts) (void)hipFree(s.pts);
+  if (s.q0) (void)hipFree(s.q0);
+  if (s.q1) (void)hipFree(s.q1);
   s = SortScratch();
 }
 
@@ -361,6 +388,53 @@ hipError_t sort_points_spatial(const double* d_src, int64_t n, int precision, vo
     hipLaunchKernelGGL(gather_kernel<double>, dim3(grid), dim3(kBlock), 0, st, d_src, n, d_perm, (double*)d_dst);
   else
     hipLaunchKernelGGL(gather_kernel<float>, dim3(grid), dim3(kBlock), 0, st, d_src, n, d_perm, (float*)d_dst);
+  return hipGetLastError();
+}
+
+hipError_t cloud_box(const double* d_src, int64_t n, SortScratch& s, hipStream_t st, double** d_box) {
+  hipError_t e;
+  if ((e = grow(&s.part, &s.part_cap, (size_t)(kBoxBlocks + 1) * 6 * sizeof(double))) != hipSuccess) return e;
+  double* box = s.part + 6 * kBoxBlocks;
+  *d_box = box;
+  if (n <= 0) return hipSuccess;  // (the slot only: curve_keys_device fills it from the host)
+  const int nb = (int)std::min<int64_t>(kBoxBlocks, (n + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(bbox_partial_kernel, dim3(nb), dim3(kBlock), 0, st, d_src, n, s.part);
+  hipLaunchKernelGGL(bbox_final_kernel, dim3(1), dim3(kBlock), 0, st, s.part, nb, box);
+  return hipGetLastError();
+}
+
+hipError_t curve_keys(const double* d_src, int64_t n, const double* d_box, uint32_t* d_keys, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(curve_key_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, d_src, n,
+                     d_box, d_keys, (int32_t*)nullptr);
+  return hipGetLastError();
+}
+
+hipError_t sort_points_keyed(const double* d_src, const uint32_t* d_keys, const int64_t* d_index, int64_t n,
+                             int precision, void* d_dst, int32_t* d_perm, SortScratch& s, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (n > INT32_MAX) return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
+  hipError_t e;
+  if ((e = grow(&s.q0, &s.q_cap0, (size_t)n * sizeof(uint64_t))) != hipSuccess) return e;
+  if ((e = grow(&s.q1, &s.q_cap1, (size_t)n * sizeof(uint64_t))) != hipSuccess) return e;
+  if ((e = grow(&s.i1, &s.i_cap1, (size_t)n * sizeof(int32_t))) != hipSuccess) return e;
+  if ((e = grow(&s.k0, &s.k_cap0, (size_t)n * sizeof(int32_t))) != hipSuccess) return e;
+  int32_t* pos0 = (int32_t*)s.k0;
+  hipLaunchKernelGGL(composite_key_kernel, dim3(grid), dim3(kBlock), 0, st, d_keys, d_index, n, s.q0, pos0);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  rocprim::double_buffer<uint64_t> keys(s.q0, s.q1);
+  rocprim::double_buffer<int32_t> vals(pos0, s.i1);
+  size_t need = 0;
+  if ((e = rocprim::radix_sort_pairs(nullptr, need, keys, vals, (size_t)n, 0, 61, st)) != hipSuccess) return e;
+  if ((e = grow((char**)&s.tmp, &s.tmp_cap, need)) != hipSuccess) return e;
+  if ((e = rocprim::radix_sort_pairs(s.tmp, need, keys, vals, (size_t)n, 0, 61, st)) != hipSuccess) return e;
+  if (precision == 64)
+    hipLaunchKernelGGL(gather_keyed_kernel<double>, dim3(grid), dim3(kBlock), 0, st, d_src, d_index, n, vals.current(),
+                       (double*)d_dst, d_perm);
+  else
+    hipLaunchKernelGGL(gather_keyed_kernel<float>, dim3(grid), dim3(kBlock), 0, st, d_src, d_index, n, vals.current(),
+                       (float*)d_dst, d_perm);
   return hipGetLastError();
 }
 

@@ -66,6 +66,9 @@ _PROTOS = {
     "fsdf_set_points_range": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_int64]),
     "fsdf_set_points_range_device": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_int64]),
     "fsdf_regroup_points": (c_int32, [c_void_p]),
+    "fsdf_cloud_box_device": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "fsdf_curve_keys_device": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "fsdf_set_points_keyed_device": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64]),
     "fsdf_regroup_auto": (c_int32, [c_void_p, POINTER(c_int32)]),
     "fsdf_set_regroup": (c_int32, [c_void_p, c_int32]),
     "fsdf_set_solver": (c_int32, [c_void_p, c_int32]),
@@ -252,6 +255,27 @@ class Context:
         check(self._lib.fsdf_set_points_range(self._ctx, ptr(pts), pts.shape[0], int(begin), int(end)), self._ctx,
               "set_points_range")
         self.n = int(end) - int(begin)
+
+    def cloud_box_device(self, d_xyz: int, n: int) -> np.ndarray:
+        """fsdf_cloud_box_device: (lo xyz, hi xyz) of a device f64 AoS cloud."""
+        box = np.empty(6, np.float64)
+        check(self._lib.fsdf_cloud_box_device(self._ctx, c_void_p(d_xyz), int(n), ptr(box)), self._ctx,
+              "cloud_box_device")
+        return box
+
+    def curve_keys_device(self, d_xyz: int, n: int, box, d_keys: int):
+        """fsdf_curve_keys_device: 30-bit Hilbert keys (uint32, device) of the
+        points in `box` (6 doubles)."""
+        b = np.ascontiguousarray(box, np.float64).reshape(6)
+        check(self._lib.fsdf_curve_keys_device(self._ctx, c_void_p(d_xyz), int(n), ptr(b), c_void_p(d_keys)),
+              self._ctx, "curve_keys_device")
+
+    def set_points_keyed_device(self, d_xyz: int, d_keys: int, d_index: int, n: int):
+        """fsdf_set_points_keyed_device: the exchanged shard becomes resident in
+        (key, whole-cloud index) order; permutation = the whole-cloud indices."""
+        check(self._lib.fsdf_set_points_keyed_device(self._ctx, c_void_p(d_xyz), c_void_p(d_keys), c_void_p(d_index),
+                                                     int(n)), self._ctx, "set_points_keyed_device")
+        self.n = int(n)
 
     def regroup_auto(self) -> bool:
         """fsdf_regroup_auto: regroup only where the library's rule says it pays

@@ -115,6 +115,86 @@ def gather_chunk_costs(local_costs, group=None, device=None) -> np.ndarray:
     return np.concatenate([b[:int(c.item())].cpu().numpy() for b, c in zip(bufs, cnts)])
 
 
+KEY_BITS = 30  # the device's curve keys (sort.hip: 10 bits per axis)
+
+
+def exchange_points(ctxs, local_pts, local_index, group=None, bins_log2: int = 16):
+    """O(N/W) ingest of one frame's cloud into spatial shards. Every rank holds
+    a 1/W slice of the sensed cloud (`local_pts` [m,3] f64 tensor on the rank's
+    device, `local_index` [m] int64: each point's index in the whole cloud):
+      1. the whole cloud's bounding box: each slice's box (fsdf_cloud_box_device)
+         and one 6-double all-reduce (MAX of (-lo, hi));
+      2. each point's 30-bit Hilbert key in that box (fsdf_curve_keys_device —
+         the keys a single context's sort_points orders by);
+      3. splitters: a 2^bins_log2-bin histogram of the keys' top bits,
+         all-reduced; rank r owns the bins where the cumulative count crosses
+         r/W of the points — W contiguous key ranges of about N/W points;
+      4. one all-to-all moves every point (xyz, key, whole-cloud index) to the
+         rank owning its key;
+      5. each context makes the received points resident in (key, whole-cloud
+         index) order (fsdf_set_points_keyed_device): the single-context sorted
+         order restricted to the rank's key range, the whole-cloud indices as
+         the permutation.
+    No rank ever holds more than its slice plus its shard: per-rank H2D and
+    device sort are O(N/W) (the whole-cloud ranges of fsdf_set_points_range
+    upload and sort all N points on every rank). A gloo group exchanges host
+    copies (the CPU tests); RCCL exchanges device tensors over xGMI. Returns
+    (this rank's resident count, the whole cloud's point count)."""
+    import torch
+    import torch.distributed as dist
+    grouped = dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size(group) if grouped else 1
+    cdev = local_pts.device if (not grouped or dist.get_backend(group) == "nccl") else torch.device("cpu")
+    ctx = ctxs[0]
+    m = int(local_pts.shape[0])
+    local_pts = local_pts.contiguous()
+    box = ctx.cloud_box_device(local_pts.data_ptr(), m)
+    t = torch.tensor(np.concatenate([-box[:3], box[3:]]), dtype=torch.float64, device=cdev)
+    n_all = torch.tensor([m], dtype=torch.int64, device=cdev)
+    if grouped:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        dist.all_reduce(n_all, op=dist.ReduceOp.SUM, group=group)
+    t = t.cpu().numpy()
+    gbox = np.concatenate([-t[:3], t[3:]])
+    keys = torch.empty(max(m, 1), dtype=torch.int32, device=local_pts.device)
+    ctx.curve_keys_device(local_pts.data_ptr(), m, gbox, keys.data_ptr())
+    keys = keys[:m]
+    if world == 1:
+        recv_pts, recv_keys, recv_idx = local_pts, keys, local_index.to(torch.int64).contiguous()
+    else:
+        bins = (keys >> (KEY_BITS - bins_log2)).to(torch.int64).to(cdev)
+        hist = torch.bincount(bins, minlength=1 << bins_log2)
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+        cum = torch.cumsum(hist, 0)
+        total = int(cum[-1].item())
+        targets = torch.tensor([total * r // world for r in range(1, world)], dtype=torch.int64, device=cdev)
+        cuts = torch.searchsorted(cum, targets, right=True)  # first bin of ranks 1 .. W-1
+        dest = torch.bucketize(bins, cuts, right=True)
+        order = torch.argsort(dest, stable=True)
+        send = torch.bincount(dest, minlength=world)
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=group)
+        sc, rc = send.tolist(), recv.tolist()
+        nr = sum(rc)
+        src_pts = local_pts.to(cdev)[order].contiguous()
+        src_keys = keys.to(cdev)[order].contiguous()
+        src_idx = local_index.to(cdev).to(torch.int64)[order].contiguous()
+        recv_pts = torch.empty((nr, 3), dtype=torch.float64, device=cdev)
+        recv_keys = torch.empty(nr, dtype=torch.int32, device=cdev)
+        recv_idx = torch.empty(nr, dtype=torch.int64, device=cdev)
+        dist.all_to_all_single(recv_pts.view(-1), src_pts.view(-1), [3 * c for c in rc], [3 * c for c in sc],
+                               group=group)
+        dist.all_to_all_single(recv_keys, src_keys, rc, sc, group=group)
+        dist.all_to_all_single(recv_idx, src_idx, rc, sc, group=group)
+        if cdev != local_pts.device:
+            recv_pts, recv_keys, recv_idx = (recv_pts.to(local_pts.device), recv_keys.to(local_pts.device),
+                                             recv_idx.to(local_pts.device))
+    n_res = int(recv_pts.shape[0])
+    for c in ctxs:
+        c.set_points_keyed_device(recv_pts.data_ptr(), recv_keys.data_ptr(), recv_idx.data_ptr(), n_res)
+    return n_res, int(n_all.item())
+
+
 def allreduce_accum(accum, group=None, async_op=False):
     """Sum the per-rank accumulators in place (torch tensor, any device).
     async_op=True returns the collective's work handle (None without a process
@@ -139,7 +219,8 @@ class ShardedCostFunctor:
 
     def __init__(self, manipulator: Manipulator, local_points, rank: int = 0, world: int = 1, device: int = 0,
                  precision: int = 64, group=None, deformation_cost_weight=default_deformation_cost_weight,
-                 engine=None, inflight: int = 1, spatial: bool = False, bounds=None):
+                 engine=None, inflight: int = 1, spatial: bool = False, bounds=None, exchange: bool = False,
+                 index_offset: int | None = None):
         """engine: an already-built context-like object to drive instead of
         manipulator.engine(device, precision) — with engine.device_type == "cpu"
         the accumulator lives in host memory and no HIP stream is used (the CPU
@@ -154,7 +235,13 @@ class ShardedCostFunctor:
         spatial_bounds(n, world): equal chunk counts) of its spatial order
         (fsdf_set_points_range); rebalance() moves the boundaries to equal
         measured cost. Per-point outputs are then in the shard's resident
-        order, global_index() names their indices in the whole cloud."""
+        order, global_index() names their indices in the whole cloud.
+        exchange = True: O(N/W) ingest — `local_points` is only this rank's
+        slice of the cloud (any split; index_offset = the whole-cloud index of
+        its first point, default: the slices concatenated in rank order) and
+        exchange_points() moves every point to the rank whose key range holds it
+        (per-point outputs and global_index() as for spatial shards;
+        set_sensed_points() swaps a new frame's slice in the same way)."""
         import contextlib
         import torch
         self.torch = torch
@@ -167,8 +254,11 @@ class ShardedCostFunctor:
         self.dev = torch.device("cpu") if on_host else torch.device("cuda", device)
         pts = torch.as_tensor(np.ascontiguousarray(local_points, np.float64).reshape(-1, 3), device=self.dev)
         self._pts = pts  # the context reads the resident copy (set_points_device does not own it)
-        self.rank, self.world, self.spatial = rank, world, spatial
-        if spatial:
+        self.rank, self.world, self.spatial, self.exchange = rank, world, spatial and not exchange, exchange
+        self._index_offset = index_offset
+        if exchange:
+            self._exchange(pts)
+        elif spatial:
             self.cloud_n = pts.shape[0]
             self.bounds = list(bounds) if bounds is not None else spatial_bounds(self.cloud_n, world)
             self.range = self.bounds[rank]
@@ -206,18 +296,61 @@ class ShardedCostFunctor:
                 c2 = manipulator.engine(device, precision, slot=1)
                 s2 = torch.cuda.Stream(self.dev)
                 c2.set_stream(s2.cuda_stream)
-                if spatial:
+                self.ctxs.append(c2)
+                if exchange:
+                    self._exchange(pts)
+                elif spatial:
                     self._plan_window(c2)
                     c2.set_points_range_device(pts.data_ptr(), pts.shape[0], *self.range)
                 else:
                     c2.set_points_device(pts.data_ptr(), pts.shape[0])
-                self.ctxs.append(c2)
                 self.streams.append(s2)
             self._on_stream = lambda slot=0: torch.cuda.stream(self.streams[slot % len(self.streams)])
             self._sync = lambda slot=0: self.streams[slot % len(self.streams)].synchronize()
         # native iterations (fsdf_eval_state_device + fsdf_state_gradient: FK,
         # RBF solve, poses, pass; chain rule after the all-reduce)
         self._native = native_capable(manipulator) and getattr(self.ctx, "native_iterations", True)
+
+    def _exchange(self, pts):
+        """exchange_points() of this rank's slice `pts` into every context."""
+        torch = self.torch
+        m = int(pts.shape[0])
+        off = self._index_offset
+        if off is None:  # the slices in rank order: this rank's offset = the earlier ranks' sizes
+            import torch.distributed as dist
+            sizes = [m]
+            if dist.is_available() and dist.is_initialized() and self.world > 1:
+                cdev = self.dev if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+                t = torch.tensor([m], dtype=torch.int64, device=cdev)
+                ts = [torch.zeros_like(t) for _ in range(self.world)]
+                dist.all_gather(ts, t, group=self.group)
+                sizes = [int(x.item()) for x in ts]
+            off = sum(sizes[:self.rank])
+        idx = torch.arange(off, off + m, dtype=torch.int64, device=self.dev)
+        ctxs = getattr(self, "ctxs", [self.ctx])
+        self.n_resident, self.cloud_n = exchange_points(ctxs, pts, idx, self.group)
+        for c in ctxs:  # (the planned pass over shards of about cloud_n / world points)
+            self._plan_window(c)
+
+    def set_sensed_points(self, local_points):
+        """A new frame's cloud (exchange shards: this rank's slice of it; spatial
+        shards: the whole cloud, the ranges kept): the shards are rebuilt, the
+        functor and the device model kept."""
+        torch = self.torch
+        for slot in (0, 1):
+            self._wait_slot(slot)
+        self._sync(0)
+        pts = torch.as_tensor(np.ascontiguousarray(local_points, np.float64).reshape(-1, 3), device=self.dev)
+        self._pts = pts
+        if self.exchange:
+            self._exchange(pts)
+        elif self.spatial:
+            self.cloud_n = pts.shape[0]
+            for c in self.ctxs:
+                c.set_points_range_device(pts.data_ptr(), pts.shape[0], *self.range)
+        else:
+            for c in self.ctxs:
+                c.set_points_device(pts.data_ptr(), pts.shape[0])
 
     def _ensure_native(self, ctx=None):
         ctx = self.ctx if ctx is None else ctx
@@ -291,8 +424,9 @@ class ShardedCostFunctor:
             ctx.set_plan(True, -1.0, -1.0, plan_window(self.cloud_n, self.world))
 
     def global_index(self) -> np.ndarray:
-        """The whole cloud's index of each resident point (spatial shards; for
-        a plain shard its own caller order is resident, indices 0..n-1 of it)."""
+        """The whole cloud's index of each resident point (spatial and exchange
+        shards; for a plain shard its own caller order is resident, indices
+        0..n-1 of it)."""
         return self.ctx.permutation()
 
     def rebalance(self):

@@ -128,6 +128,37 @@ class OracleEngine:
     def permutation(self):
         return self.perm.copy()
 
+    # exchange shards (flash.distributed.exchange_points): box, keys, keyed resident order
+    def cloud_box_device(self, ptr, n):
+        pts = self._view(ptr, 3 * n, np.float64).reshape(n, 3)
+        if n == 0:
+            return np.array([np.inf] * 3 + [-np.inf] * 3)
+        return np.concatenate([pts.min(0), pts.max(0)])
+
+    def curve_keys_device(self, ptr, n, box, keys_ptr):
+        """30-bit Morton keys in `box` (a stand-in for the device's Hilbert keys)."""
+        pts = self._view(ptr, 3 * n, np.float64).reshape(n, 3)
+        box = np.asarray(box)
+        ext = box[3:] - box[:3]
+        u = np.where(ext > 0, (pts - box[:3]) / np.where(ext > 0, ext, 1.0), 0.0)
+        q = np.clip(np.floor(u * 1024.0), 0, 1023).astype(np.int64)
+        key = np.zeros(n, np.int64)
+        for b in range(10):
+            for a in range(3):
+                key |= ((q[:, a] >> b) & 1) << (3 * b + 2 - a)
+        self._view(keys_ptr, n, np.int32)[:] = key
+
+    def set_points_keyed_device(self, ptr, keys_ptr, idx_ptr, n):
+        pts = self._view(ptr, 3 * n, np.float64).reshape(n, 3)
+        keys = self._view(keys_ptr, n, np.int32).astype(np.int64)
+        idx = self._view(idx_ptr, n, np.int64)
+        order = np.lexsort((idx, keys))
+        self.pts, self.perm, self.n = pts[order].copy(), idx[order].copy(), n
+        self.keys = keys[order].copy()
+
+    def set_plan(self, *a):
+        pass
+
     def chunk_costs(self):
         """Deterministic per-chunk stand-in durations, uneven on purpose: chunks
         of the lower half of the cloud's order cost 1, of the upper half 9."""
@@ -338,3 +369,66 @@ def test_gloo_world2_spatial_shards(name):
             assert np.allclose(g, g1, rtol=1e-9, atol=1e-10 * max(1.0, np.abs(g1).max()))
             k[idx], d[idx] = kk, dd
         assert np.array_equal(k, k1) and np.array_equal(d, d1)
+
+
+def _exchange_worker(rank, world, port, q, name):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from flash.distributed import ShardedCostFunctor, shard_range
+        m, pts, x = _scene(name)
+        # uneven slices of the caller's order: each rank uploads only its own
+        cuts = [0, len(pts) // 5, (3 * len(pts)) // 4, len(pts)][:world] + [len(pts)]
+        a, b = (cuts[rank], cuts[rank + 1]) if world == 3 else shard_range(len(pts), rank, world)
+        eng = OracleEngine(m)
+        f = ShardedCostFunctor(m, pts[a:b], rank, world, engine=eng, exchange=True)
+        c, g = f.value_and_gradient(x)
+        k, d, _ = f.per_point(x)
+        q.put((rank, f.cloud_n, b - a, c, g, f.global_index(), k, d, int(eng.keys.min(initial=2**31)),
+               int(eng.keys.max(initial=-1))))
+        # a new frame (the same slice again): the same shards, the same bits
+        f.set_sensed_points(pts[a:b])
+        c2, _ = f.value_and_gradient(x)
+        assert c2 == c
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_exchange_shards(world):
+    """O(N/W) ingest (exchange_points): each rank uploads only its slice of
+    the cloud; the ranks agree on the box, split the key range by an
+    all-reduced histogram and exchange points over all_to_all. The shards
+    partition the cloud into contiguous key ranges; cost and ∂c/∂x equal the
+    1-rank functor's, and per-point outputs at global_index() reproduce it."""
+    import multiprocessing as mp
+    from flash.distributed import ShardedCostFunctor
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q, "irb140")) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    m, pts, x = _scene("irb140")
+    one = ShardedCostFunctor(m, pts, engine=OracleEngine(m))
+    c1, g1 = one.value_and_gradient(x)
+    k1, d1, _ = one.per_point(x)
+    assert all(r[1] == len(pts) for r in res)
+    k = np.full(len(pts), -1)
+    d = np.zeros(len(pts))
+    for _, _, _, c, g, idx, kk, dd, _, _ in res:
+        assert c == pytest.approx(c1, rel=1e-10)
+        assert np.allclose(g, g1, rtol=1e-9, atol=1e-10 * max(1.0, np.abs(g1).max()))
+        k[idx], d[idx] = kk, dd
+    assert np.array_equal(np.sort(np.concatenate([r[5] for r in res])), np.arange(len(pts)))
+    assert np.array_equal(k, k1) and np.array_equal(d, d1)
+    # contiguous key ranges in rank order, about N/W points each
+    spans = [(r[8], r[9]) for r in res if len(r[5])]
+    assert all(spans[i][1] <= spans[i + 1][0] for i in range(len(spans) - 1))
+    assert max(len(r[5]) for r in res) <= 1.5 * len(pts) / world

@@ -39,7 +39,7 @@ def _c4_state():
     return m, qt, np.asarray(qe, np.float64)
 
 
-def _c4_worker(rank, world, port, cloud_path, out_dir, spatial=False):
+def _c4_worker(rank, world, port, cloud_path, out_dir, mode="slice"):
     import sys
     from conftest import ROOT
     sys.path.insert(0, os.path.join(ROOT, "point-cloud-signed-distance_amd"))
@@ -50,9 +50,14 @@ def _c4_worker(rank, world, port, cloud_path, out_dir, spatial=False):
     try:
         m, _, x = _c4_state()
         cloud = np.load(cloud_path, mmap_mode="r")
-        if spatial:  # the whole cloud on every rank, a range of its Hilbert order kept
+        spatial = mode != "slice"
+        if mode == "spatial":  # the whole cloud on every rank, a range of its Hilbert order kept
             f = ShardedCostFunctor(m, np.ascontiguousarray(cloud), rank=rank, world=world, device=0, spatial=True)
             a, b = f.range
+        elif mode == "exchange":  # only this rank's slice uploaded; points moved to their key range's rank
+            a, b = shard_range(len(cloud), rank, world)
+            f = ShardedCostFunctor(m, np.ascontiguousarray(cloud[a:b]), rank=rank, world=world, device=0,
+                                   exchange=True)
         else:
             a, b = shard_range(len(cloud), rank, world)
             f = ShardedCostFunctor(m, np.ascontiguousarray(cloud[a:b]), rank=rank, world=world, device=0)
@@ -68,11 +73,15 @@ def _c4_worker(rank, world, port, cloud_path, out_dir, spatial=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("spatial", [False, True])
-def test_c4_ten_million_points_sharded_over_eight_ranks(spatial, tmp_path):
-    """Slices of the caller's order (round 4) and density-preserving ranges of
-    the whole cloud's Hilbert order (spatial=True): per-point outputs placed at
-    their whole-cloud indices are the single context's bit for bit."""
+@pytest.mark.parametrize("mode", ["slice", "spatial", "exchange"])
+def test_c4_ten_million_points_sharded_over_eight_ranks(mode, tmp_path):
+    """Slices of the caller's order (round 4), density-preserving ranges of
+    the whole cloud's Hilbert order (spatial: every rank uploads the whole
+    cloud) and exchanged shards (exchange: every rank uploads only its slice,
+    flash.distributed.exchange_points): per-point outputs placed at their
+    whole-cloud indices are the single context's bit for bit; the exchanged
+    shards, concatenated in rank order, are exactly the single context's
+    Hilbert order."""
     import multiprocessing as mp
     from flash import synthetic
     from flash.gradientdescent import CostFunctor
@@ -82,7 +91,7 @@ def test_c4_ten_million_points_sharded_over_eight_ranks(spatial, tmp_path):
     np.save(path, cloud)
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_c4_worker, args=(r, C4_RANKS, port, path, str(tmp_path), spatial))
+    procs = [ctx.Process(target=_c4_worker, args=(r, C4_RANKS, port, path, str(tmp_path), mode))
              for r in range(C4_RANKS)]
     for p in procs:
         p.start()
@@ -94,6 +103,9 @@ def test_c4_ten_million_points_sharded_over_eight_ranks(spatial, tmp_path):
     assert all(res[r]["b"] == res[r + 1]["a"] for r in range(C4_RANKS - 1))
     # one context over the whole 10M cloud
     cf = CostFunctor(m, cloud)
+    if mode == "exchange":  # (before any pass: the track! path regroups by itself)
+        assert np.array_equal(np.concatenate([r["idx"] for r in res]), cf.ctx.permutation())
+        assert max(len(r["idx"]) for r in res) <= 1.02 * C4_POINTS / C4_RANKS
     c1, g1 = cf.value_and_gradient(x)
     _, acc1, _ = cf._pass(x)
     k1, d1, gr1 = cf.per_point(x)
@@ -168,3 +180,39 @@ def test_c3_beanbag_full_size_fp32(oracle_mod):
     # ... and the fp32 context with the oracle's fp32 instantiation (oracle/skin_impl.h)
     od32, ok32, og32 = om.skin(_c3_poses(m, x), pts[sel], rbf_rows=rows, precision=32)
     assert np.array_equal(k[sel], ok32) and np.array_equal(d[sel], od32) and np.array_equal(g[sel], og32)
+
+
+def test_exchange_ingest_one_rank_matches_set_points():
+    """fsdf_cloud_box_device + fsdf_curve_keys_device + fsdf_set_points_keyed_device
+    (exchange_points without a process group): the resident order and the
+    per-point outputs of a sorted context's fsdf_set_points, bit for bit —
+    also for a cloud whose slice arrives in another order."""
+    import flash
+    import torch
+    from flash import Models, synthetic, _lib
+    from flash.distributed import exchange_points
+    m = Models.irb140()
+    qt, qe = synthetic.perturbed_configuration(m, 81)
+    cloud = synthetic.depth_cloud(m, qt, 300007, seed=82, order="shuffled")
+    poses = flash.hull_poses(m, qe)
+    spec = [(s.hull.vertices, s.hull.faces, s.hull.planes) for s in m.surfaces]
+    a = _lib.Context(device=0, sort_points=True)
+    a.set_model(spec)
+    a.set_points(cloud)
+    perm_a = a.permutation()
+    a.set_output_order(True)
+    _, acc_a, (ka, da, ga) = a.eval(poses, per_point=True)
+    b = _lib.Context(device=0, sort_points=True)
+    b.set_model(spec)
+    rev = np.arange(len(cloud))[::-1].copy()  # the slice in reverse: the keyed order does not depend on it
+    pts = torch.as_tensor(cloud[rev], device="cuda:0")
+    idx = torch.as_tensor(rev, device="cuda:0")
+    n_res, n_all = exchange_points([b], pts, idx)
+    assert n_res == n_all == len(cloud)
+    assert np.array_equal(b.permutation(), perm_a)
+    b.set_output_order(True)
+    _, acc_b, (kb, db, gb) = b.eval(poses, per_point=True)
+    assert np.array_equal(ka, kb) and np.array_equal(da, db) and np.array_equal(ga, gb)
+    assert np.array_equal(acc_a, acc_b)  # the same resident order: the same sums
+    a.close()
+    b.close()

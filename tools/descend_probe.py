@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""A few track! frames of the bench workload (M64, 2^20 points, estimate_state's
+default solver: 30 iterations, rate 0.1, max_step 0.5) through fsdf_descend,
+device solver loop and host loop, for a rocprofv3 kernel trace of the
+iteration's launches (tools/gpu_run.sh step `descend`):
+
+    rocprofv3 --kernel-trace --output-format csv -d OUT -o run -- python3 tools/descend_probe.py
+
+then `python3 tools/descend_probe.py --trace OUT/.../run_kernel_trace.csv` prints per
+kernel the mean duration and, per iteration of the device loop, the span from
+one solver step's end to the next (the iteration's device time incl. gaps)."""
+import argparse
+import csv
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "point-cloud-signed-distance_amd"))
+
+
+def run(args):
+    import torch  # noqa: F401  (the HIP runtime torch loads, before libflashsdf)
+    from flash import Models, synthetic
+    m = Models.arm_grid() if args.model == "m64" else Models.irb140()
+    q_true, q_eval = synthetic.perturbed_configuration(m, 1234)
+    pts = synthetic.depth_cloud(m, q_true, args.points, seed=1234 + 17)
+    ctx = m.engine(0, 64)
+    surf = m.surfaces
+    ctx.set_mechanism(m.mechanism, [s.body for s in surf], [s.frame.R for s in surf], [s.frame.t for s in surf])
+    for dev_loop in (True, False):
+        ctx.set_solver(dev_loop)
+        ms = []
+        for f in range(args.frames):
+            t0 = time.perf_counter()
+            ctx.set_points(pts)
+            x, val, its = ctx.descend(np.asarray(q_eval, np.float64), 30, 0.1, 0.5, 1e-3, None, float(len(pts)))
+            ms.append((time.perf_counter() - t0) * 1e3)
+        print(f"{'device' if dev_loop else 'host'} loop: frame {statistics.median(ms):.3f} ms, {its} iterations, "
+              f"f {val:.9g}", flush=True)
+
+
+def trace(path):
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    by = {}
+    for r in rows:
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")[:60]
+        by.setdefault(name, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    for name, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
+        print(f"{name:60s} {len(v):6d} x {statistics.mean(v):8.2f} us (median {statistics.median(v):.2f})")
+    steps = [r for r in rows if "solver_step_kernel" in r["Kernel_Name"]]
+    ends = [int(r["End_Timestamp"]) for r in steps]
+    spans = [(b - a) / 1e3 for a, b in zip(ends, ends[1:]) if 0 < b - a < 1e6]
+    if spans:
+        print(f"device loop: step end -> next step end {statistics.median(spans):.2f} us median over {len(spans)}")
+    # the gaps inside an iteration: kernel starts after the previous kernel's end
+    gaps = []
+    for a, b in zip(rows, rows[1:]):
+        if "solver_step_kernel" in b["Kernel_Name"] or "pose_kernel<" in b["Kernel_Name"]:
+            g = (int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3
+            if 0 <= g < 100:
+                gaps.append((b["Kernel_Name"].split("(")[0][-30:], g))
+    for name in sorted({g[0] for g in gaps}):
+        v = [g[1] for g in gaps if g[0] == name]
+        print(f"gap before {name:30s} median {statistics.median(v):.2f} us")
+
+
+if __name__ == "__main__":
+    p = argparse.ArgumentParser()
+    p.add_argument("--model", default="m64", choices=("m64", "irb140"))
+    p.add_argument("--points", type=int, default=1 << 20)
+    p.add_argument("--frames", type=int, default=5)
+    p.add_argument("--trace", default=None)
+    a = p.parse_args()
+    if a.trace:
+        trace(a.trace)
+    else:
+        run(a)

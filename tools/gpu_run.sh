@@ -193,6 +193,13 @@ import csv, glob
 f = glob.glob('$D/ktrace/**/run_kernel_stats.csv', recursive=True)[0]
 for r in list(csv.DictReader(open(f)))[:4]:
     print('ktrace', r['Name'][:70], r['Calls'], round(float(r['AverageNs']) / 1e3, 3), 'us')" ;;
+    descend)
+      # track! frames through fsdf_descend (device and host solver loops) under a kernel trace
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
+          -d $GRAFT_REPO_ROOT/$O/descend -o run -- python3 $GRAFT_REPO_ROOT/tools/descend_probe.py \
+          > $GRAFT_REPO_ROOT/$O/descend.log 2>&1 ) || { echo DESCEND FAILED; tail $O/descend.log; exit 1; }
+      cat $O/descend.log
+      python3 tools/descend_probe.py --trace $(ls $O/descend/*/run_kernel_trace.csv $O/descend/run_kernel_trace.csv 2>/dev/null | head -1) ;;
     c5sweep)
       timeout -k 10 300 python tools/precision_sweep.py --json $O/c5_sweep.json > $O/c5_sweep.log 2>&1 \
         || { echo C5 SWEEP FAILED; tail $O/c5_sweep.log; exit 1; }

@@ -61,6 +61,13 @@ __host__ __device__ inline size_t work_doubles(int nb, int nx, int S) {
   return 1 + 6 * (size_t)S + 42 * (size_t)nb + 3 * (size_t)nx;
 }
 
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)b, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 // The tree blob, the accumulator (optional), Rb / tb and x (+ divisors) into
 // LDS: every thread issues all of its loads before its first store, so the
 // staging costs one memory latency (the blob is ~23 KB for M64: 6 16-B chunks
@@ -164,43 +171,44 @@ __device__ void fk_and_poses(const SolverTree& T, const SolverState& st, const L
   for (int b = 1 + tid; b < nb; b += kSolverBlock) {
     const int k = L.kind[b];
     if (!kin::joint_local(k, L.axis + 3 * b, L.AR + 9 * b, L.At + 3 * b, L.BR + 9 * b, L.Bt + 3 * b,
-                          k ? L.x + L.qoff[b] : L.x, L.LR + 9 * b, L.Lt + 3 * b))
+                          L.x + (k ? L.qoff[b] : 0), L.LR + 9 * b, L.Lt + 3 * b))
       atomicOr(bad, 1);
   }
   STAMP(5);
-  if (tid < 9) {
-    const double v = (tid % 4 == 0) ? 1.0 : 0.0;
-    L.R[tid] = v;
-    L.Rb[tid] = v;
-  } else if (tid < 12) {
-    L.t[tid - 9] = 0.0;
-    L.tb[tid - 9] = 0.0;
+  if (tid == 0) {  // the root: identity (one thread: no per-lane choice of the destination array)
+    for (int i = 0; i < 9; ++i) {
+      const double v = (i % 4 == 0) ? 1.0 : 0.0;
+      L.R[i] = v;
+      L.Rb[i] = v;
+    }
+    for (int i = 0; i < 3; ++i) {
+      L.t[i] = 0.0;
+      L.tb[i] = 0.0;
+    }
   }
   __syncthreads();
+  // level by level, a body's 24 output entries on 24 lanes (kin::compose_entry)
   for (int d = 0; d < T.D; ++d) {
     const int a = L.doff[d], e = L.doff[d + 1];
-    for (int i = a + tid; i < e; i += kSolverBlock) {
-      const int b = L.dord[i], p = L.parent[b];
-      kin::compose(L.R + 9 * p, L.t + 3 * p, L.LR + 9 * b, L.Lt + 3 * b, L.AR + 9 * b, L.At + 3 * b, L.R + 9 * b,
-                   L.t + 3 * b, L.Rb + 9 * b, L.tb + 3 * b);
+    for (int i = tid; i < 24 * (e - a); i += kSolverBlock) {
+      const int b = L.dord[a + i / 24], p = L.parent[b], q = i % 24;
+      const double v = kin::compose_entry(q, L.R + 9 * p, L.t + 3 * p, L.LR + 9 * b, L.Lt + 3 * b, L.AR + 9 * b,
+                                          L.At + 3 * b);
+      if (q < 9) L.R[9 * b + q] = v;
+      else if (q < 12) L.t[3 * b + q - 9] = v;
+      else if (q < 21) L.Rb[9 * b + q - 12] = v;
+      else L.tb[3 * b + q - 21] = v;
     }
     __syncthreads();
   }
   STAMP(6);
-  for (int k = tid; k < T.S; k += kSolverBlock) {
-    double P[12];
-    const int b = L.sbody[k];
-    if (b < 0) {
-      for (int i = 0; i < 12; ++i) P[i] = (i % 4 == 0 && i < 9) ? 1.0 : 0.0;
-    } else {
-      kin::surface_pose(L.R + 9 * b, L.t + 3 * b, L.FR + 9 * k, L.Ft + 3 * k, P);
-    }
-    bool fin = true;
-    for (int i = 0; i < 12; ++i) {
-      fin = fin && isfinite(P[i]);
-      st.poses[12 * k + i] = P[i];
-    }
-    if (!fin) atomicOr(bad, 2);
+  // the surface poses, one entry per lane
+  for (int i = tid; i < 12 * T.S; i += kSolverBlock) {
+    const int k = i / 12, q = i % 12, b = L.sbody[k];
+    const double v = b < 0 ? ((q % 4 == 0 && q < 9) ? 1.0 : 0.0)
+                           : kin::surface_pose_entry(q, L.R + 9 * b, L.t + 3 * b, L.FR + 9 * k, L.Ft + 3 * k);
+    st.poses[i] = v;
+    if (!isfinite(v)) atomicOr(bad, 2);
   }
   STAMP(7);
   for (int i = tid; i < 9 * nb; i += kSolverBlock) st.Rb[i] = L.Rb[i];
@@ -273,10 +281,20 @@ __global__ __launch_bounds__(kSolverBlock) void solver_step_kernel(SolverTree T,
   }
   __syncthreads();
   STAMP(3);
-  if (tid == 0) {
-    double nrm2 = 0.0;  // in index order, as the host sums it
-#pragma unroll 8
+  // |g|^2 in index order, as the host sums it: wave 0 squares in parallel, lane
+  // 0 adds the squares in order, read straight from the lanes (readlane: no
+  // LDS round trip per term)
+  double nrm2 = 0.0;
+  if (nx <= 64) {
+    if (tid < 64) {
+      const double gi = tid < nx ? L.g[tid] : 0.0;
+      const double sq = gi * gi;
+      for (int i = 0; i < nx; ++i) nrm2 += readlane_f64(sq, i);
+    }
+  } else if (tid == 0) {
     for (int i = 0; i < nx; ++i) nrm2 += L.g[i] * L.g[i];
+  }
+  if (tid == 0) {
     const double cost = L.acc[0] + st.weight * 0.0;  // (rigid: the regularizer's sum is 0.0)
     const int it = st.flags[1] + 1;
     st.flags[1] = it;

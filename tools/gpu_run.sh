@@ -200,6 +200,11 @@ for r in list(csv.DictReader(open(f)))[:4]:
           > $GRAFT_REPO_ROOT/$O/descend.log 2>&1 ) || { echo DESCEND FAILED; tail $O/descend.log; exit 1; }
       cat $O/descend.log
       python3 tools/descend_probe.py --trace $(ls $O/descend/*/run_kernel_trace.csv $O/descend/run_kernel_trace.csv 2>/dev/null | head -1) ;;
+    c4proj)
+      # BASELINE C4 projection from one GPU: per-pass and per-frame (ingest) max over ranks (tools/c4_projection.py)
+      timeout -k 10 600 python -u tools/c4_projection.py > $O/c4_projection.jsonl 2> $O/c4_projection.err \
+        || { echo C4PROJ FAILED; tail $O/c4_projection.err; exit 1; }
+      cut -c1-300 $O/c4_projection.jsonl ;;
     c5sweep)
       timeout -k 10 300 python tools/precision_sweep.py --json $O/c5_sweep.json > $O/c5_sweep.log 2>&1 \
         || { echo C5 SWEEP FAILED; tail $O/c5_sweep.log; exit 1; }

@@ -89,6 +89,10 @@ def main():
         for i in range(8):  # first pass (tier shape), plan, planned passes
             ctx.eval_device(poses[i & 1], acc.data_ptr(), *outs)
         torch.cuda.synchronize()
+        # the chunk costs of the range in the whole cloud's Hilbert chunk order —
+        # before any regroup, which permutes the chunks (round-5 advice: costs
+        # read after the regroup mis-placed the balanced cuts)
+        pre_costs = ctx.chunk_costs()
         if regroup:
             ctx.regroup_points()
             for i in range(8):  # other chunks: plan anew
@@ -105,7 +109,7 @@ def main():
             kms, _, launches = ctx.pass_times()
             ctx.profile_pass(False)
             best = (min(best[0], step), min(best[1], kms / max(launches, 1)))
-        return best
+        return best, pre_costs
 
     for w in (int(x) for x in a.ws.split(",")):
         eq_costs = None
@@ -121,11 +125,10 @@ def main():
             steps, kernels, costs, kinds = [], [], [], []
             for r in range(w):
                 load(split, bounds, r)
-                s, k = step_rank(a.regroup and split != "slice")
+                (s, k), cc = step_rank(a.regroup and split != "slice")
                 steps.append(s)
                 kernels.append(k)
                 kinds.append(ctx.pass_kernel_name())
-                cc = ctx.chunk_costs()
                 costs.append(cc)
             if split == "spatial":
                 cat = np.concatenate(costs).astype(np.float64)

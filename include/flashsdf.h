@@ -215,14 +215,18 @@ int fsdf_state_gradient(fsdf_ctx* ctx, const double* x, const double* accum, dou
  * value_out = f of the last evaluation, iterations_out = evaluations made. */
 int fsdf_descend(fsdf_ctx* ctx, double* x, int32_t iteration_limit, double rate, double max_step, double tolerance,
                  const double* divisors, double n_points, double* value_out, int32_t* iterations_out);
-/* Where fsdf_descend iterates for rigid scenes (no RBF skin, no deformation):
- * device_loop = 1 (default) — every iteration on the device, the frame's
- * passes and solver steps enqueued up front and read back once (FK, chain rule,
- * NaiveSolver step in one small workgroup after each pass: the host loop's
- * arithmetic in the same order, so x, value and iterations are bit-identical
- * to it; after convergence the remaining launches return at once); 0 — the
- * host loop around fsdf_value_and_gradient, one synchronization per iteration.
- * RBF scenes always use the host loop. */
+/* Where fsdf_descend iterates. device_loop = 0 (default): the host loop around
+ * fsdf_value_and_gradient, one synchronization per iteration. 1: rigid scenes
+ * (no RBF skin, no deformation) iterate on the device where the mechanism fits
+ * the solver step's 64 KB of LDS, others on the host; 2: the device loop is
+ * required (FSDF_ERR_STATE otherwise). The device loop enqueues the frame's
+ * passes and solver steps up front and reads x, value and count back once
+ * (csrc/solver.hip: FK, chain rule and the clipped NaiveSolver step in one
+ * workgroup after each pass, the host loop's arithmetic in the same order — x,
+ * value and iterations bit-identical to it; after convergence the remaining
+ * launches return at once). Measured on M64 at 2^20 points its solver step
+ * (~15 us) costs about what the host round trip does, so the host loop stays
+ * the default. */
 int fsdf_set_solver(fsdf_ctx* ctx, int32_t device_loop);
 
 /* ---- context ---------------------------------------------------------------- */

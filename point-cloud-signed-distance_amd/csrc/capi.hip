@@ -190,7 +190,8 @@ struct fsdf_ctx {
   // device solver loop of fsdf_descend (solver.hip): the mechanism's device
   // arrays (built on the first device descend after fsdf_set_mechanism) and
   // one frame's state; pinned staging for x / divisors in and x, f, flags out
-  int solver_device = 1;             // fsdf_set_solver
+  int solver_device = 0;             // fsdf_set_solver: 0 host loop (default: measured faster, DESIGN.md §7
+                                     // round 6), 1 device where possible, 2 device required
   bool solver_tree_ok = false;
   fsdf::SolverTree stree;
   double* d_stree_d = nullptr;       // the tree blob (fsdf::SolverTree::blob)
@@ -1752,15 +1753,35 @@ static int build_solver_tree(fsdf_ctx* c) {
     iv.insert(iv.end(), v.begin(), v.end());
     return at;
   };
+  // dord / doff: every body's path from the root, its ancestors of depth 1 .. its own
+  // (the device composes a body's chain in registers, one thread per body)
   std::vector<int32_t> dord, doff(1, 0), hord, hoff(1, 0), coff(1, 0), clist, soff(1, 0), slist;
-  for (int d = 1; d <= D; ++d) {
-    for (int b = 1; b < nb; ++b)
-      if (depth[b] == d) dord.push_back(b);
+  dord.reserve((size_t)nb * (size_t)(D + 1));
+  for (int b = 0; b < nb; ++b) {
+    std::vector<int32_t> path;
+    for (int a = b; a > 0; a = M.parent[a]) path.push_back(a);
+    dord.insert(dord.end(), path.rbegin(), path.rend());
     doff.push_back((int32_t)dord.size());
+  }
+  int widest = 0;  // the most parents at one height: the subtree sums run in one wave when 6x that fits
+  // chains: every body but the root has at most one child (IRB140, M64's arms): body b's
+  // subtree is the list b, child, grandchild, ... (dlist / dof), summed in one thread
+  bool chains = true;
+  for (int b = 1; b < nb; ++b) chains = chains && nchild[b] <= 1;
+  std::vector<int32_t> dlist, dof(1, 0);
+  if (chains) {
+    std::vector<int32_t> child(nb, -1);
+    for (int b = 1; b < nb; ++b)
+      if (M.parent[b] > 0) child[M.parent[b]] = b;
+    for (int b = 0; b < nb; ++b) {
+      for (int a = b; b > 0 && a >= 0; a = child[a]) dlist.push_back(a);
+      dof.push_back((int32_t)dlist.size());
+    }
   }
   for (int h = 1; h <= H; ++h) {
     for (int b = 1; b < nb; ++b)
       if (nchild[b] && height[b] == h) hord.push_back(b);
+    widest = std::max(widest, (int)hord.size() - hoff.back());
     hoff.push_back((int32_t)hord.size());
   }
   for (int p = 0; p < nb; ++p) {
@@ -1773,7 +1794,8 @@ static int build_solver_tree(fsdf_ctx* c) {
   }
   const size_t o_parent = put(M.parent), o_kind = put(M.kind), o_qoff = put(M.qoff), o_dord = put(dord),
                o_doff = put(doff), o_hord = put(hord), o_hoff = put(hoff), o_coff = put(coff), o_clist = put(clist),
-               o_soff = put(soff), o_slist = put(slist), o_sb = put(M.surface_body);
+               o_soff = put(soff), o_slist = put(slist), o_sb = put(M.surface_body), o_dlist = put(dlist),
+               o_dof = put(dof);
   std::vector<double> dv;
   auto putd = [&](const std::vector<double>& v) {
     const size_t at = dv.size();
@@ -1804,8 +1826,12 @@ static int build_solver_tree(fsdf_ctx* c) {
   T.parent = (int)o_parent;
   T.kind = (int)o_kind;
   T.qoff = (int)o_qoff;
-  T.depth_order = (int)o_dord;
-  T.depth_off = (int)o_doff;
+  T.path_list = (int)o_dord;
+  T.path_off = (int)o_doff;
+  T.narrow = 6 * widest <= 64;
+  T.chains = chains;
+  T.chain_list = (int)o_dlist;
+  T.chain_off = (int)o_dof;
   T.height_order = (int)o_hord;
   T.height_off = (int)o_hoff;
   T.child_off = (int)o_coff;
@@ -1877,6 +1903,7 @@ static int descend_device(fsdf_ctx* c, double* x, int32_t iteration_limit, doubl
   st.n_points = n_points;
   st.weight = M.weight;
   st.limit = iteration_limit;
+  HIPCHECK(c, hipMemsetAsync(c->d_solver_flags, 0, 4 * sizeof(int), c->stream));
   HIPCHECK(c, fsdf::launch_solver_init(c->stree, st, c->stream));
   for (int it = 0; it < iteration_limit; ++it) {
     int rc = run_pass(c, nullptr, c->d_pts, c->n, c->d_accum, nullptr, nullptr, nullptr, nullptr, true, st.poses,
@@ -1913,7 +1940,8 @@ static int descend_device(fsdf_ctx* c, double* x, int32_t iteration_limit, doubl
 
 extern "C" int fsdf_set_solver(fsdf_ctx* c, int32_t device_loop) {
   if (!c) return FSDF_ERR_ARG;
-  c->solver_device = device_loop != 0;
+  if (device_loop < 0 || device_loop > 2) return fail(c, FSDF_ERR_ARG, "set_solver: mode %d", device_loop);
+  c->solver_device = device_loop;
   return FSDF_OK;
 }
 
@@ -1929,11 +1957,20 @@ extern "C" int fsdf_descend(fsdf_ctx* c, double* x, int32_t iteration_limit, dou
   if ((int)Mc.surface_body.size() != c->lm.S || (int)Mc.poses.size() != 12 * c->lm.S)
     return fail(c, FSDF_ERR_STATE, "descend: mechanism registered for another surface list (call fsdf_set_mechanism)");
   // rigid scenes (no RBF skin, no deformation) iterate on the device when the
-  // mechanism fits the step's LDS (at most 8 + 2S + depth + height + 4 ints and
-  // 69 nb + 18 S + 3 nx + 1 doubles: M64's 65 bodies take 49 KB)
-  const int ni_max = 8 * Mc.nb + 2 * c->lm.S + 2 * Mc.nb + 4;
-  if (c->solver_device && iteration_limit > 0 && c->lm.R == 0 && Mc.n_deform == 0 && c->n > 0 &&
-      fsdf::solver_fits(Mc.nb, Mc.nq, c->lm.S, ni_max))
+  // mechanism's tree and the step's work arrays fit the step's LDS (M64's 65
+  // bodies: ~45 KB)
+  bool device_loop = c->solver_device && iteration_limit > 0 && c->lm.R == 0 && Mc.n_deform == 0 && c->n > 0;
+  if (device_loop && !c->solver_tree_ok) {
+    HIPCHECK(c, hipSetDevice(c->device));
+    const int rc = build_solver_tree(c);
+    if (rc) return rc;
+  }
+  device_loop = device_loop && fsdf::solver_fits(Mc.nb, Mc.nq, c->lm.S, c->stree.ni);
+  if (c->solver_device == 2 && iteration_limit > 0 && !device_loop)
+    return fail(c, FSDF_ERR_STATE, "descend: the device loop was required (fsdf_set_solver 2) but the scene %s",
+                c->lm.R > 0 || Mc.n_deform > 0 ? "has RBF skins / deformations" :
+                c->n == 0 ? "has no resident points" : "does not fit the solver step's LDS");
+  if (device_loop)
     return descend_device(c, x, iteration_limit, rate, max_step, tolerance, divisors, n_points, value_out,
                           iterations_out);
   const int ns = c->mech.nq + 3 * c->mech.n_deform;

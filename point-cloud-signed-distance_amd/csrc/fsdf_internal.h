@@ -265,17 +265,21 @@ hipError_t regroup_points(void** d_pts, int64_t* pts_cap, int64_t n, int precisi
 // later access in their level loops is an LDS access.
 struct SolverTree {
   int nb = 0, nx = 0, S = 0;
-  int D = 0;  // depth levels of bodies >= 1: depth_order[depth_off[d] .. depth_off[d+1]) at depth d+1
+  int D = 0;  // depth of the deepest body
   int H = 0;  // height levels of bodies with children: height_order[height_off[h] .. ) at height h+1
+  int narrow = 0;  // every height level has <= 10 parents: the subtree sums run in one wave
+  int chains = 0;  // every non-root body has <= 1 child: subtree sums along chain lists, no levels
   // one blob: the doubles [nd], then the ints [ni], padded to 16 B — copied into
   // LDS with one batch of 16-B loads per thread (one memory latency)
   const void* blob = nullptr;
   int ni = 0, nd = 0, chunks16 = 0;
   // offsets into the ints
-  int parent = 0, kind = 0, qoff = 0, depth_order = 0, depth_off = 0, height_order = 0, height_off = 0;
+  // path_list[path_off[b] .. path_off[b+1]): body b's ancestors from depth 1 down to b
+  int parent = 0, kind = 0, qoff = 0, path_list = 0, path_off = 0, height_order = 0, height_off = 0;
   int child_off = 0, child_list = 0;  // [nb+1], children in descending index
   int surf_off = 0, surf_list = 0;    // [nb+1], surfaces in ascending index
   int surface_body = 0;               // [S]
+  int chain_list = 0, chain_off = 0;  // (chains) [nb+1]: body b, its child, grandchild, ...
   // offsets into the doubles
   int axis = 0, AR = 0, At = 0, BR = 0, Bt = 0, frame_R = 0, frame_t = 0;  // frames: [S][9], [S][3]
 };
@@ -296,7 +300,7 @@ struct SolverState {
 bool solver_fits(int nb, int nx, int S, int ni);
 // diagnostic builds (-DFSDF_SOLVER_TIMES=1): the last step's phase clocks (16, 100 MHz)
 void solver_times(unsigned long long* out);
-// FK of st.x -> poses, Rb, tb; flags = (error != 0, 0, error)
+// FK of st.x -> poses, Rb, tb (flags zeroed by the caller; set on an error)
 hipError_t launch_solver_init(const SolverTree& T, const SolverState& st, hipStream_t s);
 // one NaiveSolver iteration from the pass's accumulator (skips once flags[0] is set)
 hipError_t launch_solver_step(const SolverTree& T, const SolverState& st, const double* d_accum, hipStream_t s);

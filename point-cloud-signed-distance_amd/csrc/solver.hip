@@ -53,7 +53,8 @@ __device__ unsigned long long g_solver_times[64];
 struct Lds {
   const double *axis, *AR, *At, *BR, *Bt, *FR, *Ft;
   double *acc, *Rb, *tb, *sub, *LR, *Lt, *R, *t, *x, *g, *div;
-  const int32_t *parent, *kind, *qoff, *dord, *doff, *hord, *hoff, *coff, *clist, *soff, *slist, *sbody;
+  const int32_t *parent, *kind, *qoff, *plist, *poff, *hord, *hoff, *coff, *clist, *soff, *slist, *sbody;
+  const int32_t *chlist, *choff;
 };
 
 // the doubles after the blob: acc | Rb | tb | x | div | sub | LR | Lt | R | t | g
@@ -74,7 +75,7 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 // per thread). A copy loop that stores each load before the next one waits a
 // full memory round trip (~1-2 us) per element per thread — measured 28 us per
 // step that way.
-constexpr int kBlobPer = 8;   // 16-B blob chunks per thread: blobs up to 32 KB
+constexpr int kBlobPer = 12;  // 16-B blob chunks per thread: blobs up to 48 KB
 constexpr int kDynPer = 8;    // dynamic doubles per thread (accum, Rb|tb, x, div): up to 2,048
 
 __device__ Lds stage(const SolverTree& T, const SolverState& st, double* lds, const double* accum) {
@@ -120,8 +121,8 @@ __device__ Lds stage(const SolverTree& T, const SolverState& st, double* lds, co
   L.parent = iv + T.parent;
   L.kind = iv + T.kind;
   L.qoff = iv + T.qoff;
-  L.dord = iv + T.depth_order;
-  L.doff = iv + T.depth_off;
+  L.plist = iv + T.path_list;
+  L.poff = iv + T.path_off;
   L.hord = iv + T.height_order;
   L.hoff = iv + T.height_off;
   L.coff = iv + T.child_off;
@@ -129,6 +130,8 @@ __device__ Lds stage(const SolverTree& T, const SolverState& st, double* lds, co
   L.soff = iv + T.surf_off;
   L.slist = iv + T.surf_list;
   L.sbody = iv + T.surface_body;
+  L.chlist = iv + T.chain_list;
+  L.choff = iv + T.chain_off;
   d += 2 * T.chunks16;  // (the blob, padded to 16 B)
   L.acc = d;
   d += 1 + 6 * S;
@@ -163,10 +166,11 @@ __device__ Lds stage(const SolverTree& T, const SolverState& st, double* lds, co
   return L;
 }
 
-// FK of L.x into L.R, t, Rb, tb; then the surface poses (global) and Rb, tb
-// (global, for the next chain rule). *bad: 1 a zero quaternion / unknown
-// joint, 2 a non-finite pose.
-__device__ void fk_and_poses(const SolverTree& T, const SolverState& st, const Lds& L, int* bad, int it0 = -1) {
+// FK of L.x into L.R, t, Rb, tb (LDS; *bad |= 1 for a zero quaternion /
+// unknown joint). Global memory is not touched: a workgroup barrier after a
+// global store waits for the store to complete (its release fence), so every
+// store of the step is issued after the last barrier (publish()).
+__device__ void fk(const SolverTree& T, const Lds& L, int* bad) {
   const int tid = threadIdx.x, nb = T.nb;
   for (int b = 1 + tid; b < nb; b += kSolverBlock) {
     const int k = L.kind[b];
@@ -174,7 +178,6 @@ __device__ void fk_and_poses(const SolverTree& T, const SolverState& st, const L
                           L.x + (k ? L.qoff[b] : 0), L.LR + 9 * b, L.Lt + 3 * b))
       atomicOr(bad, 1);
   }
-  STAMP(5);
   if (tid == 0) {  // the root: identity (one thread: no per-lane choice of the destination array)
     for (int i = 0; i < 9; ++i) {
       const double v = (i % 4 == 0) ? 1.0 : 0.0;
@@ -187,33 +190,70 @@ __device__ void fk_and_poses(const SolverTree& T, const SolverState& st, const L
     }
   }
   __syncthreads();
-  // level by level, a body's 24 output entries on 24 lanes (kin::compose_entry)
-  for (int d = 0; d < T.D; ++d) {
-    const int a = L.doff[d], e = L.doff[d + 1];
-    for (int i = tid; i < 24 * (e - a); i += kSolverBlock) {
-      const int b = L.dord[a + i / 24], p = L.parent[b], q = i % 24;
-      const double v = kin::compose_entry(q, L.R + 9 * p, L.t + 3 * p, L.LR + 9 * b, L.Lt + 3 * b, L.AR + 9 * b,
-                                          L.At + 3 * b);
-      if (q < 9) L.R[9 * b + q] = v;
-      else if (q < 12) L.t[3 * b + q - 9] = v;
-      else if (q < 21) L.Rb[9 * b + q - 12] = v;
-      else L.tb[3 * b + q - 21] = v;
+  // one thread per body composes its chain from the root in registers (every
+  // ancestor's product as the host's level order computes it: the same bits,
+  // no barrier per level); the ancestors' R, t only, and the joint frame
+  // Rb, tb = R_parent · joint_to_parent for b itself
+  for (int b = 1 + tid; b < nb; b += kSolverBlock) {
+    double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, t[3] = {0, 0, 0}, v[12], w[12];
+    const int q0 = L.poff[b], q1 = L.poff[b + 1];
+    for (int q = q0; q < q1; ++q) {
+      const int a = L.plist[q];
+      double LR[9], Lt[3];
+      kin::load(L.LR + 9 * a, LR, 9);
+      kin::load(L.Lt + 3 * a, Lt, 3);
+      if (q == q1 - 1) {
+        double AR[9], At[3];
+        kin::load(L.AR + 9 * a, AR, 9);
+        kin::load(L.At + 3 * a, At, 3);
+#pragma unroll
+        for (int e = 0; e < 12; ++e) w[e] = kin::compose_entry(12 + e, R, t, LR, Lt, AR, At);
+      }
+#pragma unroll
+      for (int e = 0; e < 12; ++e) v[e] = kin::compose_entry(e, R, t, LR, Lt, nullptr, nullptr);
+#pragma unroll
+      for (int e = 0; e < 9; ++e) R[e] = v[e];
+#pragma unroll
+      for (int e = 0; e < 3; ++e) t[e] = v[9 + e];
     }
-    __syncthreads();
+    kin::store(L.R + 9 * b, v, 9);
+    kin::store(L.t + 3 * b, v + 9, 3);
+    kin::store(L.Rb + 9 * b, w, 9);
+    kin::store(L.tb + 3 * b, w + 9, 3);
   }
-  STAMP(6);
-  // the surface poses, one entry per lane
-  for (int i = tid; i < 12 * T.S; i += kSolverBlock) {
-    const int k = i / 12, q = i % 12, b = L.sbody[k];
-    const double v = b < 0 ? ((q % 4 == 0 && q < 9) ? 1.0 : 0.0)
-                           : kin::surface_pose_entry(q, L.R + 9 * b, L.t + 3 * b, L.FR + 9 * k, L.Ft + 3 * k);
-    st.poses[i] = v;
-    if (!isfinite(v)) atomicOr(bad, 2);
+  __syncthreads();
+}
+
+// After the last barrier: the surface poses (one entry per lane; a non-finite
+// entry marks the frame failed, error 2), the joint frames for the next chain
+// rule, x, and — thread 0 — f, the iteration count and the done / error flags.
+// pose = false: the last iteration (no pass follows) publishes x and the flags only.
+__device__ void publish(const SolverTree& T, const SolverState& st, const Lds& L, bool pose, int bad, double f,
+                        int it, int done) {
+  const int tid = threadIdx.x, nb = T.nb;
+  if (pose) {
+    for (int i = tid; i < 12 * T.S; i += kSolverBlock) {
+      const int k = i / 12, q = i % 12, b = L.sbody[k];
+      const double v = b < 0 ? ((q % 4 == 0 && q < 9) ? 1.0 : 0.0)
+                             : kin::surface_pose_entry(q, L.R + 9 * b, L.t + 3 * b, L.FR + 9 * k, L.Ft + 3 * k);
+      st.poses[i] = v;
+      if (!isfinite(v)) {  // (every writer writes the same values)
+        st.flags[2] = 2;
+        st.flags[0] = 1;
+      }
+    }
+    for (int i = tid; i < 9 * nb; i += kSolverBlock) st.Rb[i] = L.Rb[i];
+    for (int i = tid; i < 3 * nb; i += kSolverBlock) st.tb[i] = L.tb[i];
   }
-  STAMP(7);
-  for (int i = tid; i < 9 * nb; i += kSolverBlock) st.Rb[i] = L.Rb[i];
-  for (int i = tid; i < 3 * nb; i += kSolverBlock) st.tb[i] = L.tb[i];
-  STAMP(8);
+  for (int i = tid; i < T.nx; i += kSolverBlock) st.x[i] = L.x[i];
+  if (tid == 0) {
+    *st.f = f;
+    st.flags[1] = it;
+    if (bad || done) {
+      st.flags[2] = bad ? 1 : 0;
+      st.flags[0] = 1;
+    }
+  }
 }
 
 __global__ __launch_bounds__(kSolverBlock) void solver_init_kernel(SolverTree T, SolverState st) {
@@ -223,48 +263,84 @@ __global__ __launch_bounds__(kSolverBlock) void solver_init_kernel(SolverTree T,
   if (tid == 0) bad = 0;
   const Lds L = stage(T, st, lds, nullptr);
   __syncthreads();
-  fk_and_poses(T, st, L, &bad);
-  __syncthreads();
-  if (tid == 0) {
-    st.flags[1] = 0;
-    st.flags[2] = bad;
-    st.flags[0] = bad ? 1 : 0;
-    *st.f = 0.0;
-  }
+  fk(T, L, &bad);  // (ends with a barrier; the host zeroed the flags before this launch)
+  publish(T, st, L, true, bad, 0.0, 0, 0);
 }
 
 __global__ __launch_bounds__(kSolverBlock) void solver_step_kernel(SolverTree T, SolverState st,
                                                                    const double* __restrict__ accum) {
-  if (st.flags[0]) return;  // converged (or failed): the frame's remaining steps are no-ops
+  // (the frame's flags load with the stage's loads; the done check waits for them)
+  const int done = __builtin_nontemporal_load(st.flags), it_before = __builtin_nontemporal_load(st.flags + 1);
   extern __shared__ double lds[];
   __shared__ int bad, verdict;
+  __shared__ double s_f;
   const int tid = threadIdx.x, nb = T.nb, nx = T.nx;
 #if FSDF_SOLVER_TIMES
-  const int it0 = st.flags[1];
+  const int it0 = it_before;
 #endif
   STAMP(0);
   if (tid == 0) bad = 0;
   const Lds L = stage(T, st, lds, accum);
+  if (done) return;  // converged (or failed): the frame's remaining steps are no-ops (uniform)
   __syncthreads();
   STAMP(1);
-  // body wrenches: each body's surfaces in index order (fsdf_config_gradient)
-  for (int i = tid; i < 6 * nb; i += kSolverBlock) {
-    const int b = i / 6, j = i - 6 * b;
-    double s = 0.0;
-    for (int q = L.soff[b]; q < L.soff[b + 1]; ++q) s += L.acc[1 + 6 * L.slist[q] + j];
-    L.sub[i] = s;
-  }
-  __syncthreads();
-  // subtree sums: parents by height, each adding its children in descending index
-  for (int h = 0; h < T.H; ++h) {
-    const int a = L.hoff[h], e = L.hoff[h + 1];
-    for (int i = tid; i < 6 * (e - a); i += kSolverBlock) {
-      const int p = L.hord[a + i / 6], j = i % 6;
-      double s = L.sub[6 * p + j];
-      for (int q = L.coff[p]; q < L.coff[p + 1]; ++q) s += L.sub[6 * L.clist[q] + j];
-      L.sub[6 * p + j] = s;
+  if (T.chains) {
+    // chains (every non-root body has <= 1 child): body b's subtree sum along
+    // its chain, deepest first — sub[a] = own[a] + sub[child], own[a] the body's
+    // surfaces summed in index order from 0.0: fsdf_config_gradient's additions
+    // in its order, in one thread per (b, component), no level barriers
+    for (int i = tid; i < 6 * (nb - 1); i += kSolverBlock) {
+      const int b = 1 + i / 6, j = i % 6;
+      const int q0 = L.choff[b], q1 = L.choff[b + 1];
+      double s = 0.0;
+      for (int q = q1 - 1; q >= q0; --q) {
+        const int a = L.chlist[q];
+        double o = 0.0;
+        for (int u = L.soff[a]; u < L.soff[a + 1]; ++u) o += L.acc[1 + 6 * L.slist[u] + j];
+        s = q == q1 - 1 ? o : o + s;
+      }
+      L.sub[6 * b + j] = s;
     }
     __syncthreads();
+  } else {
+    // body wrenches: each body's surfaces in index order (fsdf_config_gradient)
+    for (int i = tid; i < 6 * nb; i += kSolverBlock) {
+      const int b = i / 6, j = i - 6 * b;
+      double s = 0.0;
+      for (int q = L.soff[b]; q < L.soff[b + 1]; ++q) s += L.acc[1 + 6 * L.slist[q] + j];
+      L.sub[i] = s;
+    }
+    __syncthreads();
+    // subtree sums: parents by height, each adding its children in descending
+    // index; a narrow tree (<= 10 parents per height) in one wave, its levels
+    // ordered by wave-local fences instead of workgroup barriers
+    if (T.narrow) {
+      if (tid < 64) {
+        for (int h = 0; h < T.H; ++h) {
+          const int a = L.hoff[h], e = L.hoff[h + 1];
+          if (tid < 6 * (e - a)) {
+            const int p = L.hord[a + tid / 6], j = tid % 6;
+            double s = L.sub[6 * p + j];
+            for (int q = L.coff[p]; q < L.coff[p + 1]; ++q) s += L.sub[6 * L.clist[q] + j];
+            L.sub[6 * p + j] = s;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+      __syncthreads();
+    } else {
+      for (int h = 0; h < T.H; ++h) {
+        const int a = L.hoff[h], e = L.hoff[h + 1];
+        for (int i = tid; i < 6 * (e - a); i += kSolverBlock) {
+          const int p = L.hord[a + i / 6], j = i % 6;
+          double s = L.sub[6 * p + j];
+          for (int q = L.coff[p]; q < L.coff[p + 1]; ++q) s += L.sub[6 * L.clist[q] + j];
+          L.sub[6 * p + j] = s;
+        }
+        __syncthreads();
+      }
+    }
   }
   STAMP(2);
   for (int b = 1 + tid; b < nb; b += kSolverBlock) {
@@ -294,44 +370,31 @@ __global__ __launch_bounds__(kSolverBlock) void solver_step_kernel(SolverTree T,
   } else if (tid == 0) {
     for (int i = 0; i < nx; ++i) nrm2 += L.g[i] * L.g[i];
   }
+  const int it = it_before + 1;
   if (tid == 0) {
     const double cost = L.acc[0] + st.weight * 0.0;  // (rigid: the regularizer's sum is 0.0)
-    const int it = st.flags[1] + 1;
-    st.flags[1] = it;
-    *st.f = cost / st.n_points;
+    s_f = cost / st.n_points;
     verdict = bad ? 3 : (sqrt(nrm2) < st.tol ? 1 : (it >= st.limit ? 2 : 0));
   }
   __syncthreads();
   const int v = verdict;
+  const double f = s_f;
   if (v == 3 || v == 1) {  // failed / converged: x stays
-    if (tid == 0) {
-      st.flags[2] = v == 3 ? 1 : 0;
-      st.flags[0] = 1;
-    }
+    publish(T, st, L, false, v == 3, f, it, 1);
     return;
   }
-  for (int i = tid; i < nx; i += kSolverBlock) {
-    const double xi = L.x[i] + kin::clipped_step(st.rate, L.g[i], st.max_step);
-    L.x[i] = xi;
-    st.x[i] = xi;
-  }
+  for (int i = tid; i < nx; i += kSolverBlock) L.x[i] = L.x[i] + kin::clipped_step(st.rate, L.g[i], st.max_step);
   if (v == 2) {  // the last iteration: no pass follows
-    if (tid == 0) st.flags[0] = 1;
+    __syncthreads();
+    publish(T, st, L, false, 0, f, it, 1);
     return;
   }
   __syncthreads();
   STAMP(4);
-#if FSDF_SOLVER_TIMES
-  fk_and_poses(T, st, L, &bad, it0);
-#else
-  fk_and_poses(T, st, L, &bad);
-#endif
-  __syncthreads();
+  fk(T, L, &bad);  // (ends with a barrier)
+  STAMP(6);
+  publish(T, st, L, true, bad, f, it, 0);
   STAMP(9);
-  if (tid == 0 && bad) {
-    st.flags[2] = bad;
-    st.flags[0] = 1;
-  }
 }
 
 size_t solver_lds_bytes(const SolverTree& T) {

@@ -293,10 +293,13 @@ class Context:
         check(self._lib.fsdf_set_regroup(self._ctx, self.REGROUP_AUTO if auto else self.REGROUP_OFF), self._ctx,
               "set_regroup")
 
-    def set_solver(self, device_loop: bool):
-        """fsdf_set_solver: descend's iterations on the device (rigid scenes;
-        default) or the host loop around value_and_gradient."""
-        check(self._lib.fsdf_set_solver(self._ctx, int(bool(device_loop))), self._ctx, "set_solver")
+    def set_solver(self, device_loop):
+        """fsdf_set_solver: descend's iterations on the device where the scene
+        allows (True / 1: rigid scenes), required there ("require" / 2:
+        FSDF_ERR_STATE otherwise), or the host loop around value_and_gradient
+        (False / 0, the default)."""
+        mode = 2 if device_loop == "require" else int(device_loop)
+        check(self._lib.fsdf_set_solver(self._ctx, mode), self._ctx, "set_solver")
 
     def regroup_points(self):
         """Regroup the resident cloud by each point's nearest surface in the

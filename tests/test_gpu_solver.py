@@ -64,7 +64,7 @@ def test_device_loop_bit_identical_to_host_loop(name, n):
     div = np.linspace(1.0, 1.5, nx)
     for tol, limit, rate, div_ in ((0.0, 7, 0.5, None), (1e-3, 40, 2.0, div), (1e30, 5, 1.0, None)):
         res = []
-        for dev_loop in (False, True):
+        for dev_loop in (False, "require"):  # (require: fails rather than fall back to the host loop)
             ctx.set_solver(dev_loop)
             res.append(cf.descend(x0, limit, rate, 0.05, tol, div_, float(len(pts))))
         (xa, fa, ia), (xb, fb, ib) = res
@@ -77,7 +77,7 @@ def test_device_loop_bit_identical_to_host_loop(name, n):
             assert ib == 1 and np.array_equal(xb, x0)
             c, _ = cf.value_and_gradient(x0)
             assert fb == c / len(pts)
-    ctx.set_solver(True)
+    ctx.set_solver(False)
 
 
 def test_device_loop_refuses_bad_configuration():
@@ -89,7 +89,7 @@ def test_device_loop_refuses_bad_configuration():
     cf = CostFunctor(m, pts)
     bad = x0.copy()
     bad[13:17] = 0.0
-    for dev_loop in (False, True):
+    for dev_loop in (False, "require"):
         cf.ctx.set_solver(dev_loop)
         with pytest.raises(FlashNativeError):
             cf.descend(bad, 3, 1.0, 0.05, 0.0, None, float(len(pts)))
@@ -110,6 +110,7 @@ def test_auto_regroup_descend_matches_unregrouped(name):
     surf = m.surfaces
     ctx = m.engine(0, 64)
     ctx.set_mechanism(m.mechanism, [s.body for s in surf], [s.frame.R for s in surf], [s.frame.t for s in surf])
+    ctx.set_solver("require")
     out = {}
     for auto in (False, True):
         ctx.set_regroup(auto)
@@ -151,3 +152,21 @@ def test_regrouped_range_refuses_chunk_costs():
     ctx.set_points_range(pts, 0, 100032)
     ctx.eval(poses)
     ctx.chunk_costs()
+
+
+def test_device_loop_required_refuses_rbf_scene():
+    """fsdf_set_solver(2): an RBF scene cannot iterate on the device: refused
+    (FSDF_ERR_STATE) instead of silently running the host loop."""
+    from flash import Models
+    from flash._lib import FlashNativeError
+    from flash.gradientdescent import CostFunctor
+    m, x0 = Models.irb_and_squishable()
+    rng = np.random.default_rng(3)
+    pts = np.array([-0.1, -0.3, 0.55]) + rng.random((3000, 3)) * np.array([1.0, 1.0, 0.8])
+    cf = CostFunctor(m, pts)
+    cf.ctx.set_solver("require")
+    with pytest.raises(FlashNativeError):
+        cf.descend(np.asarray(x0, np.float64), 2, 1.0, 0.05, 0.0, None, float(len(pts)))
+    cf.ctx.set_solver(True)
+    x, f, its = cf.descend(np.asarray(x0, np.float64), 2, 1.0, 0.05, 0.0, None, float(len(pts)))
+    assert its == 2 and np.isfinite(f)

@@ -32,7 +32,7 @@ def run(args):
     surf = m.surfaces
     ctx.set_mechanism(m.mechanism, [s.body for s in surf], [s.frame.R for s in surf], [s.frame.t for s in surf])
     for dev_loop in (True, False):
-        ctx.set_solver(dev_loop)
+        ctx.set_solver("require" if dev_loop else False)
         ms = []
         for f in range(args.frames):
             t0 = time.perf_counter()
@@ -52,21 +52,24 @@ def trace(path):
         by.setdefault(name, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     for name, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
         print(f"{name:60s} {len(v):6d} x {statistics.mean(v):8.2f} us (median {statistics.median(v):.2f})")
-    steps = [r for r in rows if "solver_step_kernel" in r["Kernel_Name"]]
-    ends = [int(r["End_Timestamp"]) for r in steps]
-    spans = [(b - a) / 1e3 for a, b in zip(ends, ends[1:]) if 0 < b - a < 1e6]
+    steps = [i for i, r in enumerate(rows) if "solver_step_kernel" in r["Kernel_Name"]]
+    spans, busy = [], []
+    for i0, i1 in zip(steps, steps[1:]):
+        a, b = int(rows[i0]["End_Timestamp"]), int(rows[i1]["End_Timestamp"])
+        if not 0 < b - a < 1e6:
+            continue
+        spans.append((b - a) / 1e3)  # one iteration: after a step to the end of the next
+        busy.append(sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[i0 + 1:i1 + 1]) / 1e3)
     if spans:
-        print(f"device loop: step end -> next step end {statistics.median(spans):.2f} us median over {len(spans)}")
-    # the gaps inside an iteration: kernel starts after the previous kernel's end
-    gaps = []
-    for a, b in zip(rows, rows[1:]):
-        if "solver_step_kernel" in b["Kernel_Name"] or "pose_kernel<" in b["Kernel_Name"]:
-            g = (int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3
-            if 0 <= g < 100:
-                gaps.append((b["Kernel_Name"].split("(")[0][-30:], g))
-    for name in sorted({g[0] for g in gaps}):
-        v = [g[1] for g in gaps if g[0] == name]
-        print(f"gap before {name:30s} median {statistics.median(v):.2f} us")
+        print(f"device loop: iteration span {statistics.median(spans):.2f} us, kernels busy "
+              f"{statistics.median(busy):.2f} us, idle {statistics.median([s - b for s, b in zip(spans, busy)]):.2f} us "
+              f"(median over {len(spans)})")
+    # host loop: the iterations' pose -> pass -> reduce triplets (pose_kernel_args) and the gap before each pose
+    poses = [i for i, r in enumerate(rows) if "pose_kernel_args" in r["Kernel_Name"]]
+    gaps = [(int(rows[i]["Start_Timestamp"]) - int(rows[i - 1]["End_Timestamp"])) / 1e3 for i in poses if i > 0]
+    gaps = [g for g in gaps if 0 <= g < 1000]
+    if gaps:
+        print(f"host loop: idle before each iteration's pose kernel {statistics.median(gaps):.2f} us median")
 
 
 if __name__ == "__main__":

@@ -661,6 +661,52 @@ def main():
             torch.cuda.synchronize()
         allreduce_ms = (time.perf_counter() - t_ar) / args.steps * 1e3
 
+    # W > 1 spatial shards: the per-frame ingest, measured both ways on every rank
+    # (max over ranks, median of 3 after one warm-up), from pinned host memory:
+    # round 5's whole-cloud ranges (every rank uploads and sorts all N points,
+    # fsdf_set_points_range) and round 6's exchanged shards (each rank uploads
+    # its N/W slice; box all-reduce, keys, histogram splitters, one RCCL
+    # all-to-all, keyed sort: flash.distributed.exchange_points)
+    ingest = None
+    if world > 1 and bounds is not None:
+        from flash.distributed import exchange_points
+        a, b = shard_range(len(pts), rank, world)
+        whole = torch.empty((len(pts), 3), dtype=torch.float64, pin_memory=True)
+        whole.copy_(torch.from_numpy(np.ascontiguousarray(pts)))
+        cx = manip.engine(device=local, precision=args.precision, cull=not args.no_cull, sort_points=True, slot=CS)
+        cx.set_stream(torch.cuda.current_stream().cuda_stream)
+
+        def timed_max(fn, reps=4):
+            ts = []
+            for _ in range(reps):
+                dist.barrier()
+                torch.cuda.synchronize()
+                t_ = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                tt = torch.tensor([(time.perf_counter() - t_) * 1e3], dtype=torch.float64, device=dev)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                ts.append(float(tt.item()))
+            return float(np.median(ts[1:]))
+
+        counts = []
+
+        def exchange():
+            d_sl = whole[a:b].to(dev, non_blocking=True)
+            idx = torch.arange(a, b, dtype=torch.int64, device=dev)
+            counts.append(exchange_points([cx], d_sl, idx)[0])
+
+        ms_exchange = timed_max(exchange)
+        ms_range = timed_max(lambda: cx.set_points_range(whole.numpy(), *bounds[rank]))
+        nmax = torch.tensor([counts[-1]], dtype=torch.int64, device=dev)
+        dist.all_reduce(nmax, op=dist.ReduceOp.MAX)
+        ingest = {"exchange_ms": ms_exchange, "whole_cloud_range_ms": ms_range,
+                  "exchange_shard_points_max": int(nmax.item()), "slice_points": b - a,
+                  "note": "per-frame ingest from pinned host memory, max over ranks: exchanged shards (N/W upload per "
+                          "rank + box all-reduce + keys + histogram splitters + one all-to-all over the backend + "
+                          "keyed sort) vs whole-cloud ranges (every rank uploads and sorts all N points)"}
+        del whole
+
     weak = None
     if also_weak:
         del pts
@@ -766,6 +812,7 @@ def main():
                                         "memory + host wait, every step (a track! iteration's device latency; its "
                                         "host FK and chain rule are in full_iteration_ms)"),
                 "set_points_ms_per_frame": set_points_ms,
+                "ingest_per_frame": ingest,
                 "measured_frame": frame_rec,
                 "regroup_ms_per_frame": REGROUP_MS,
                 "regroup_note": ("fsdf_regroup_auto once per frame after its first passes (the library's rule: the pass "

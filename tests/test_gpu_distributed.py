@@ -191,8 +191,8 @@ def _nccl_worker(port, out_dir):
         x = np.asarray(qe, np.float64)
         xs = [x + 1e-3 * i for i in range(5)]
         out = {}
-        for spatial in (False, True):
-            f = ShardedCostFunctor(m, pts, rank=0, world=1, device=0, spatial=spatial)
+        for spatial in (0, 1, 2):  # slices, whole-cloud ranges, exchanged shards (one RCCL rank)
+            f = ShardedCostFunctor(m, pts, rank=0, world=1, device=0, spatial=spatial == 1, exchange=spatial == 2)
             many = f.value_and_gradient_many(xs)  # pass i+1 enqueued before the all-reduce of pass i is waited on
             one = [f.value_and_gradient(xi) for xi in xs]
             out[f"c_many{int(spatial)}"] = np.array([c for c, _ in many])
@@ -202,6 +202,8 @@ def _nccl_worker(port, out_dir):
             k, d, gr = f.per_point(x)
             out[f"k{int(spatial)}"], out[f"d{int(spatial)}"], out[f"gr{int(spatial)}"] = k, d, gr
             out[f"idx{int(spatial)}"] = f.global_index() if spatial else np.arange(len(pts))
+            if spatial == 2:  # exchange_points ran its box all-reduce over RCCL; the shard is the whole cloud
+                out["n_exchange"] = np.array([f.n_resident, f.cloud_n])
         out["backend"] = np.array(dist.get_backend())
         # the functor's all-reduce is a real RCCL collective here, not skipped for one rank
         from flash.distributed import allreduce_accum
@@ -220,8 +222,8 @@ def test_nccl_world1_pipelined(tmp_path):
     (two RCCL ranks cannot share a device): world size 1, the asynchronous
     all-reduce's work handle ordering the next pass and the read-back on the
     compute stream. Pipelined value_and_gradient_many equals one call per x bit
-    for bit, slices and spatial shards alike, and equals the unsharded
-    CostFunctor (cost / gradient to 1e-12, per-point outputs exactly)."""
+    for bit, slices, spatial shards and exchanged shards alike, and equals the
+    unsharded CostFunctor (cost / gradient to 1e-12, per-point outputs exactly)."""
     import multiprocessing as mp
     from flash import Models, synthetic
     from flash.gradientdescent import CostFunctor
@@ -239,7 +241,8 @@ def test_nccl_world1_pipelined(tmp_path):
     cf = CostFunctor(m, pts)
     want = [cf.value_and_gradient(x + 1e-3 * i) for i in range(5)]
     k1, d1, gr1 = cf.per_point(x)
-    for s in (0, 1):
+    assert np.array_equal(r["n_exchange"], [len(pts), len(pts)])
+    for s in (0, 1, 2):
         assert np.array_equal(r[f"c_many{s}"], r[f"c_one{s}"]) and np.array_equal(r[f"g_many{s}"], r[f"g_one{s}"])
         for i, (c, g) in enumerate(want):
             assert r[f"c_one{s}"][i] == pytest.approx(c, rel=1e-12)

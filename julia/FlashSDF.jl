@@ -149,6 +149,15 @@ the same per-point results and evaluate fewer hulls per 64-point chunk."
 regroup_points!(ctx::Context) = check(ctx.ptr, ccall((:fsdf_regroup_points, lib), Cint, (Ptr{Void},), ctx.ptr),
                                       "regroup_points")
 
+"The same where the library's rule says it pays (fsdf_regroup_auto: the last pass
+ran one wave per 64-point chunk — clouds above the planned window); true when it
+regrouped. GPUCost applies it after a new cloud's first evaluation."
+function regroup_auto!(ctx::Context)
+    applied = Ref{Int32}(0)
+    check(ctx.ptr, ccall((:fsdf_regroup_auto, lib), Cint, (Ptr{Void}, Ref{Int32}), ctx.ptr, applied), "regroup_auto")
+    applied[] != 0
+end
+
 "The posed scene in the state's number type (Float64 or Dual): per surface the
 world pose (R, t) (identity for RBF skins) and, per RBF skin, its world centres
 and solved coefficients u = (w; a; b)."
@@ -220,6 +229,7 @@ type GPUCost{P} <: Function
     memo_x::Vector{Float64}
     memo_accum::Vector{Float64}
     weight::Float64
+    fresh::Bool   # the resident cloud has not been evaluated yet (the regroup follows its first pass)
 end
 
 function GPUCost(manipulator::Manipulator, sensed_points::AbstractVector;
@@ -227,7 +237,7 @@ function GPUCost(manipulator::Manipulator, sensed_points::AbstractVector;
     ctx = Context(manipulator; device=device)
     set_points!(ctx, sensed_points)
     GPUCost(manipulator, ctx, Dict{DataType, ManipulatorState}(), Float64[], Float64[],
-            Float64(deformation_cost_weight))
+            Float64(deformation_cost_weight), true)
 end
 
 function state_for{T}(f::GPUCost, ::Type{T})
@@ -250,6 +260,10 @@ function residual_pass!(f::GPUCost, geo::SceneGeometry, xv::Vector{Float64})
                                (Ptr{Void}, Ptr{Float64}, Ref{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64},
                                 Ptr{Float64}),
                                f.ctx.ptr, poses, c, accum, C_NULL, C_NULL, C_NULL), "eval")
+        if f.fresh   # once per frame, after its first pass (per-point results unchanged, sums to rounding)
+            regroup_auto!(f.ctx)
+            f.fresh = false
+        end
         f.memo_x = copy(xv)
         f.memo_accum = accum
     end

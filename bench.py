@@ -16,17 +16,22 @@ labelled as such, the aggregate of two independent passes in flight
 (config.inflight_throughput).
 
 Sharding (contiguous point ranges, uploaded once per frame):
-  (default)           strong scaling of the metric's cloud: ONE 2^20-point M64
-                      cloud (the same seed on every rank) split into W spatial
+  (default)           weak scaling of the metric's cloud (`value`): every rank
+                      its own 2^20-point M64 cloud (rank r seeded seed+17(r+1);
+                      rank 0's is the N = 1 cloud), the 1+6S-double all-reduce
+                      every step — the path partitions into independent point
+                      ranges joined by that one collective. For W > 1 the strong
+                      figure is measured in the same run and reported beside it
+                      (`strong`): ONE 2^20-point cloud split into W spatial
                       shards — contiguous ranges of the whole cloud's Hilbert
                       order (fsdf_set_points_range), rebalanced after the settle
-                      to equal measured chunk time — `value`; for W > 1 the weak
-                      figure (2^20 points per GPU) is measured in the same run
-                      and reported beside it (`weak`)
-  --slice-shards      strong scaling over slices of the caller's order (A/B)
+                      to equal measured chunk time — with the per-frame ingest
+                      both ways (`config.ingest_per_frame`)
+  --slice-shards      the strong side figure over slices of the caller's order (A/B)
   --points P          weak scaling only: every rank owns its own P-point cloud
   --global-points G   strong scaling only, of a G-point cloud
-  --config c4         BASELINE config 4: IRB140, 10·2^20 points, strong scaling
+  --config c4         BASELINE config 4: IRB140, ONE 10·2^20-point cloud, strong
+                      scaling (`value`), the weak figure beside it (`weak`)
 For W > 1 the per-pass all-reduce is also timed on its own (`allreduce_ms`:
 host-synchronised all-reduces of the accumulator, mean over `steps`), and the
 backend that ran is named (`config.backend`).
@@ -77,10 +82,10 @@ TELEMETRY = {}  # device_telemetry() at the start and the end of the timed regio
 
 CONFIGS = {
     # name: (model, default points, scaling, description)
-    "m64": ("arm_grid", 1 << 20, "strong",
+    "m64": ("arm_grid", 1 << 20, "weak",
             "M64: 8 IRB140 arms (7 link hulls + ATI hull each) on a 2x4 grid, 64 convex hulls, 48 DOF; seeded "
             "synthetic depth cloud (SURVEY.md §8d generator G)"),
-    "c2": ("irb140", 1 << 20, "strong", "C2: IRB140 rigid model (7 hulls, 6 DOF), 2^20 synthetic points"),
+    "c2": ("irb140", 1 << 20, "weak", "C2: IRB140 rigid model (7 hulls, 6 DOF), 2^20 synthetic points"),
     "c4": ("irb140", 10 << 20, "strong", "C4: IRB140 rigid model, ONE 10*2^20-point cloud sharded over the GPUs"),
 }
 
@@ -325,8 +330,15 @@ def main():
         scaling = "strong"
     elif args.points is not None:
         scaling = "weak"
-    # W > 1 with the default workload: the weak figure is measured beside
-    also_weak = world > 1 and args.points is None and args.global_points is None and scaling == "strong"
+    # W > 1 with the default workload. M64 / C2 (the metric's 1M-point cloud):
+    # the headline is weak scaling — every rank its own 2^20-point cloud, the
+    # pass's per-DOF all-reduce over the backend every step — and the strong
+    # figure (ONE 2^20 cloud split into W spatial shards) is measured beside it;
+    # C4 (ONE 10*2^20 cloud over the GPUs) is strong by definition, the weak
+    # figure beside it
+    explicit = args.points is not None or args.global_points is not None
+    also_weak = world > 1 and not explicit and scaling == "strong"
+    also_strong = world > 1 and not explicit and scaling == "weak"
     manip = getattr(Models, model_name)()
     q_true, q_eval = synthetic.perturbed_configuration(manip, args.seed)
 
@@ -667,8 +679,7 @@ def main():
     # fsdf_set_points_range) and round 6's exchanged shards (each rank uploads
     # its N/W slice; box all-reduce, keys, histogram splitters, one RCCL
     # all-to-all, keyed sort: flash.distributed.exchange_points)
-    ingest = None
-    if world > 1 and bounds is not None:
+    def measure_ingest(pts):
         from flash.distributed import exchange_points
         a, b = shard_range(len(pts), rank, world)
         whole = torch.empty((len(pts), 3), dtype=torch.float64, pin_memory=True)
@@ -700,12 +711,15 @@ def main():
         ms_range = timed_max(lambda: cx.set_points_range(whole.numpy(), *bounds[rank]))
         nmax = torch.tensor([counts[-1]], dtype=torch.int64, device=dev)
         dist.all_reduce(nmax, op=dist.ReduceOp.MAX)
-        ingest = {"exchange_ms": ms_exchange, "whole_cloud_range_ms": ms_range,
+        rec = {"exchange_ms": ms_exchange, "whole_cloud_range_ms": ms_range,
                   "exchange_shard_points_max": int(nmax.item()), "slice_points": b - a,
                   "note": "per-frame ingest from pinned host memory, max over ranks: exchanged shards (N/W upload per "
                           "rank + box all-reduce + keys + histogram splitters + one all-to-all over the backend + "
                           "keyed sort) vs whole-cloud ranges (every rank uploads and sorts all N points)"}
         del whole
+        return rec
+
+    ingest = measure_ingest(pts) if world > 1 and bounds is not None else None
 
     weak = None
     if also_weak:
@@ -716,6 +730,24 @@ def main():
                 "global_points": default_points * world, "ms_per_step": w_elapsed / args.steps * 1e3,
                 "pass_ms": w_pass, "pass_kernel_ms": w_kernel,
                 "note": "weak scaling beside the strong value: every rank its own 2^20-point cloud"}
+
+    strong = None
+    if also_strong:
+        del pts
+        pts_s = strong_shard(default_points)  # (spatial: sets bounds; --slice-shards: this rank's slice)
+        s_elapsed, s_pass, s_kernel, s_set = run_cloud(pts_s, bounds)
+        n_s = torch.tensor([ctxs[0].n], dtype=torch.int64, device=dev)
+        dist.all_reduce(n_s, op=dist.ReduceOp.MAX)
+        strong = {"value": default_points * args.steps / s_elapsed, "global_points": default_points,
+                  "points_per_gpu_max": int(n_s.item()), "ms_per_step": s_elapsed / args.steps * 1e3,
+                  "pass_ms": s_pass, "pass_kernel_ms": s_kernel, "set_points_ms_per_frame": s_set,
+                  "partition": ("spatial: contiguous ranges of the whole cloud's Hilbert order (fsdf_set_points_range), "
+                                "rebalanced after the settle to equal measured chunk time" if bounds is not None else
+                                "slices of the caller's order"),
+                  "shard_bounds": bounds,
+                  "note": "strong scaling beside the weak value: ONE 2^20-point cloud split over the W ranks"}
+        if bounds is not None:
+            ingest = measure_ingest(pts_s)
 
     iter_ms = frame_rec = None
     if rank == 0 and world == 1 and not args.no_full_iteration:
@@ -780,11 +812,11 @@ def main():
                                 f"{ctx.accum_len} f64 per pass" if world > 1 else
                                 f"one GPU ({scaling} figure of the metric's cloud); at W > 1 one "
                                 f"{ctx.accum_len}-f64 all-reduce per pass"),
-                "partition": (None if world == 1 else
+                "partition": (None if world == 1 else "one cloud per rank" if scaling == "weak" else
                               "spatial: contiguous ranges of the whole cloud's Hilbert order (fsdf_set_points_range), "
                               "rebalanced after the settle to equal measured chunk time" if bounds is not None else
-                              "slices of the caller's order" if scaling == "strong" else "one cloud per rank"),
-                "shard_bounds": bounds,
+                              "slices of the caller's order"),
+                "shard_bounds": bounds if scaling == "strong" else None,
                 "backend": backend,
                 "allreduce_ms": allreduce_ms,
                 "allreduce_overlap": ("asynchronous all-reduce, two accumulators: step i+1's pass overlaps step "
@@ -853,6 +885,8 @@ def main():
         out["telemetry"] = TELEMETRY
         if weak is not None:
             out["weak"] = weak
+        if strong is not None:
+            out["strong"] = strong
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(manip, pts, q_eval, args.cpu_seconds)
         print(json.dumps(out), flush=True)

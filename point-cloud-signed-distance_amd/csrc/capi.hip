@@ -1693,8 +1693,25 @@ static int iteration_finish(fsdf_ctx* c, const double* x, const double* accum, d
   return FSDF_OK;
 }
 
+// diagnostic builds (-DFSDF_HOST_TIMES=1): host-side clocks of the host solver
+// loop's iterations — prepare (FK, poses), launches, the wait, the chain rule —
+// summed here and printed by fsdf_descend (stderr), to split the GPU's idle
+// gap between iterations into host work and synchronisation latency
+#if FSDF_HOST_TIMES
+#include <chrono>
+static double g_host_t[8];
+static long g_host_n;
+static inline double host_now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+#define HOST_STAMP(i) const double ht_##i = host_now_us()
+#else
+#define HOST_STAMP(i)
+#endif
+
 extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cost_out, double* grad_out) {
   if (!c) return FSDF_ERR_ARG;
+  HOST_STAMP(0);
   if (!x || !cost_out || !grad_out) return fail(c, FSDF_ERR_ARG, "value_and_gradient: null argument");
   int rc = iteration_prepare(c, x, "value_and_gradient");
   if (rc) return rc;
@@ -1705,12 +1722,24 @@ extern "C" int fsdf_value_and_gradient(fsdf_ctx* c, const double* x, double* cos
   if (rc) return rc;
   double* d_acc_host = nullptr;
   HIPCHECK(c, hipHostGetDevicePointer((void**)&d_acc_host, c->h_acc, 0));
+  HOST_STAMP(1);
   rc = run_pass(c, M.poses.data(), c->d_pts, c->n, d_acc_host, nullptr, nullptr, nullptr, nullptr, true);
   if (rc) return rc;
+  HOST_STAMP(2);
   rc = iteration_regroup(c);  // (stream-ordered after the pass: the sync below covers it)
   if (rc) return rc;
   HIPCHECK(c, hipStreamSynchronize(c->stream));
-  return iteration_finish(c, x, c->h_acc, cost_out, grad_out, "value_and_gradient");
+  HOST_STAMP(3);
+  rc = iteration_finish(c, x, c->h_acc, cost_out, grad_out, "value_and_gradient");
+#if FSDF_HOST_TIMES
+  HOST_STAMP(4);
+  g_host_t[0] += ht_1 - ht_0;  // prepare
+  g_host_t[1] += ht_2 - ht_1;  // pose + pass + reduce launches
+  g_host_t[2] += ht_3 - ht_2;  // wait (device work + wake-up)
+  g_host_t[3] += ht_4 - ht_3;  // chain rule
+  ++g_host_n;
+#endif
+  return rc;
 #else
   rc = run_pass(c, M.poses.data(), c->d_pts, c->n, c->d_accum, nullptr, nullptr, nullptr, nullptr, true);
   if (rc) return rc;
@@ -1977,6 +2006,11 @@ extern "C" int fsdf_descend(fsdf_ctx* c, double* x, int32_t iteration_limit, dou
   std::vector<double> g(ns);
   double f = 0.0;
   int it = 0;
+#if FSDF_HOST_TIMES
+  for (double& v : g_host_t) v = 0.0;
+  g_host_n = 0;
+  const double ht_start = host_now_us();
+#endif
   while (it < iteration_limit) {
     double cost = 0.0;
     const int rc = fsdf_value_and_gradient(c, x, &cost, g.data());
@@ -1994,6 +2028,13 @@ extern "C" int fsdf_descend(fsdf_ctx* c, double* x, int32_t iteration_limit, dou
     if (std::sqrt(nrm2) < tolerance) break;
     for (int i = 0; i < ns; ++i) x[i] = x[i] + std::min(std::max(-rate * g[i], -max_step), max_step);
   }
+#if FSDF_HOST_TIMES
+  if (g_host_n > 0) {
+    const double span = host_now_us() - ht_start, k = (double)g_host_n;
+    fprintf(stderr, "host loop per iteration (us): prepare %.2f launches %.2f wait %.2f chain %.2f total %.2f (%ld)\n",
+            g_host_t[0] / k, g_host_t[1] / k, g_host_t[2] / k, g_host_t[3] / k, span / k, g_host_n);
+  }
+#endif
   if (value_out) *value_out = f;
   return FSDF_OK;
 }

@@ -9,7 +9,13 @@ is bench.py's; these are the companion numbers DESIGN.md §7 reports).
       recorded squishable cloud tiled + G, flash.synthetic.c5_cloud), f32 vs f64
   M64 the metric model, for reference
 Each: one residual pass incl. the RBF parameter upload; mean pass-kernel time
-(HIP events) and whole-pass wall time over R passes; set_points once (sorted).
+(HIP events) and whole-pass wall time over R passes (the Python prepare_pass
+path); set_points once (sorted). Then the product's unit of work per config —
+a track! frame through the native solver loop (CostFunctor.descend =
+fsdf_descend: estimate_state's NaiveSolver rate 0.1, max_step 0.5, 30
+iterations, tolerance 0 so every frame runs all 30, src/tracking.jl:12-15) on
+the resident cloud: ms per iteration with the host loop and, for rigid scenes,
+the device loop (csrc/solver.hip), and tracking point-evals/s.
 
     python tools/bench_configs.py [--reps 20] [--json out.json]
 """
@@ -52,8 +58,37 @@ def run(name, m, x, pts, precision, reps):
     row = {"config": name, "points": len(pts), "surfaces": len(m.surfaces), "states": flash.num_states(m),
            "precision": precision, "pass_kernel_ms": kms, "evals_per_s_kernel": len(pts) / kms * 1e3,
            "pass_wall_ms_incl_host": wall * 1e3, "evals_per_s_wall": len(pts) / wall}
+    row.update(track_frame(m, x, pts, precision))
     print(json.dumps(row), flush=True)
     return row
+
+
+def track_frame(m, x, pts, precision, iters=30, frames=3):
+    """Median of `frames` native solver frames (after one untimed) on the
+    resident cloud: fsdf_descend with the host loop and, where the scene allows
+    it (rigid: no RBF skin, no deformation), the device loop."""
+    import statistics
+    from flash.gradientdescent import CostFunctor
+    from flash._lib import FlashNativeError
+    cf = CostFunctor(m, pts, precision=precision)
+    x0 = np.asarray(x, np.float64)
+    out = {}
+    for name, mode in (("host_loop", False), ("device_loop", "require")):
+        cf.ctx.set_solver(mode)
+        try:
+            cf.descend(x0, iters, 0.1, 0.5, 0.0, None, float(len(pts)))
+        except FlashNativeError:
+            continue  # (device loop: RBF scenes iterate on the host)
+        ts = []
+        for _ in range(frames):
+            t = time.perf_counter()
+            _, f, its = cf.descend(x0, iters, 0.1, 0.5, 0.0, None, float(len(pts)))
+            ts.append((time.perf_counter() - t) * 1e3)
+        ms = statistics.median(ts)
+        out[f"frame_{name}_ms_per_iteration"] = ms / its
+        out[f"frame_{name}_tracking_evals_per_s"] = len(pts) * its / (ms / 1e3)
+    cf.ctx.set_solver(False)
+    return out
 
 
 def main():

@@ -34,7 +34,13 @@ namespace fsdf {
 
 namespace {
 
+// kSolverBlock: the unit the staging capacities are counted in (kBlobPer /
+// kDynPer per thread of a 256-thread group); kStepThreads: the kernels'
+// width. 16 waves run the step's per-(body, component) loops in one round
+// (6 (nb - 1) = 384 for M64) and publish the 12 S pose entries in one round:
+// the M64 step 15.8 -> 12.6 us against 4 waves (profiles/r06/solver_nt/)
 constexpr int kSolverBlock = 256;
+constexpr int kStepThreads = 1024;
 
 #if FSDF_SOLVER_TIMES
 __device__ unsigned long long g_solver_times[64];
@@ -78,23 +84,26 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 constexpr int kBlobPer = 12;  // 16-B blob chunks per thread: blobs up to 48 KB
 constexpr int kDynPer = 8;    // dynamic doubles per thread (accum, Rb|tb, x, div): up to 2,048
 
+template <int NT>
 __device__ Lds stage(const SolverTree& T, const SolverState& st, double* lds, const double* accum) {
+  // (per-thread load counts for NT threads: the same totals as kBlobPer / kDynPer at kSolverBlock)
+  constexpr int BP = (kBlobPer * kSolverBlock + NT - 1) / NT, DP = (kDynPer * kSolverBlock + NT - 1) / NT;
   const int tid = threadIdx.x, nb = T.nb, nx = T.nx, S = T.S;
   typedef double D2 __attribute__((ext_vector_type(2)));
   // loads: blob chunks, then the dynamic doubles (a flat index over accum | Rb tb | x | div)
   const D2* blob = (const D2*)T.blob;
-  D2 bv[kBlobPer];
+  D2 bv[BP];
 #pragma unroll
-  for (int u = 0; u < kBlobPer; ++u) {
-    const int i = tid + u * kSolverBlock;
+  for (int u = 0; u < BP; ++u) {
+    const int i = tid + u * NT;
     bv[u] = i < T.chunks16 ? blob[i] : D2{0.0, 0.0};
   }
   const int na = accum ? 1 + 6 * S : 0, nr = accum ? 12 * nb : 0, nd_ = st.div ? nx : 0;
   const int ndyn = na + nr + nx + nd_;
-  double dv[kDynPer];
+  double dv[DP];
 #pragma unroll
-  for (int u = 0; u < kDynPer; ++u) {
-    const int i = tid + u * kSolverBlock;
+  for (int u = 0; u < DP; ++u) {
+    const int i = tid + u * NT;
     double v = 0.0;
     if (i < na) v = accum[i];
     else if (i < na + nr) v = st.Rb[i - na];  // (Rb | tb adjacent in the state buffer)
@@ -106,8 +115,8 @@ __device__ Lds stage(const SolverTree& T, const SolverState& st, double* lds, co
   double* d = lds;
   D2* l2 = (D2*)lds;
 #pragma unroll
-  for (int u = 0; u < kBlobPer; ++u) {
-    const int i = tid + u * kSolverBlock;
+  for (int u = 0; u < BP; ++u) {
+    const int i = tid + u * NT;
     if (i < T.chunks16) l2[i] = bv[u];
   }
   L.axis = d + T.axis;
@@ -157,12 +166,12 @@ __device__ Lds stage(const SolverTree& T, const SolverState& st, double* lds, co
   // the dynamic doubles land at acc (accum | Rb tb | x | div are contiguous
   // there too; without an accumulator x lands at L.x)
 #pragma unroll
-  for (int u = 0; u < kDynPer; ++u) {
-    const int i = tid + u * kSolverBlock;
+  for (int u = 0; u < DP; ++u) {
+    const int i = tid + u * NT;
     if (i < na + nr) L.acc[i] = dv[u];
     else if (i < ndyn) L.x[i - na - nr] = dv[u];
   }
-  for (int i = tid; i < nx; i += kSolverBlock) L.g[i] = 0.0;
+  for (int i = tid; i < nx; i += NT) L.g[i] = 0.0;
   return L;
 }
 
@@ -170,9 +179,10 @@ __device__ Lds stage(const SolverTree& T, const SolverState& st, double* lds, co
 // unknown joint). Global memory is not touched: a workgroup barrier after a
 // global store waits for the store to complete (its release fence), so every
 // store of the step is issued after the last barrier (publish()).
+template <int NT>
 __device__ void fk(const SolverTree& T, const Lds& L, int* bad) {
   const int tid = threadIdx.x, nb = T.nb;
-  for (int b = 1 + tid; b < nb; b += kSolverBlock) {
+  for (int b = 1 + tid; b < nb; b += NT) {
     const int k = L.kind[b];
     if (!kin::joint_local(k, L.axis + 3 * b, L.AR + 9 * b, L.At + 3 * b, L.BR + 9 * b, L.Bt + 3 * b,
                           L.x + (k ? L.qoff[b] : 0), L.LR + 9 * b, L.Lt + 3 * b))
@@ -194,14 +204,26 @@ __device__ void fk(const SolverTree& T, const Lds& L, int* bad) {
   // ancestor's product as the host's level order computes it: the same bits,
   // no barrier per level); the ancestors' R, t only, and the joint frame
   // Rb, tb = R_parent · joint_to_parent for b itself
-  for (int b = 1 + tid; b < nb; b += kSolverBlock) {
+  for (int b = 1 + tid; b < nb; b += NT) {
     double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, t[3] = {0, 0, 0}, v[12], w[12];
     const int q0 = L.poff[b], q1 = L.poff[b + 1];
+    // the next ancestor's joint motion is loaded while this one composes
+    double nLR[9], nLt[3];
+    int an = L.plist[q0];
+    kin::load(L.LR + 9 * an, nLR, 9);
+    kin::load(L.Lt + 3 * an, nLt, 3);
     for (int q = q0; q < q1; ++q) {
-      const int a = L.plist[q];
+      const int a = an;
       double LR[9], Lt[3];
-      kin::load(L.LR + 9 * a, LR, 9);
-      kin::load(L.Lt + 3 * a, Lt, 3);
+#pragma unroll
+      for (int e = 0; e < 9; ++e) LR[e] = nLR[e];
+#pragma unroll
+      for (int e = 0; e < 3; ++e) Lt[e] = nLt[e];
+      if (q + 1 < q1) {
+        an = L.plist[q + 1];
+        kin::load(L.LR + 9 * an, nLR, 9);
+        kin::load(L.Lt + 3 * an, nLt, 3);
+      }
       if (q == q1 - 1) {
         double AR[9], At[3];
         kin::load(L.AR + 9 * a, AR, 9);
@@ -228,11 +250,12 @@ __device__ void fk(const SolverTree& T, const Lds& L, int* bad) {
 // entry marks the frame failed, error 2), the joint frames for the next chain
 // rule, x, and — thread 0 — f, the iteration count and the done / error flags.
 // pose = false: the last iteration (no pass follows) publishes x and the flags only.
+template <int NT>
 __device__ void publish(const SolverTree& T, const SolverState& st, const Lds& L, bool pose, int bad, double f,
                         int it, int done) {
   const int tid = threadIdx.x, nb = T.nb;
   if (pose) {
-    for (int i = tid; i < 12 * T.S; i += kSolverBlock) {
+    for (int i = tid; i < 12 * T.S; i += NT) {
       const int k = i / 12, q = i % 12, b = L.sbody[k];
       const double v = b < 0 ? ((q % 4 == 0 && q < 9) ? 1.0 : 0.0)
                              : kin::surface_pose_entry(q, L.R + 9 * b, L.t + 3 * b, L.FR + 9 * k, L.Ft + 3 * k);
@@ -242,10 +265,10 @@ __device__ void publish(const SolverTree& T, const SolverState& st, const Lds& L
         st.flags[0] = 1;
       }
     }
-    for (int i = tid; i < 9 * nb; i += kSolverBlock) st.Rb[i] = L.Rb[i];
-    for (int i = tid; i < 3 * nb; i += kSolverBlock) st.tb[i] = L.tb[i];
+    for (int i = tid; i < 9 * nb; i += NT) st.Rb[i] = L.Rb[i];
+    for (int i = tid; i < 3 * nb; i += NT) st.tb[i] = L.tb[i];
   }
-  for (int i = tid; i < T.nx; i += kSolverBlock) st.x[i] = L.x[i];
+  for (int i = tid; i < T.nx; i += NT) st.x[i] = L.x[i];
   if (tid == 0) {
     *st.f = f;
     st.flags[1] = it;
@@ -256,22 +279,26 @@ __device__ void publish(const SolverTree& T, const SolverState& st, const Lds& L
   }
 }
 
-__global__ __launch_bounds__(kSolverBlock) void solver_init_kernel(SolverTree T, SolverState st) {
+__global__ __launch_bounds__(kStepThreads) void solver_init_kernel(SolverTree T, SolverState st) {
   extern __shared__ double lds[];
   __shared__ int bad;
   const int tid = threadIdx.x;
   if (tid == 0) bad = 0;
-  const Lds L = stage(T, st, lds, nullptr);
+  const Lds L = stage<kStepThreads>(T, st, lds, nullptr);
   __syncthreads();
-  fk(T, L, &bad);  // (ends with a barrier; the host zeroed the flags before this launch)
-  publish(T, st, L, true, bad, 0.0, 0, 0);
+  fk<kStepThreads>(T, L, &bad);  // (ends with a barrier; the host zeroed the flags before this launch)
+  publish<kStepThreads>(T, st, L, true, bad, 0.0, 0, 0);
 }
 
-__global__ __launch_bounds__(kSolverBlock) void solver_step_kernel(SolverTree T, SolverState st,
-                                                                   const double* __restrict__ accum) {
+// One step over NT threads (solver_step_kernel: kStepThreads). (A launch
+// that also did the pass's final reduce — its last workgroup running the step
+// — measured no faster: the hand-off between workgroups costs what the launch
+// saves; branch archive/fused-reduce-step)
+template <int NT>
+__device__ void step_body(const SolverTree& T, const SolverState& st, const double* __restrict__ accum,
+                          double* __restrict__ lds) {
   // (the frame's flags load with the stage's loads; the done check waits for them)
   const int done = __builtin_nontemporal_load(st.flags), it_before = __builtin_nontemporal_load(st.flags + 1);
-  extern __shared__ double lds[];
   __shared__ int bad, verdict;
   __shared__ double s_f;
   const int tid = threadIdx.x, nb = T.nb, nx = T.nx;
@@ -280,7 +307,7 @@ __global__ __launch_bounds__(kSolverBlock) void solver_step_kernel(SolverTree T,
 #endif
   STAMP(0);
   if (tid == 0) bad = 0;
-  const Lds L = stage(T, st, lds, accum);
+  const Lds L = stage<NT>(T, st, lds, accum);
   if (done) return;  // converged (or failed): the frame's remaining steps are no-ops (uniform)
   __syncthreads();
   STAMP(1);
@@ -288,23 +315,38 @@ __global__ __launch_bounds__(kSolverBlock) void solver_step_kernel(SolverTree T,
     // chains (every non-root body has <= 1 child): body b's subtree sum along
     // its chain, deepest first — sub[a] = own[a] + sub[child], own[a] the body's
     // surfaces summed in index order from 0.0: fsdf_config_gradient's additions
-    // in its order, in one thread per (b, component), no level barriers
-    for (int i = tid; i < 6 * (nb - 1); i += kSolverBlock) {
+    // in its order, no level barriers. First every own[a] (one thread per (a,
+    // component); into L.LR, free until the FK), then one thread per (b,
+    // component) walks its chain, the next four own[] loads issued before
+    // their additions (a chain level costs an addition, not a chain of
+    // dependent LDS loads)
+    double* own = L.LR;
+    for (int i = tid; i < 6 * (nb - 1); i += NT) {
+      const int a = 1 + i / 6, j = i % 6;
+      double o = 0.0;
+      for (int u = L.soff[a]; u < L.soff[a + 1]; ++u) o += L.acc[1 + 6 * L.slist[u] + j];
+      own[6 * a + j] = o;
+    }
+    __syncthreads();
+    for (int i = tid; i < 6 * (nb - 1); i += NT) {
       const int b = 1 + i / 6, j = i % 6;
-      const int q0 = L.choff[b], q1 = L.choff[b + 1];
-      double s = 0.0;
-      for (int q = q1 - 1; q >= q0; --q) {
-        const int a = L.chlist[q];
-        double o = 0.0;
-        for (int u = L.soff[a]; u < L.soff[a + 1]; ++u) o += L.acc[1 + 6 * L.slist[u] + j];
-        s = q == q1 - 1 ? o : o + s;
+      const int q0 = L.choff[b];
+      int q = L.choff[b + 1] - 1;
+      double s = own[6 * L.chlist[q] + j];
+      for (--q; q >= q0; q -= 4) {
+        double v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = q - k >= q0 ? own[6 * L.chlist[q - k] + j] : 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (q - k >= q0) s = v[k] + s;
       }
       L.sub[6 * b + j] = s;
     }
     __syncthreads();
   } else {
     // body wrenches: each body's surfaces in index order (fsdf_config_gradient)
-    for (int i = tid; i < 6 * nb; i += kSolverBlock) {
+    for (int i = tid; i < 6 * nb; i += NT) {
       const int b = i / 6, j = i - 6 * b;
       double s = 0.0;
       for (int q = L.soff[b]; q < L.soff[b + 1]; ++q) s += L.acc[1 + 6 * L.slist[q] + j];
@@ -332,7 +374,7 @@ __global__ __launch_bounds__(kSolverBlock) void solver_step_kernel(SolverTree T,
     } else {
       for (int h = 0; h < T.H; ++h) {
         const int a = L.hoff[h], e = L.hoff[h + 1];
-        for (int i = tid; i < 6 * (e - a); i += kSolverBlock) {
+        for (int i = tid; i < 6 * (e - a); i += NT) {
           const int p = L.hord[a + i / 6], j = i % 6;
           double s = L.sub[6 * p + j];
           for (int q = L.coff[p]; q < L.coff[p + 1]; ++q) s += L.sub[6 * L.clist[q] + j];
@@ -343,14 +385,14 @@ __global__ __launch_bounds__(kSolverBlock) void solver_step_kernel(SolverTree T,
     }
   }
   STAMP(2);
-  for (int b = 1 + tid; b < nb; b += kSolverBlock) {
+  for (int b = 1 + tid; b < nb; b += NT) {
     const int k = L.kind[b];
     if (k && !kin::joint_gradient(k, L.axis + 3 * b, L.Rb + 9 * b, L.tb + 3 * b, L.x + L.qoff[b], L.sub + 6 * b,
                                   L.g + L.qoff[b]))
       atomicOr(&bad, 1);
   }
   __syncthreads();
-  for (int i = tid; i < nx; i += kSolverBlock) {
+  for (int i = tid; i < nx; i += NT) {
     double gi = L.g[i] / st.n_points;
     if (L.div) gi = gi / L.div[i];
     L.g[i] = gi;
@@ -380,21 +422,27 @@ __global__ __launch_bounds__(kSolverBlock) void solver_step_kernel(SolverTree T,
   const int v = verdict;
   const double f = s_f;
   if (v == 3 || v == 1) {  // failed / converged: x stays
-    publish(T, st, L, false, v == 3, f, it, 1);
+    publish<NT>(T, st, L, false, v == 3, f, it, 1);
     return;
   }
-  for (int i = tid; i < nx; i += kSolverBlock) L.x[i] = L.x[i] + kin::clipped_step(st.rate, L.g[i], st.max_step);
+  for (int i = tid; i < nx; i += NT) L.x[i] = L.x[i] + kin::clipped_step(st.rate, L.g[i], st.max_step);
   if (v == 2) {  // the last iteration: no pass follows
     __syncthreads();
-    publish(T, st, L, false, 0, f, it, 1);
+    publish<NT>(T, st, L, false, 0, f, it, 1);
     return;
   }
   __syncthreads();
   STAMP(4);
-  fk(T, L, &bad);  // (ends with a barrier)
+  fk<NT>(T, L, &bad);  // (ends with a barrier)
   STAMP(6);
-  publish(T, st, L, true, bad, f, it, 0);
+  publish<NT>(T, st, L, true, bad, f, it, 0);
   STAMP(9);
+}
+
+__global__ __launch_bounds__(kStepThreads) void solver_step_kernel(SolverTree T, SolverState st,
+                                                                   const double* __restrict__ accum) {
+  extern __shared__ double lds[];
+  step_body<kStepThreads>(T, st, accum, lds);
 }
 
 size_t solver_lds_bytes(const SolverTree& T) {
@@ -413,7 +461,7 @@ bool solver_fits(int nb, int nx, int S, int ni) {
 }
 
 hipError_t launch_solver_init(const SolverTree& T, const SolverState& st, hipStream_t s) {
-  hipLaunchKernelGGL(solver_init_kernel, dim3(1), dim3(kSolverBlock), solver_lds_bytes(T), s, T, st);
+  hipLaunchKernelGGL(solver_init_kernel, dim3(1), dim3(kStepThreads), solver_lds_bytes(T), s, T, st);
   return hipGetLastError();
 }
 
@@ -426,8 +474,9 @@ void solver_times(unsigned long long* out) {
 }
 
 hipError_t launch_solver_step(const SolverTree& T, const SolverState& st, const double* d_accum, hipStream_t s) {
-  hipLaunchKernelGGL(solver_step_kernel, dim3(1), dim3(kSolverBlock), solver_lds_bytes(T), s, T, st, d_accum);
+  hipLaunchKernelGGL(solver_step_kernel, dim3(1), dim3(kStepThreads), solver_lds_bytes(T), s, T, st, d_accum);
   return hipGetLastError();
 }
+
 
 }  // namespace fsdf

@@ -52,7 +52,8 @@ def trace(path):
         by.setdefault(name, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     for name, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
         print(f"{name:60s} {len(v):6d} x {statistics.mean(v):8.2f} us (median {statistics.median(v):.2f})")
-    steps = [i for i, r in enumerate(rows) if "solver_step_kernel" in r["Kernel_Name"]]
+    # (the step: solver_step_kernel, or the reduce + step kernel of FSDF_FUSED_STEP builds)
+    steps = [i for i, r in enumerate(rows) if "step_kernel" in r["Kernel_Name"]]
     spans, busy = [], []
     for i0, i1 in zip(steps, steps[1:]):
         a, b = int(rows[i0]["End_Timestamp"]), int(rows[i1]["End_Timestamp"])

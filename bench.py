@@ -108,6 +108,14 @@ def parse():
                    help="N = 1: after the timed region, also measure the aggregate throughput of this many "
                         "independent passes in flight (config.inflight_throughput; 0 = skip). Not the headline: "
                         "only independent configurations (line-search trials, several hypotheses) can overlap")
+    p.add_argument("--accum-ring", type=int, default=2,
+                   help="W > 1: accumulators per context in the timed loop (rounded up to even); a buffer is "
+                        "reused only after its previous all-reduce completed, so a deeper ring leaves the pass "
+                        "stream fewer waits on the collective stream")
+    p.add_argument("--collective", default="torch", choices=("torch", "rccl"),
+                   help="W > 1: the per-step all-reduce through torch.distributed (its own collective stream, "
+                        "asynchronous, ordered by events) or RCCL itself in order on the pass's stream "
+                        "(flash.distributed.RcclComm)")
     p.add_argument("--config", default="m64", choices=sorted(CONFIGS))
     g = p.add_mutually_exclusive_group()
     g.add_argument("--points", type=int, default=None, help="points per GPU (weak scaling)")
@@ -317,8 +325,13 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group(os.environ.get("FSDF_BENCH_BACKEND", "nccl"))
+    elif os.environ.get("FSDF_BENCH_GROUP_AT_1"):
+        # rehearsal of the W > 1 step loop on one GPU: an RCCL group of one rank,
+        # so the timed steps take the grouped path (stream switch + asynchronous
+        # all-reduce every step) and show its host cost against the device's
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29633", rank=0, world_size=1)
     dev = torch.device("cuda", local)
-    backend = dist.get_backend() if world > 1 else None
+    backend = dist.get_backend() if dist.is_initialized() else None
 
     import flash
     from flash import Models, synthetic
@@ -379,6 +392,11 @@ def main():
     # is made torch's current stream, so the collectives and timing events order
     # after it
     streams = [torch.cuda.Stream(dev) for _ in range(CS)]
+    stream_handles = [st_.cuda_stream for st_ in streams]
+    RCCL = None
+    if args.collective == "rccl" and dist.is_initialized():
+        from flash.distributed import RcclComm
+        RCCL = RcclComm()
     torch.cuda.set_stream(streams[0])
     stream = streams[0]
     for c, cx in enumerate(ctxs):
@@ -386,7 +404,8 @@ def main():
         cx.set_stream(streams[c].cuda_stream)
     ctx = ctxs[0]
     # two accumulators per context (the all-reduce of one overlaps the next pass)
-    accums = [[torch.zeros(ctx.accum_len, dtype=torch.float64, device=dev) for _ in range(2)] for _ in range(CS)]
+    RING = max(2, args.accum_ring + (args.accum_ring & 1))  # (even: a buffer always holds one configuration)
+    accums = [[torch.zeros(ctx.accum_len, dtype=torch.float64, device=dev) for _ in range(RING)] for _ in range(CS)]
     h_acc = torch.empty(ctx.accum_len, dtype=torch.float64, pin_memory=True)
     accum = accums[0][0]
 
@@ -436,33 +455,38 @@ def main():
         # context's stream — step i+1's pass runs while step i's collective is
         # in flight (flash/distributed.py); a buffer is reused only after its
         # previous collective completed
-        pending = [[None, None] for _ in range(CS)]
+        pending = [[None] * RING for _ in range(CS)]
 
         # (no process group — N = 1: no collective to order, and every context
         # is bound to its own stream by set_stream, so the step is the library
         # call alone; torch's stream switch cost ~5 us of host time per step,
         # enough to starve the device between 0.1 ms passes)
-        acc_ptrs = [[accums[c][s_].data_ptr() for s_ in (0, 1)] for c in range(CS)]
+        acc_ptrs = [[accums[c][r_].data_ptr() for r_ in range(RING)] for c in range(CS)]
         grouped = dist.is_available() and dist.is_initialized()
+        alen = ctx.accum_len
 
         def step(i, nctx=C):
-            c, s_ = i % nctx, (i // nctx) & 1
+            c, s_, r_ = i % nctx, (i // nctx) & 1, (i // nctx) % RING
             if not grouped:
-                ctxs[c].eval_device(poses[s_], acc_ptrs[c][s_], *outs[c])
+                ctxs[c].eval_device(poses[s_], acc_ptrs[c][r_], *outs[c])
+                return
+            if RCCL is not None:  # in order on the context's stream: no waits, no events
+                ctxs[c].eval_device(poses[s_], acc_ptrs[c][r_], *outs[c])
+                RCCL.allreduce(acc_ptrs[c][r_], alen, stream_handles[c])
                 return
             with torch.cuda.stream(streams[c]):
-                if pending[c][s_] is not None:
-                    pending[c][s_].wait()
-                ctxs[c].eval_device(poses[s_], acc_ptrs[c][s_], *outs[c])
-                pending[c][s_] = allreduce_accum(accums[c][s_], async_op=True)
+                if pending[c][r_] is not None:
+                    pending[c][r_].wait()
+                ctxs[c].eval_device(poses[s_], acc_ptrs[c][r_], *outs[c])
+                pending[c][r_] = allreduce_accum(accums[c][r_], async_op=True)
 
         def drain():
             for c in range(CS):
-                for s_ in (0, 1):
-                    if pending[c][s_] is not None:
+                for r_ in range(RING):
+                    if pending[c][r_] is not None:
                         with torch.cuda.stream(streams[c]):
-                            pending[c][s_].wait()
-                        pending[c][s_] = None
+                            pending[c][r_].wait()
+                        pending[c][r_] = None
 
         def join(nctx=C):  # the first context's stream waits for every other context's stream
             for st in streams[1:nctx]:
@@ -818,9 +842,12 @@ def main():
                               "slices of the caller's order"),
                 "shard_bounds": bounds if scaling == "strong" else None,
                 "backend": backend,
+                "grouped_at_one_rank": (world == 1 and backend is not None) or None,
                 "allreduce_ms": allreduce_ms,
                 "allreduce_overlap": ("asynchronous all-reduce, two accumulators: step i+1's pass overlaps step "
                                       "i's collective" if world > 1 else None),
+                "accum_ring": RING if (world > 1 or backend) else None,
+                "collective": (args.collective if backend else None),
                 "inflight": C,
                 "inflight_note": (f"{C} independent passes in flight: {C} contexts over the same resident cloud, each on "
                                   f"its own HIP stream, step i on context i % {C} (two configurations alternate); every "
@@ -890,7 +917,9 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(manip, pts, q_eval, args.cpu_seconds)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if RCCL is not None:
+        RCCL.close()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -209,6 +209,61 @@ def allreduce_accum(accum, group=None, async_op=False):
     return None if async_op else accum
 
 
+class RcclComm:
+    """A communicator of RCCL itself (the librccl torch loads), whose sum
+    all-reduce is enqueued on a HIP stream the caller names — in order with
+    the pass on that stream, no collective stream and no cross-stream events
+    (torch's ProcessGroupNCCL runs every collective on a stream of its own,
+    ordered by an event each way). Built collectively over the process
+    group: rank 0's ncclGetUniqueId is broadcast, every rank joins with
+    ncclCommInitRank (the current HIP device)."""
+
+    _lib = None
+
+    @classmethod
+    def _load(cls):
+        if cls._lib is None:
+            import ctypes
+            import os
+            import torch
+            lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
+            cls._Uid = type("ncclUniqueId", (ctypes.Structure,), {"_fields_": [("internal", ctypes.c_char * 128)]})
+            lib.ncclGetUniqueId.argtypes = [ctypes.POINTER(cls._Uid)]
+            lib.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, cls._Uid, ctypes.c_int]
+            lib.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_void_p, ctypes.c_void_p]
+            lib.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+            for f in ("ncclGetUniqueId", "ncclCommInitRank", "ncclAllReduce", "ncclCommDestroy"):
+                getattr(lib, f).restype = ctypes.c_int
+            cls._lib = lib
+        return cls._lib
+
+    def __init__(self, group=None):
+        import ctypes
+        import torch.distributed as dist
+        lib = self._load()
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        uid = self._Uid()
+        if rank == 0 and lib.ncclGetUniqueId(ctypes.byref(uid)) != 0:
+            raise RuntimeError("ncclGetUniqueId failed")
+        box = [bytes(uid.internal) if rank == 0 else None]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        uid.internal = box[0]
+        self.comm = ctypes.c_void_p()
+        if lib.ncclCommInitRank(ctypes.byref(self.comm), world, uid, rank) != 0:
+            raise RuntimeError("ncclCommInitRank failed")
+
+    def allreduce(self, ptr: int, count: int, stream: int) -> None:
+        """In-place sum of `count` f64 at device pointer `ptr`, on HIP stream `stream` (0: the null stream)."""
+        if self._lib.ncclAllReduce(ptr, ptr, count, 8, 0, self.comm, stream) != 0:  # ncclFloat64, ncclSum
+            raise RuntimeError("ncclAllReduce failed")
+
+    def close(self) -> None:
+        if self.comm:
+            self._lib.ncclCommDestroy(self.comm)
+            self.comm = None
+
+
 def chain_gradient(manip: Manipulator, x: np.ndarray, accum: np.ndarray, weight, solves=()) -> np.ndarray:
     """∂c/∂x from an (all-reduced) accumulator (see gradientdescent.gradient_from_accum)."""
     return gradient_from_accum(manip, np.asarray(x, np.float64), np.asarray(accum), list(solves), weight)

@@ -275,7 +275,7 @@ class ShardedCostFunctor:
     def __init__(self, manipulator: Manipulator, local_points, rank: int = 0, world: int = 1, device: int = 0,
                  precision: int = 64, group=None, deformation_cost_weight=default_deformation_cost_weight,
                  engine=None, inflight: int = 1, spatial: bool = False, bounds=None, exchange: bool = False,
-                 index_offset: int | None = None):
+                 index_offset: int | None = None, collective: str = "torch"):
         """engine: an already-built context-like object to drive instead of
         manipulator.engine(device, precision) — with engine.device_type == "cpu"
         the accumulator lives in host memory and no HIP stream is used (the CPU
@@ -296,7 +296,12 @@ class ShardedCostFunctor:
         its first point, default: the slices concatenated in rank order) and
         exchange_points() moves every point to the rank whose key range holds it
         (per-point outputs and global_index() as for spatial shards;
-        set_sensed_points() swaps a new frame's slice in the same way)."""
+        set_sensed_points() swaps a new frame's slice in the same way).
+        collective = "rccl" (HIP contexts over an RCCL group): each pass's
+        all-reduce is RCCL itself, in order on the pass's stream (RcclComm) —
+        no collective stream, no events; "torch" (default): torch.distributed's
+        asynchronous all_reduce (profiles/r06/collective/). close() releases
+        the RCCL communicator."""
         import contextlib
         import torch
         self.torch = torch
@@ -310,6 +315,11 @@ class ShardedCostFunctor:
         pts = torch.as_tensor(np.ascontiguousarray(local_points, np.float64).reshape(-1, 3), device=self.dev)
         self._pts = pts  # the context reads the resident copy (set_points_device does not own it)
         self.rank, self.world, self.spatial, self.exchange = rank, world, spatial and not exchange, exchange
+        if collective not in ("torch", "rccl"):
+            raise ValueError(f"collective: 'torch' or 'rccl', not {collective!r}")
+        if collective == "rccl" and on_host:
+            raise ValueError("collective='rccl' needs a HIP context")
+        self._rccl = RcclComm(group) if collective == "rccl" else None
         self._index_offset = index_offset
         if exchange:
             self._exchange(pts)
@@ -443,7 +453,11 @@ class ShardedCostFunctor:
                 poses, self._solves = prepare_pass(ctx, self.manipulator, self.state.q,
                                                    self.state.deformation_data)
                 ctx.eval_device(poses, acc.data_ptr())
-            work = allreduce_accum(acc, self.group, async_op=True)
+            if self._rccl is not None:  # in order on this stream: nothing to wait for later
+                self._rccl.allreduce(acc.data_ptr(), acc.numel(), self.streams[slot % len(self.streams)].cuda_stream)
+                work = None
+            else:
+                work = allreduce_accum(acc, self.group, async_op=True)
         self._pending[slot] = work
         self.accum = acc
         return slot, work
@@ -525,8 +539,18 @@ class ShardedCostFunctor:
         self._slot, self.accum = 0, self.accums[0]
         with self._on_stream(0):
             self.ctx.eval_device(poses, self.accum.data_ptr(), k.data_ptr(), d.data_ptr(), g.data_ptr())
-            allreduce_accum(self.accum, self.group)
+            if self._rccl is not None:
+                self._rccl.allreduce(self.accum.data_ptr(), self.accum.numel(), self.streams[0].cuda_stream)
+            else:
+                allreduce_accum(self.accum, self.group)
             return k[:n].cpu().numpy(), d[:n].cpu().numpy(), g[:n].cpu().numpy()
+
+    def close(self):
+        """Release the RCCL communicator (collective='rccl'); before the process group is destroyed."""
+        if self._rccl is not None:
+            self._sync(0)
+            self._rccl.close()
+            self._rccl = None
 
     def value_and_gradient(self, x):
         x = np.asarray(x, np.float64)

@@ -204,6 +204,13 @@ def _nccl_worker(port, out_dir):
             out[f"idx{int(spatial)}"] = f.global_index() if spatial else np.arange(len(pts))
             if spatial == 2:  # exchange_points ran its box all-reduce over RCCL; the shard is the whole cloud
                 out["n_exchange"] = np.array([f.n_resident, f.cloud_n])
+        # RCCL in order on the functor's stream (collective="rccl"): the same bits
+        f = ShardedCostFunctor(m, pts, rank=0, world=1, device=0, collective="rccl")
+        many = f.value_and_gradient_many(xs)
+        one = [f.value_and_gradient(xi) for xi in xs]
+        out["c_rccl"] = np.array([c for c, _ in many] + [c for c, _ in one])
+        out["g_rccl"] = np.array([g for _, g in many] + [g for _, g in one])
+        f.close()
         out["backend"] = np.array(dist.get_backend())
         # the functor's all-reduce is a real RCCL collective here, not skipped for one rank
         from flash.distributed import allreduce_accum
@@ -212,6 +219,17 @@ def _nccl_worker(port, out_dir):
         out["work"] = np.array(work is not None)
         work.wait()
         out["probe"] = probe.cpu().numpy()
+        # RCCL itself on a stream of ours (flash.distributed.RcclComm, bench.py --collective rccl)
+        from flash.distributed import RcclComm
+        comm = RcclComm()
+        s = torch.cuda.Stream()
+        v = torch.arange(385, dtype=torch.float64, device="cuda") * 0.5
+        with torch.cuda.stream(s):
+            v.mul_(2.0)  # (ordered before the collective on the same stream)
+            comm.allreduce(v.data_ptr(), v.numel(), s.cuda_stream)
+        s.synchronize()
+        comm.close()
+        out["rccl"] = v.cpu().numpy()
         np.savez(os.path.join(out_dir, "nccl.npz"), **out)
     finally:
         dist.destroy_process_group()
@@ -234,6 +252,9 @@ def test_nccl_world1_pipelined(tmp_path):
     assert p.exitcode == 0
     r = dict(np.load(os.path.join(tmp_path, "nccl.npz")))
     assert str(r["backend"]) == "nccl" and bool(r["work"]) and np.array_equal(r["probe"], np.ones(3))
+    assert np.array_equal(r["rccl"], np.arange(385, dtype=np.float64))
+    assert np.array_equal(r["c_rccl"], np.concatenate([r["c_many0"], r["c_one0"]]))
+    assert np.array_equal(r["g_rccl"], np.concatenate([r["g_many0"], r["g_one0"]]))
     m = Models.arm_grid()
     qt, qe = synthetic.perturbed_configuration(m, 65)
     pts = synthetic.depth_cloud(m, qt, 200003, seed=66, order="shuffled")

@@ -259,6 +259,16 @@ int fsdf_set_rbf_params(fsdf_ctx* ctx, const double* params, int64_t n_doubles);
 int fsdf_set_points(fsdf_ctx* ctx, const double* xyz, int64_t n);
 /* Same, from a device-resident AoS buffer (copied device-to-device). */
 int fsdf_set_points_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n);
+/* The next frame's cloud ahead of time (a frame loop over recorded or queued
+ * clouds, src/gradientdescent.jl:43 once per frame): fsdf_prefetch_points
+ * starts its host-to-device copy on a stream of the context's own and returns
+ * at once, so the copy runs during the current frame's passes (overlapped from
+ * page-locked memory; the caller keeps xyz unchanged until the next call
+ * below returns; a second prefetch replaces a pending one);
+ * fsdf_set_points_prefetched then makes it resident as fsdf_set_points would
+ * (FSDF_ERR_STATE when nothing is pending). */
+int fsdf_prefetch_points(fsdf_ctx* ctx, const double* xyz, int64_t n);
+int fsdf_set_points_prefetched(fsdf_ctx* ctx);
 /* One rank's shard of a cloud split over several devices (the
  * cost is a plain sum over points, src/gradientdescent.jl:32): the whole
  * n-point cloud is uploaded and ordered (the Hilbert order with sort_points,

@@ -24,6 +24,10 @@
 #include "fsdf_internal.h"
 #include "kin_impl.h"
 
+#ifndef FSDF_POSE_OVERLAP
+#define FSDF_POSE_OVERLAP 0  // (pose_model: measured slower, off)
+#endif
+
 namespace {
 
 constexpr int kPoseRing = 8;
@@ -122,6 +126,11 @@ struct fsdf_ctx {
   fsdf::SortScratch sort;            // per-frame sort scratch (grown only)
   double* d_staging = nullptr;       // host-source clouds land here first
   int64_t staging_cap = 0;
+  // the next frame's cloud, copied ahead on a stream of its own (fsdf_prefetch_points)
+  double* d_prefetch = nullptr;
+  int64_t prefetch_cap = 0, prefetch_n = -1;  // -1: none pending
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t ev_prefetch = nullptr;
   bool ranged = false;               // the resident cloud is a range of a larger one (fsdf_set_points_range)
   void* d_range_pts = nullptr;       // fsdf_set_points_range: the whole cloud, sorted (scratch)
   int32_t* d_range_perm = nullptr;
@@ -294,8 +303,20 @@ extern "C" int fsdf_create(fsdf_ctx** out, const fsdf_opts* opts) {
     return FSDF_ERR_HIP;
   }
   c->stream = c->own_stream;
+  // the prefetch copy stream right after the context stream: HIP hands out its
+  // hardware queues round robin by stream creation, so the two land on
+  // different queues (on a shared one the copy would serialise with the passes)
+  if (hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_prefetch, hipEventDisableTiming) != hipSuccess) {
+    (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return FSDF_ERR_HIP;
+  }
   for (int i = 0; i < kPoseRing; ++i) c->pose_ev[i] = nullptr;
-  if (hipStreamCreateWithFlags(&c->pose_stream, hipStreamNonBlocking) != hipSuccess ||
+  // (the pose stream only where the pose overlap is built in: every stream of a
+  // process shares its few hardware queues — GPU_MAX_HW_QUEUES, 4 by default —
+  // and a stream sharing the context stream's queue serialises with it)
+  if ((FSDF_POSE_OVERLAP && hipStreamCreateWithFlags(&c->pose_stream, hipStreamNonBlocking) != hipSuccess) ||
       hipEventCreateWithFlags(&c->ev_pose, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_pm_free[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_pm_free[1], hipEventDisableTiming) != hipSuccess) {
@@ -312,12 +333,16 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->pose_stream) (void)hipStreamSynchronize(c->pose_stream);
+  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
   free_model(c);
   dfree(c->d_pts);
   dfree(c->d_perm);
   dfree(c->d_chunk_ws);
   dfree(c->d_prior);
   dfree(c->d_staging);
+  dfree(c->d_prefetch);
+  if (c->ev_prefetch) (void)hipEventDestroy(c->ev_prefetch);
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   dfree(c->d_range_pts);
   dfree(c->d_range_perm);
   fsdf::free_sort_scratch(c->sort);
@@ -955,6 +980,45 @@ extern "C" int fsdf_set_points_device(fsdf_ctx* c, const double* d_xyz, int64_t 
   return set_points_impl(c, d_xyz, n, true, 0, n);
 }
 
+// The next frame's cloud ahead of time: its host-to-device copy runs on a
+// stream of the context's own while the current frame's passes run on the
+// context stream (the copy engine beside the compute units), and
+// fsdf_set_points_prefetched then makes it resident from the device copy —
+// the per-frame ingest loses its host-link transfer (25 MB at 2^20 points).
+// The copy overlaps only from page-locked host memory; the caller keeps xyz
+// unchanged until fsdf_set_points_prefetched returns. A second prefetch
+// replaces a pending one.
+extern "C" int fsdf_prefetch_points(fsdf_ctx* c, const double* xyz, int64_t n) {
+  if (!c) return FSDF_ERR_ARG;
+  if (n < 0 || (n > 0 && !xyz)) return fail(c, FSDF_ERR_ARG, "prefetch_points: bad buffer (n=%lld)", (long long)n);
+  HIPCHECK(c, hipSetDevice(c->device));
+  // (an earlier prefetch's copy may still write the buffer; a consumed one's
+  // sort has finished: fsdf_set_points_prefetched returns after it)
+  HIPCHECK(c, hipStreamSynchronize(c->copy_stream));
+  if (c->prefetch_cap < n) {
+    dfree(c->d_prefetch);
+    c->prefetch_cap = 0;
+    HIPCHECK(c, hipMalloc(&c->d_prefetch, (size_t)n * 3 * sizeof(double)));
+    c->prefetch_cap = n;
+  }
+  if (n > 0)
+    HIPCHECK(c, hipMemcpyAsync(c->d_prefetch, xyz, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice,
+                               c->copy_stream));
+  HIPCHECK(c, hipEventRecord(c->ev_prefetch, c->copy_stream));
+  c->prefetch_n = n;
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_set_points_prefetched(fsdf_ctx* c) {
+  if (!c) return FSDF_ERR_ARG;
+  if (c->prefetch_n < 0) return fail(c, FSDF_ERR_STATE, "set_points_prefetched: no prefetch pending");
+  const int64_t n = c->prefetch_n;
+  c->prefetch_n = -1;
+  HIPCHECK(c, hipSetDevice(c->device));
+  HIPCHECK(c, hipStreamWaitEvent(c->stream, c->ev_prefetch, 0));  // the sort reads the copy
+  return set_points_impl(c, c->d_prefetch, n, true, 0, n);
+}
+
 extern "C" int fsdf_set_points_range(fsdf_ctx* c, const double* xyz, int64_t n, int64_t begin, int64_t end) {
   return set_points_impl(c, xyz, n, false, begin, end, true);
 }
@@ -1054,9 +1118,6 @@ static int upload_poses(fsdf_ctx* c, const double* poses, hipStream_t st) {
   return FSDF_OK;
 }
 
-#ifndef FSDF_POSE_OVERLAP
-#define FSDF_POSE_OVERLAP 0
-#endif
 // Pose the model for one pass into the next posed buffer. With
 // FSDF_POSE_OVERLAP the upload and pose kernel run on the context's pose
 // stream — behind the last reader of that buffer (two passes back), ahead of

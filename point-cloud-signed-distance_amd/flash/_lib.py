@@ -63,6 +63,8 @@ _PROTOS = {
     "fsdf_set_rbf_params": (c_int32, [c_void_p, c_void_p, c_int64]),
     "fsdf_set_points": (c_int32, [c_void_p, c_void_p, c_int64]),
     "fsdf_set_points_device": (c_int32, [c_void_p, c_void_p, c_int64]),
+    "fsdf_prefetch_points": (c_int32, [c_void_p, c_void_p, c_int64]),
+    "fsdf_set_points_prefetched": (c_int32, [c_void_p]),
     "fsdf_set_points_range": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_int64]),
     "fsdf_set_points_range_device": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_int64]),
     "fsdf_regroup_points": (c_int32, [c_void_p]),
@@ -245,6 +247,20 @@ class Context:
     def set_points_device(self, dev_ptr: int, n: int):
         check(self._lib.fsdf_set_points_device(self._ctx, c_void_p(dev_ptr), n), self._ctx, "set_points_device")
         self.n = n
+
+    def prefetch_points(self, xyz: np.ndarray):
+        """Start the next frame's upload (fsdf_prefetch_points: a copy on the
+        context's own stream, overlapping the current frame's passes when `xyz`
+        is page-locked); set_points_prefetched() makes it resident. The array is
+        held until then (the copy reads it)."""
+        pts = np.ascontiguousarray(xyz, np.float64).reshape(-1, 3)
+        check(self._lib.fsdf_prefetch_points(self._ctx, ptr(pts), pts.shape[0]), self._ctx, "prefetch_points")
+        self._prefetched = pts
+
+    def set_points_prefetched(self):
+        check(self._lib.fsdf_set_points_prefetched(self._ctx), self._ctx, "set_points_prefetched")
+        self.n = self._prefetched.shape[0]
+        self._prefetched = None
 
     def set_points_range(self, xyz: np.ndarray, begin: int, end: int):
         """One shard of a cloud split over devices (fsdf_set_points_range):

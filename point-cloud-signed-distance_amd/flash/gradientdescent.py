@@ -134,10 +134,26 @@ class CostFunctor:
 
     def set_sensed_points(self, sensed_points):
         """Swap the resident cloud (a new frame): one upload + device sort; the
-        functor, its state and the device model are kept."""
-        self.sensed_points = np.ascontiguousarray(sensed_points, np.float64).reshape(-1, 3)
-        self.ctx.set_points(self.sensed_points)
+        functor, its state and the device model are kept. The array given to
+        prefetch_sensed_points last is made resident from its device copy."""
+        pre, src = getattr(self, "_prefetched", None), getattr(self, "_prefetched_src", None)
+        self._prefetched = self._prefetched_src = None
+        if pre is not None and sensed_points is src:  # (the object prefetched: its device copy)
+            self.sensed_points = pre
+            self.ctx.set_points_prefetched()
+        else:
+            self.sensed_points = np.ascontiguousarray(sensed_points, np.float64).reshape(-1, 3)
+            self.ctx.set_points(self.sensed_points)
         self.manipulator._resident_cloud = self._resident
+
+    def prefetch_sensed_points(self, sensed_points):
+        """Start the NEXT frame's upload now (fsdf_prefetch_points: a copy on a
+        stream of the context's own, running under the current frame's passes —
+        fully when the array is page-locked); set_sensed_points(that array)
+        then skips the host-to-device copy. The array must not change until then."""
+        self._prefetched = np.ascontiguousarray(sensed_points, np.float64).reshape(-1, 3)
+        self._prefetched_src = sensed_points
+        self.ctx.prefetch_points(self._prefetched)
 
     def regroup(self):
         """Once per frame, after its first evaluation: regroup the resident

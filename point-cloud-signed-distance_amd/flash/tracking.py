@@ -135,11 +135,15 @@ class Tracker:
         self.set_points_ms: list[float] = []
         self.iterations: list[int] = []
 
-    def step(self, sensed_points, callback=None) -> np.ndarray:
-        """gradient_descent!(state, model, sensed_points): one frame."""
+    def step(self, sensed_points, callback=None, next_points=None) -> np.ndarray:
+        """gradient_descent!(state, model, sensed_points): one frame.
+        next_points (optional): the next frame's cloud, whose upload then runs
+        under this frame's solver iterations (CostFunctor.prefetch_sensed_points)."""
         pts = np.asarray(sensed_points, np.float64).reshape(-1, 3)
         t0 = time.perf_counter()
-        self.cost.set_sensed_points(pts)
+        self.cost.set_sensed_points(sensed_points)  # (the object itself: a prefetched frame is matched by identity)
+        if next_points is not None:
+            self.cost.prefetch_sensed_points(next_points)
         t1 = time.perf_counter()
         x = _optimize(self.cost, len(pts), flatten(self.state), callback, self.solver)
         unflatten(self.state, x)
@@ -161,5 +165,11 @@ def track(manipulator: Manipulator, frames, state: ManipulatorState | None = Non
     (examples/irb_and_squishable.ipynb cells 11-12). `frames` yields sensed
     clouds ([n,3]); returns (the per-frame solutions [F, n_states], the Tracker)."""
     tr = Tracker(manipulator, state, solver, device, precision)
-    xs = [tr.step(f, callback) for f in frames]
+    xs = []
+    it = iter(frames)
+    cur = next(it, None)
+    while cur is not None:
+        nxt = next(it, None)  # (its upload overlaps this frame's iterations)
+        xs.append(tr.step(cur, callback, next_points=nxt))
+        cur = nxt
     return np.array(xs), tr

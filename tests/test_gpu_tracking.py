@@ -153,3 +153,48 @@ def test_native_descend_matches_python_loop(scene):
     c, g = cf.value_and_gradient(x0)
     assert its == 1 and f1 == c / len(pts)
     assert np.array_equal(x1, x0 + np.clip(-5.0 * (g / len(pts)), -0.05, 0.05))
+
+
+def test_prefetched_frames_same_bits():
+    """track() uploads frame t+1 during frame t's iterations
+    (fsdf_prefetch_points on the context's copy stream, fsdf_set_points_prefetched):
+    the per-frame solutions equal a Tracker.step loop without prefetch bit for
+    bit (native solver loop). The ABI refuses set_points_prefetched with nothing
+    pending, a second prefetch replaces the first, and a page-locked cloud
+    becomes resident exactly as fsdf_set_points makes it."""
+    import torch
+    import flash
+    from flash import Models
+    from flash._lib import FlashNativeError
+    from flash.tracking import NaiveSolver, Tracker, track
+    m = Models.irb140()
+    qs, clouds = _sequence(m, frames=5, n=20000, seed=90)
+    n = flash.num_states(m)
+    out = []
+    for prefetch in (True, False):
+        state = flash.ManipulatorState(m)
+        state.q[:] = qs[0] + 0.03
+        solver = NaiveSolver(n, rate=20.0, max_step=0.1, iteration_limit=10)
+        if prefetch:
+            xs, _ = track(m, clouds, state=state, solver=solver)
+        else:
+            tr = Tracker(m, state, solver)
+            xs = np.array([tr.step(c) for c in clouds])
+        out.append(xs)
+    assert np.array_equal(out[0], out[1])
+    ctx, ref = m.engine(0, 64, slot=5), m.engine(0, 64, slot=6)
+    poses = flash.hull_poses(m, qs[2])
+    with pytest.raises(FlashNativeError):
+        ctx.set_points_prefetched()
+    pinned = torch.empty((len(clouds[3]), 3), dtype=torch.float64, pin_memory=True)
+    pinned.copy_(torch.from_numpy(clouds[3]))
+    ctx.prefetch_points(clouds[1])
+    ctx.prefetch_points(pinned.numpy())  # replaces the pending prefetch
+    ctx.set_points_prefetched()
+    ref.set_points(clouds[3])
+    assert ctx.n == ref.n == len(clouds[3])
+    (c0, a0, (k0, d0, g0)), (c1, a1, (k1, d1, g1)) = ctx.eval(poses, True), ref.eval(poses, True)
+    assert c0 == c1 and np.array_equal(a0, a1)
+    assert np.array_equal(k0, k1) and np.array_equal(d0, d1) and np.array_equal(g0, g1)
+    with pytest.raises(FlashNativeError):  # consumed
+        ctx.set_points_prefetched()

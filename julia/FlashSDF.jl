@@ -91,7 +91,9 @@ type Context
     manipulator::Manipulator
     S::Int
     accum_len::Int
+    prefetched::Any   # the cloud fsdf_prefetch_points is copying (rooted until consumed)
 end
+Context(ptr, manip, S, accum_len) = Context(ptr, manip, S, accum_len, nothing)
 
 function Context(manip::Manipulator; device::Integer=0, precision::Integer=64, sort_points::Bool=true)
     ref = Ref{Ptr{Void}}(C_NULL)
@@ -130,6 +132,22 @@ function set_points!{T}(ctx::Context, pts::AbstractVector{SVector{3, T}})
     P = convert(Vector{SVector{3, Float64}}, pts)
     check(ctx.ptr, ccall((:fsdf_set_points, lib), Cint, (Ptr{Void}, Ptr{Float64}, Int64),
                          ctx.ptr, reinterpret(Float64, P), length(P)), "set_points")
+end
+
+"Start the NEXT frame's upload now (fsdf_prefetch_points: a copy on the context's
+own stream, under the current frame's iterations — overlapped when the buffer is
+page-locked); set_points_prefetched! makes it resident. The buffer is rooted in the
+context until then and must not change."
+function prefetch_points!{T}(ctx::Context, pts::AbstractVector{SVector{3, T}})
+    P = convert(Vector{SVector{3, Float64}}, pts)
+    check(ctx.ptr, ccall((:fsdf_prefetch_points, lib), Cint, (Ptr{Void}, Ptr{Float64}, Int64),
+                         ctx.ptr, reinterpret(Float64, P), length(P)), "prefetch_points")
+    ctx.prefetched = P
+end
+
+function set_points_prefetched!(ctx::Context)
+    check(ctx.ptr, ccall((:fsdf_set_points_prefetched, lib), Cint, (Ptr{Void},), ctx.ptr), "set_points_prefetched")
+    ctx.prefetched = nothing
 end
 
 "One GPU's shard of the frame's cloud (the cost is a sum over points,

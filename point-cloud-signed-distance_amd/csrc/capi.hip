@@ -129,6 +129,13 @@ struct fsdf_ctx {
   // the next frame's cloud, copied ahead on a stream of its own (fsdf_prefetch_points)
   double* d_prefetch = nullptr;
   int64_t prefetch_cap = 0, prefetch_n = -1;  // -1: none pending
+  // ... and its resident form, sorted there too (swapped in by fsdf_set_points_prefetched)
+  bool prefetch_sorted = false;
+  void* d_pts_next = nullptr;
+  int32_t* d_perm_next = nullptr;
+  float* d_chunk_ws_next = nullptr;
+  int64_t pts_cap_next = 0, perm_cap_next = 0, chunk_ws_cap_next = 0;
+  fsdf::SortScratch sort_next;
   hipStream_t copy_stream = nullptr;
   hipEvent_t ev_prefetch = nullptr;
   bool ranged = false;               // the resident cloud is a range of a larger one (fsdf_set_points_range)
@@ -341,6 +348,10 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   dfree(c->d_prior);
   dfree(c->d_staging);
   dfree(c->d_prefetch);
+  dfree(c->d_pts_next);
+  dfree(c->d_perm_next);
+  dfree(c->d_chunk_ws_next);
+  fsdf::free_sort_scratch(c->sort_next);
   if (c->ev_prefetch) (void)hipEventDestroy(c->ev_prefetch);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   dfree(c->d_range_pts);
@@ -771,7 +782,7 @@ static int adopt_points_device(fsdf_ctx* c, const double* d_src, int64_t n, void
   return FSDF_OK;
 }
 
-static int finish_resident(fsdf_ctx* c, int64_t n, bool ranged);
+static int finish_resident(fsdf_ctx* c, int64_t n, bool ranged, bool spheres_done = false);
 
 // [begin, end): the resident cloud is that range of the whole cloud's order
 // (the Hilbert order of all n points with sort_points, else the caller's);
@@ -868,9 +879,10 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
 }
 
 // the per-cloud state of a new resident cloud of n points (d_pts / d_perm
-// written, stream-ordered): chunk spheres, seed buffer, plan and regroup state
-static int finish_resident(fsdf_ctx* c, int64_t n, bool ranged) {
-  if (n > 0) {  // per-chunk bounding spheres of the resident order (pose-independent)
+// written, stream-ordered): chunk spheres (unless spheres_done: a prefetched
+// cloud's came with it), seed buffer, plan and regroup state
+static int finish_resident(fsdf_ctx* c, int64_t n, bool ranged, bool spheres_done) {
+  if (n > 0 && !spheres_done) {  // per-chunk bounding spheres of the resident order (pose-independent)
     // (padded to whole 4-chunk pass workgroups: every wave of a hull-partitioned
     // pass reads its chunk's row, also past the cloud's end)
     const int64_t nc = ((n + 63) / 64 + 3) & ~(int64_t)3;
@@ -882,6 +894,8 @@ static int finish_resident(fsdf_ctx* c, int64_t n, bool ranged) {
       c->chunk_ws_cap = nc;
     }
     HIPCHECK(c, fsdf::launch_chunk_spheres(c->precision, c->d_pts, n, nc, c->d_chunk_ws, c->stream));
+  }
+  if (n > 0) {
     if (c->prior_cap < n) {  // (the previous frame's passes are done: synchronised above)
       dfree(c->d_prior);
       c->prior_cap = 0;
@@ -1004,6 +1018,37 @@ extern "C" int fsdf_prefetch_points(fsdf_ctx* c, const double* xyz, int64_t n) {
   if (n > 0)
     HIPCHECK(c, hipMemcpyAsync(c->d_prefetch, xyz, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice,
                                c->copy_stream));
+  // the next resident cloud, Hilbert-sorted on the copy stream as well (its own
+  // buffers and sort scratch: the current frame's cloud is untouched), so the
+  // next frame's set_points_prefetched only swaps buffers
+  c->prefetch_sorted = false;
+  if (n > 0 && c->sort_points && n <= INT32_MAX) {
+    const size_t tsz = c->precision == 64 ? sizeof(double) : sizeof(float);
+    const int64_t nc = ((n + 63) / 64 + 3) & ~(int64_t)3;  // (finish_resident's padding)
+    if (c->pts_cap_next < n) {
+      dfree(c->d_pts_next);
+      c->pts_cap_next = 0;
+      HIPCHECK(c, hipMalloc(&c->d_pts_next, (size_t)n * 3 * tsz));
+      c->pts_cap_next = n;
+    }
+    if (c->perm_cap_next < n) {
+      dfree(c->d_perm_next);
+      c->perm_cap_next = 0;
+      HIPCHECK(c, hipMalloc(&c->d_perm_next, (size_t)n * sizeof(int32_t)));
+      c->perm_cap_next = n;
+    }
+    if (c->chunk_ws_cap_next < nc) {
+      dfree(c->d_chunk_ws_next);
+      c->chunk_ws_cap_next = 0;
+      HIPCHECK(c, hipMalloc(&c->d_chunk_ws_next, (size_t)nc * 4 * sizeof(float)));
+      c->chunk_ws_cap_next = nc;
+    }
+    hipError_t e = fsdf::sort_points_spatial(c->d_prefetch, n, c->precision, c->d_pts_next, c->d_perm_next,
+                                             c->sort_next, c->copy_stream);
+    if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "prefetch_points (sort): %s", hipGetErrorString(e));
+    HIPCHECK(c, fsdf::launch_chunk_spheres(c->precision, c->d_pts_next, n, nc, c->d_chunk_ws_next, c->copy_stream));
+    c->prefetch_sorted = true;
+  }
   HIPCHECK(c, hipEventRecord(c->ev_prefetch, c->copy_stream));
   c->prefetch_n = n;
   return FSDF_OK;
@@ -1015,8 +1060,19 @@ extern "C" int fsdf_set_points_prefetched(fsdf_ctx* c) {
   const int64_t n = c->prefetch_n;
   c->prefetch_n = -1;
   HIPCHECK(c, hipSetDevice(c->device));
-  HIPCHECK(c, hipStreamWaitEvent(c->stream, c->ev_prefetch, 0));  // the sort reads the copy
-  return set_points_impl(c, c->d_prefetch, n, true, 0, n);
+  HIPCHECK(c, hipStreamWaitEvent(c->stream, c->ev_prefetch, 0));  // (the copy, and the sort when done there)
+  if (!c->prefetch_sorted) return set_points_impl(c, c->d_prefetch, n, true, 0, n);
+  // the sorted next cloud becomes resident: the current frame's work is done
+  // (synchronised), its buffers become the next prefetch's
+  HIPCHECK(c, hipStreamSynchronize(c->stream));
+  c->n = 0;
+  std::swap(c->d_pts, c->d_pts_next);
+  std::swap(c->pts_cap, c->pts_cap_next);
+  std::swap(c->d_perm, c->d_perm_next);
+  std::swap(c->perm_cap, c->perm_cap_next);
+  std::swap(c->d_chunk_ws, c->d_chunk_ws_next);
+  std::swap(c->chunk_ws_cap, c->chunk_ws_cap_next);
+  return finish_resident(c, n, false, true);
 }
 
 extern "C" int fsdf_set_points_range(fsdf_ctx* c, const double* xyz, int64_t n, int64_t begin, int64_t end) {

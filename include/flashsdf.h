@@ -266,7 +266,10 @@ int fsdf_set_points_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n);
  * page-locked memory; the caller keeps xyz unchanged until the next call
  * below returns; a second prefetch replaces a pending one);
  * fsdf_set_points_prefetched then makes it resident as fsdf_set_points would
- * (FSDF_ERR_STATE when nothing is pending). */
+ * (FSDF_ERR_STATE when nothing is pending). A sorting context also Hilbert-
+ * sorts the prefetched cloud on that stream, into a second resident buffer set,
+ * so fsdf_set_points_prefetched only swaps buffers. fsdf_set_points meanwhile
+ * leaves a pending prefetch pending. */
 int fsdf_prefetch_points(fsdf_ctx* ctx, const double* xyz, int64_t n);
 int fsdf_set_points_prefetched(fsdf_ctx* ctx);
 /* One rank's shard of a cloud split over several devices (the

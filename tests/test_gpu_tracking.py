@@ -198,3 +198,41 @@ def test_prefetched_frames_same_bits():
     assert np.array_equal(k0, k1) and np.array_equal(d0, d1) and np.array_equal(g0, g1)
     with pytest.raises(FlashNativeError):  # consumed
         ctx.set_points_prefetched()
+
+
+@pytest.mark.parametrize("sort_points", [True, False])
+def test_prefetch_edge_cases(sort_points):
+    """fsdf_prefetch_points with an unsorted context (consumed through the
+    plain device ingest), an empty cloud, and a plain set_points between a
+    prefetch and its consumption (the prefetched cloud still becomes resident,
+    then the next frame's buffers are swapped back and forth): every resident
+    cloud evaluates exactly as fsdf_set_points makes it."""
+    import flash
+    from flash import Models
+    m = Models.irb140()
+    qs, clouds = _sequence(m, frames=4, n=30000, seed=95)
+    poses = flash.hull_poses(m, qs[1])
+    ctx = m.engine(0, 64, sort_points=sort_points, slot=7)
+    ref = m.engine(0, 64, sort_points=sort_points, slot=8)
+
+    def same(pts):
+        ref.set_points(pts)
+        assert ctx.n == ref.n == len(pts)
+        (c0, a0, p0), (c1, a1, p1) = ctx.eval(poses, True), ref.eval(poses, True)
+        assert c0 == c1 and np.array_equal(a0, a1)
+        for u, v in zip(p0, p1):
+            assert np.array_equal(u, v)
+
+    ctx.prefetch_points(np.zeros((0, 3)))
+    ctx.set_points_prefetched()
+    assert ctx.n == 0
+    ctx.prefetch_points(clouds[0])
+    ctx.set_points(clouds[1])  # (does not consume the prefetch)
+    same(clouds[1])
+    ctx.set_points_prefetched()
+    same(clouds[0])
+    for t in (2, 3, 0):  # buffers swapped back and forth
+        ctx.prefetch_points(clouds[t])
+        ctx.eval(poses)  # (a pass of the current frame while the next one is copied)
+        ctx.set_points_prefetched()
+        same(clouds[t])

@@ -1182,19 +1182,16 @@ static int upload_poses(fsdf_ctx* c, const double* poses, hipStream_t st) {
 // buffer index to release with release_posed() after its last reader.
 // Measured: the cross-stream event waits cost more than the overlap saves
 // (+10 us per step on M64), so it is off and the pose kernel runs in order.
-// d_poses_dev (optional): the poses are already on the device (the device
-// solver loop writes them, solver.hip); skip: its done flag.
-static int pose_model(fsdf_ctx* c, const double* poses, fsdf::PosedModel** out, int* buf,
-                      const double* d_poses_dev = nullptr, const int* skip = nullptr) {
+// posed: the model is already posed on the device (the device solver loop's
+// step poses the next pass's model itself, solver.hip): no pose launch.
+static int pose_model(fsdf_ctx* c, const double* poses, fsdf::PosedModel** out, int* buf, bool posed = false) {
   const int b = FSDF_POSE_OVERLAP ? c->pm_next : 0;
   c->pm_next ^= FSDF_POSE_OVERLAP ? 1 : 0;
   fsdf::PosedModel* P = b ? &c->pm_alt : &c->pm;
   P->rbf_rows = c->pm.rbf_rows;  // per-pass RBF rows: one buffer, context-stream ordered
   const hipStream_t ps = FSDF_POSE_OVERLAP ? c->pose_stream : c->stream;
   if (FSDF_POSE_OVERLAP) HIPCHECK(c, hipStreamWaitEvent(ps, c->ev_pm_free[b], 0));
-  if (d_poses_dev) {
-    HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, d_poses_dev, *P, ps, nullptr, skip));
-  } else {
+  if (!posed) {
     int rc = upload_poses(c, poses, ps);
     if (rc) return rc;
     HIPCHECK(c, fsdf::launch_pose(c->precision, c->lm, c->d_poses, *P, ps,
@@ -1328,15 +1325,16 @@ static int run_planned(fsdf_ctx* c, const fsdf::PosedModel& P, const void* d_pts
 #endif
 // schedule: resident-cloud passes (repeated over the same cloud) launch their
 // workgroups heaviest-first by the previous pass's durations
-// d_poses_dev / skip: the device solver loop's poses and done flag (pose_model)
+// posed / skip: the device solver loop's pass — its model posed by the
+// previous step (pose_model), its done flag
 static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t n, double* d_accum,
                     int32_t* d_kstar, double* d_d, double* d_grad, const int32_t* d_perm, bool schedule,
-                    const double* d_poses_dev = nullptr, const int* skip = nullptr) {
+                    bool posed = false, const int* skip = nullptr) {
   if (c->lm.R > 0 && !c->rbf_ready)
     return fail(c, FSDF_ERR_STATE, "eval: the scene has RBF surfaces: call fsdf_set_rbf_params first");
   fsdf::PosedModel* P = nullptr;
   int pbuf = 0;
-  int rc = pose_model(c, poses, &P, &pbuf, d_poses_dev, skip);
+  int rc = pose_model(c, poses, &P, &pbuf, posed);
   if (rc) return rc;
   const bool resident = d_pts == c->d_pts && n == c->n;
   const int nblocks = fsdf::pass_blocks(n, c->lm);
@@ -2004,14 +2002,14 @@ static int descend_device(fsdf_ctx* c, double* x, int32_t iteration_limit, doubl
                           double tolerance, const double* divisors, double n_points, double* value_out,
                           int32_t* iterations_out) {
   auto& M = c->mech;
-  const int nx = M.nq, nb = M.nb, S = c->lm.S;
+  const int nx = M.nq, nb = M.nb;
   HIPCHECK(c, hipSetDevice(c->device));
   if (!c->solver_tree_ok) {
     const int rc = build_solver_tree(c);
     if (rc) return rc;
   }
-  // device: x [nx] | div [nx] | Rb [9 nb] | tb [3 nb] | poses [12 S] | f; flags [4] int
-  const size_t need = (size_t)2 * nx + 12 * (size_t)nb + 12 * (size_t)S + 1;
+  // device: x [2][nx] (slots by iteration parity) | div [nx] | Rb|tb [2][12 nb] | f; flags [4] int
+  const size_t need = (size_t)3 * nx + 24 * (size_t)nb + 1;
   if (c->solver_cap < need) {
     HIPCHECK(c, hipStreamSynchronize(c->stream));
     dfree(c->d_solver);
@@ -2020,8 +2018,8 @@ static int descend_device(fsdf_ctx* c, double* x, int32_t iteration_limit, doubl
     c->solver_cap = need;
   }
   if (!c->d_solver_flags) HIPCHECK(c, hipMalloc(&c->d_solver_flags, 4 * sizeof(int)));
-  // pinned: x [nx] | div [nx] | f | flags [4] (as 2 doubles)
-  const size_t hneed = (size_t)2 * nx + 3;
+  // pinned: x [2][nx] | div [nx] | f | flags [4] (as 2 doubles)
+  const size_t hneed = (size_t)3 * nx + 3;
   if (c->h_solver_cap < hneed) {
     if (c->h_solver) HIPCHECK(c, hipHostFree(c->h_solver));
     c->h_solver = nullptr;
@@ -2031,17 +2029,15 @@ static int descend_device(fsdf_ctx* c, double* x, int32_t iteration_limit, doubl
   }
   double* h = c->h_solver;
   HIPCHECK(c, hipStreamSynchronize(c->stream));  // (the pinned staging of an earlier frame is free)
-  memcpy(h, x, (size_t)nx * sizeof(double));
-  if (divisors) memcpy(h + nx, divisors, (size_t)nx * sizeof(double));
-  HIPCHECK(c, hipMemcpyAsync(c->d_solver, h, (size_t)(divisors ? 2 : 1) * nx * sizeof(double),
+  memcpy(h, x, (size_t)nx * sizeof(double));  // (slot 0)
+  if (divisors) memcpy(h + 2 * nx, divisors, (size_t)nx * sizeof(double));
+  HIPCHECK(c, hipMemcpyAsync(c->d_solver, h, (size_t)(divisors ? 3 : 1) * nx * sizeof(double),
                              hipMemcpyHostToDevice, c->stream));
   fsdf::SolverState st;
   st.x = c->d_solver;
-  st.div = divisors ? c->d_solver + nx : nullptr;
-  st.Rb = c->d_solver + 2 * nx;
-  st.tb = st.Rb + 9 * nb;
-  st.poses = st.tb + 3 * nb;
-  st.f = st.poses + 12 * S;
+  st.div = divisors ? c->d_solver + 2 * nx : nullptr;
+  st.Rb = c->d_solver + 3 * nx;
+  st.f = st.Rb + 24 * nb;
   st.flags = c->d_solver_flags;
   st.rate = rate;
   st.max_step = max_step;
@@ -2050,23 +2046,33 @@ static int descend_device(fsdf_ctx* c, double* x, int32_t iteration_limit, doubl
   st.weight = M.weight;
   st.limit = iteration_limit;
   HIPCHECK(c, hipMemsetAsync(c->d_solver_flags, 0, 4 * sizeof(int), c->stream));
-  HIPCHECK(c, fsdf::launch_solver_init(c->stree, st, c->stream));
+  // (the init and every step pose the next pass's model themselves: the
+  // passes below launch no pose kernel; FSDF_POSE_OVERLAP is off, c->pm is
+  // the one posed model)
+  HIPCHECK(c, fsdf::launch_solver_init(c->stree, st, c->lm, c->pm, c->precision, c->stream));
+  HOST_STAMP(0);
   for (int it = 0; it < iteration_limit; ++it) {
-    int rc = run_pass(c, nullptr, c->d_pts, c->n, c->d_accum, nullptr, nullptr, nullptr, nullptr, true, st.poses,
+    int rc = run_pass(c, nullptr, c->d_pts, c->n, c->d_accum, nullptr, nullptr, nullptr, nullptr, true, true,
                       st.flags);
     if (rc) return rc;
     if (it == 0) {
       rc = iteration_regroup(c);
       if (rc) return rc;
     }
-    HIPCHECK(c, fsdf::launch_solver_step(c->stree, st, c->d_accum, c->stream));
+    HIPCHECK(c, fsdf::launch_solver_step(c->stree, st, c->d_accum, c->lm, c->pm, c->precision, it, c->stream));
   }
-  HIPCHECK(c, hipMemcpyAsync(h, st.x, (size_t)nx * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HIPCHECK(c, hipMemcpyAsync(h + 2 * nx, st.f, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HIPCHECK(c, hipMemcpyAsync(h + 2 * nx + 1, st.flags, 4 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HOST_STAMP(1);
+  HIPCHECK(c, hipMemcpyAsync(h, st.x, (size_t)2 * nx * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(c, hipMemcpyAsync(h + 3 * nx, st.f, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(c, hipMemcpyAsync(h + 3 * nx + 1, st.flags, 4 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(c, hipStreamSynchronize(c->stream));
+#if FSDF_HOST_TIMES
+  HOST_STAMP(2);
+  fprintf(stderr, "device loop: enqueue %.1f us (%d iterations), then wait %.1f us\n", ht_1 - ht_0, iteration_limit,
+          ht_2 - ht_1);
+#endif
   int flags[4];
-  memcpy(flags, h + 2 * nx + 1, sizeof flags);
+  memcpy(flags, h + 3 * nx + 1, sizeof flags);
 #ifdef FSDF_SOLVER_TIMES
   {
     unsigned long long tt[16];
@@ -2076,11 +2082,11 @@ static int descend_device(fsdf_ctx* c, double* x, int32_t iteration_limit, doubl
     fprintf(stderr, "\n");
   }
 #endif
-  memcpy(x, h, (size_t)nx * sizeof(double));
+  memcpy(x, h + (size_t)(flags[1] & 1) * nx, (size_t)nx * sizeof(double));  // (the last iteration's slot)
   if (iterations_out) *iterations_out = flags[1];
   if (flags[2] == 2) return fail(c, FSDF_ERR_ARG, "descend: poses not finite (configuration diverged)");
   if (flags[2]) return fail(c, FSDF_ERR_ARG, "descend: forward kinematics / chain rule (bad configuration)");
-  if (value_out) *value_out = h[2 * nx];
+  if (value_out) *value_out = h[3 * nx];
   return FSDF_OK;
 }
 
@@ -2105,7 +2111,9 @@ extern "C" int fsdf_descend(fsdf_ctx* c, double* x, int32_t iteration_limit, dou
   // rigid scenes (no RBF skin, no deformation) iterate on the device when the
   // mechanism's tree and the step's work arrays fit the step's LDS (M64's 65
   // bodies: ~45 KB)
-  bool device_loop = c->solver_device && iteration_limit > 0 && c->lm.R == 0 && Mc.n_deform == 0 && c->n > 0;
+  // (the step poses c->pm itself: not with the double-buffered pose overlap)
+  bool device_loop = c->solver_device && iteration_limit > 0 && c->lm.R == 0 && Mc.n_deform == 0 && c->n > 0 &&
+                     !FSDF_POSE_OVERLAP;
   if (device_loop && !c->solver_tree_ok) {
     HIPCHECK(c, hipSetDevice(c->device));
     const int rc = build_solver_tree(c);

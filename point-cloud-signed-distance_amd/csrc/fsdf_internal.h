@@ -283,15 +283,18 @@ struct SolverTree {
   // offsets into the doubles
   int axis = 0, AR = 0, At = 0, BR = 0, Bt = 0, frame_R = 0, frame_t = 0;  // frames: [S][9], [S][3]
 };
-// One frame's solver state (device): x [nx], optional divisors [nx], the joint
-// frames of the last FK (Rb [nb][9], tb [nb][3]), the poses the next pass reads
-// [S][12], f = the last evaluation's cost / n_points, flags [3] = (done — the
-// skip flag of the frame's launches —, iterations, error: 1 FK / chain rule,
-// 2 a non-finite pose).
+// One frame's solver state (device), two slots by iteration parity (a step
+// launch's workgroups read slot (k & 1) while its workgroup 0 writes slot
+// (k+1 & 1)): x [2][nx], the joint frames of the last FK Rb|tb [2][12 nb]
+// (Rb [nb][9] then tb [nb][3] per slot); optional divisors [nx]; f = the last
+// evaluation's cost / n_points; flags [3] = (done — the skip flag of the
+// frame's launches —, iterations (x of the last one in slot iterations & 1),
+// error: 1 FK / chain rule, 2 a non-finite pose). (The next pass's posed
+// model is written by the step itself: pose_impl.h.)
 struct SolverState {
   double* x = nullptr;
   const double* div = nullptr;
-  double *Rb = nullptr, *tb = nullptr, *poses = nullptr, *f = nullptr;
+  double *Rb = nullptr, *f = nullptr;
   int* flags = nullptr;
   double rate = 0.0, max_step = 0.0, tol = 0.0, n_points = 1.0, weight = 0.0;
   int limit = 0;
@@ -300,10 +303,15 @@ struct SolverState {
 bool solver_fits(int nb, int nx, int S, int ni);
 // diagnostic builds (-DFSDF_SOLVER_TIMES=1): the last step's phase clocks (16, 100 MHz)
 void solver_times(unsigned long long* out);
-// FK of st.x -> poses, Rb, tb (flags zeroed by the caller; set on an error)
-hipError_t launch_solver_init(const SolverTree& T, const SolverState& st, hipStream_t s);
-// one NaiveSolver iteration from the pass's accumulator (skips once flags[0] is set)
-hipError_t launch_solver_step(const SolverTree& T, const SolverState& st, const double* d_accum, hipStream_t s);
+// FK of st.x -> Rb, tb and the first pass's posed model pm (flags zeroed by the
+// caller; set on an error)
+hipError_t launch_solver_init(const SolverTree& T, const SolverState& st, const LocalModel& lm,
+                              const PosedModel& pm, int precision, hipStream_t s);
+// one NaiveSolver iteration from the pass's accumulator, ending with the next
+// pass's posed model pm (skips once flags[0] is set)
+hipError_t launch_solver_step(const SolverTree& T, const SolverState& st, const double* d_accum,
+                              const LocalModel& lm, const PosedModel& pm, int precision, int it_before,
+                              hipStream_t s);
 
 // Exchanged spatial shards (fsdf_set_points_keyed_device): the bounding box
 // (lo xyz, hi xyz; a device pointer into the scratch) of a device f64 cloud,

@@ -25,6 +25,7 @@
 
 #include "fsdf_internal.h"
 #include "kin_impl.h"
+#include "pose_impl.h"
 
 #ifndef FSDF_SOLVER_TIMES
 #define FSDF_SOLVER_TIMES 0  // diagnostic builds: per-phase clocks of the step (capi.hip prints them)
@@ -45,7 +46,7 @@ constexpr int kStepThreads = 1024;
 #if FSDF_SOLVER_TIMES
 __device__ unsigned long long g_solver_times[64];
 #define STAMP(i) \
-  if (threadIdx.x == 0 && it0 == 5) g_solver_times[i] = wall_clock64()
+  if (threadIdx.x == 0 && blockIdx.x == 0 && it0 == 5) g_solver_times[i] = wall_clock64()
 #else
 #define STAMP(i)
 #endif
@@ -58,14 +59,14 @@ __device__ unsigned long long g_solver_times[64];
 // barrier, not a global-memory round trip.
 struct Lds {
   const double *axis, *AR, *At, *BR, *Bt, *FR, *Ft;
-  double *acc, *Rb, *tb, *sub, *LR, *Lt, *R, *t, *x, *g, *div;
+  double *acc, *Rb, *tb, *sub, *LR, *Lt, *R, *t, *x, *g, *div, *P;
   const int32_t *parent, *kind, *qoff, *plist, *poff, *hord, *hoff, *coff, *clist, *soff, *slist, *sbody;
   const int32_t *chlist, *choff;
 };
 
-// the doubles after the blob: acc | Rb | tb | x | div | sub | LR | Lt | R | t | g
+// the doubles after the blob: acc | Rb | tb | x | div | sub | LR | Lt | R | t | g | P (the surface poses)
 __host__ __device__ inline size_t work_doubles(int nb, int nx, int S) {
-  return 1 + 6 * (size_t)S + 42 * (size_t)nb + 3 * (size_t)nx;
+  return 1 + 18 * (size_t)S + 42 * (size_t)nb + 3 * (size_t)nx;
 }
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
@@ -85,7 +86,7 @@ constexpr int kBlobPer = 12;  // 16-B blob chunks per thread: blobs up to 48 KB
 constexpr int kDynPer = 8;    // dynamic doubles per thread (accum, Rb|tb, x, div): up to 2,048
 
 template <int NT>
-__device__ Lds stage(const SolverTree& T, const SolverState& st, double* lds, const double* accum) {
+__device__ Lds stage(const SolverTree& T, const SolverState& st, double* lds, const double* accum, int slot) {
   // (per-thread load counts for NT threads: the same totals as kBlobPer / kDynPer at kSolverBlock)
   constexpr int BP = (kBlobPer * kSolverBlock + NT - 1) / NT, DP = (kDynPer * kSolverBlock + NT - 1) / NT;
   const int tid = threadIdx.x, nb = T.nb, nx = T.nx, S = T.S;
@@ -106,8 +107,8 @@ __device__ Lds stage(const SolverTree& T, const SolverState& st, double* lds, co
     const int i = tid + u * NT;
     double v = 0.0;
     if (i < na) v = accum[i];
-    else if (i < na + nr) v = st.Rb[i - na];  // (Rb | tb adjacent in the state buffer)
-    else if (i < na + nr + nx) v = st.x[i - na - nr];
+    else if (i < na + nr) v = st.Rb[(size_t)slot * 12 * nb + (i - na)];  // (Rb | tb adjacent in a slot)
+    else if (i < na + nr + nx) v = st.x[(size_t)slot * nx + (i - na - nr)];
     else if (i < ndyn) v = st.div[i - na - nr - nx];
     dv[u] = v;
   }
@@ -163,6 +164,8 @@ __device__ Lds stage(const SolverTree& T, const SolverState& st, double* lds, co
   L.t = d;
   d += 3 * nb;
   L.g = d;
+  d += nx;
+  L.P = d;
   // the dynamic doubles land at acc (accum | Rb tb | x | div are contiguous
   // there too; without an accumulator x lands at L.x)
 #pragma unroll
@@ -180,7 +183,8 @@ __device__ Lds stage(const SolverTree& T, const SolverState& st, double* lds, co
 // global store waits for the store to complete (its release fence), so every
 // store of the step is issued after the last barrier (publish()).
 template <int NT>
-__device__ void fk(const SolverTree& T, const Lds& L, int* bad) {
+__device__ void fk(const SolverTree& T, const Lds& L, int* bad, int it0 = -1) {
+  (void)it0;  // (FSDF_SOLVER_TIMES: the iteration whose phases are clocked)
   const int tid = threadIdx.x, nb = T.nb;
   for (int b = 1 + tid; b < nb; b += NT) {
     const int k = L.kind[b];
@@ -200,12 +204,13 @@ __device__ void fk(const SolverTree& T, const Lds& L, int* bad) {
     }
   }
   __syncthreads();
+  STAMP(5);
   // one thread per body composes its chain from the root in registers (every
   // ancestor's product as the host's level order computes it: the same bits,
   // no barrier per level); the ancestors' R, t only, and the joint frame
   // Rb, tb = R_parent · joint_to_parent for b itself
   for (int b = 1 + tid; b < nb; b += NT) {
-    double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, t[3] = {0, 0, 0}, v[12], w[12];
+    double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, t[3] = {0, 0, 0}, v[12], w[12], Rp[9], tp[3];
     const int q0 = L.poff[b], q1 = L.poff[b + 1];
     // the next ancestor's joint motion is loaded while this one composes
     double nLR[9], nLt[3];
@@ -224,19 +229,27 @@ __device__ void fk(const SolverTree& T, const Lds& L, int* bad) {
         kin::load(L.LR + 9 * an, nLR, 9);
         kin::load(L.Lt + 3 * an, nLt, 3);
       }
-      if (q == q1 - 1) {
-        double AR[9], At[3];
-        kin::load(L.AR + 9 * a, AR, 9);
-        kin::load(L.At + 3 * a, At, 3);
+      (void)a;
 #pragma unroll
-        for (int e = 0; e < 12; ++e) w[e] = kin::compose_entry(12 + e, R, t, LR, Lt, AR, At);
-      }
+      for (int e = 0; e < 9; ++e) Rp[e] = R[e];  // (the parent's frame, for b's joint frame below)
+#pragma unroll
+      for (int e = 0; e < 3; ++e) tp[e] = t[e];
 #pragma unroll
       for (int e = 0; e < 12; ++e) v[e] = kin::compose_entry(e, R, t, LR, Lt, nullptr, nullptr);
 #pragma unroll
       for (int e = 0; e < 9; ++e) R[e] = v[e];
 #pragma unroll
       for (int e = 0; e < 3; ++e) t[e] = v[9 + e];
+    }
+    // b's joint frame Tb_b = T_parent · joint_to_parent, after the walk (not a
+    // branch on the last level inside it: lanes of different depths would run
+    // that branch at every level between them)
+    {
+      double AR[9], At[3];
+      kin::load(L.AR + 9 * b, AR, 9);
+      kin::load(L.At + 3 * b, At, 3);
+#pragma unroll
+      for (int e = 0; e < 12; ++e) w[e] = kin::compose_entry(12 + e, Rp, tp, nullptr, nullptr, AR, At);
     }
     kin::store(L.R + 9 * b, v, 9);
     kin::store(L.t + 3 * b, v + 9, 3);
@@ -246,59 +259,84 @@ __device__ void fk(const SolverTree& T, const Lds& L, int* bad) {
   __syncthreads();
 }
 
-// After the last barrier: the surface poses (one entry per lane; a non-finite
-// entry marks the frame failed, error 2), the joint frames for the next chain
-// rule, x, and — thread 0 — f, the iteration count and the done / error flags.
+// The end of a step (and of the init): the surface poses into LDS (a
+// non-finite entry marks the frame failed, error 2), then — the next pass's
+// pose, in this launch instead of a pose kernel of its own — every work item
+// of the model's pose from them (pose_impl.h: world planes, screening pairs,
+// stage images, vertices, spheres and scales into the posed model the pass
+// reads), the joint frames for the next chain rule, x and — thread 0 — f, the
+// iteration count and the done / error flags. Every global store is issued
+// after the last barrier (a barrier's release fence would wait for them).
 // pose = false: the last iteration (no pass follows) publishes x and the flags only.
-template <int NT>
+template <typename TP, int NT>
 __device__ void publish(const SolverTree& T, const SolverState& st, const Lds& L, bool pose, int bad, double f,
-                        int it, int done) {
-  const int tid = threadIdx.x, nb = T.nb;
+                        int it, int done, const LocalModel& lm, const PosedModel& pm) {
+  const int tid = threadIdx.x, nb = T.nb, wg = blockIdx.x;
+  const int slot = it & 1;  // (the state the next step reads: x, Rb, tb of iteration it)
+  __shared__ int nonfinite;
   if (pose) {
+    if (tid == 0) nonfinite = 0;
+    __syncthreads();
     for (int i = tid; i < 12 * T.S; i += NT) {
       const int k = i / 12, q = i % 12, b = L.sbody[k];
       const double v = b < 0 ? ((q % 4 == 0 && q < 9) ? 1.0 : 0.0)
                              : kin::surface_pose_entry(q, L.R + 9 * b, L.t + 3 * b, L.FR + 9 * k, L.Ft + 3 * k);
-      st.poses[i] = v;
-      if (!isfinite(v)) {  // (every writer writes the same values)
-        st.flags[2] = 2;
-        st.flags[0] = 1;
-      }
+      L.P[i] = v;
+      if (!isfinite(v)) nonfinite = 1;  // (every writer writes the same value)
     }
-    for (int i = tid; i < 9 * nb; i += NT) st.Rb[i] = L.Rb[i];
-    for (int i = tid; i < 3 * nb; i += NT) st.tb[i] = L.tb[i];
+    __syncthreads();
+    // this workgroup's NT consecutive work items of the pose (whole waves: the
+    // total is a multiple of 64, as NT)
+    const int item = wg * NT + tid;
+    if (item < pose_items(lm))
+      pose_item<TP>(lm, L.P, (TP*)pm.planes_w, pm.spheres_w, (TP*)pm.verts_w, (TP*)pm.hscale_w,
+                    sizeof(TP) == 8 ? pm.screen_w : nullptr, sizeof(TP) == 8 ? (I4*)pm.image_w : nullptr, item);
   }
-  for (int i = tid; i < T.nx; i += NT) st.x[i] = L.x[i];
+  if (wg != 0) return;  // (the state: workgroup 0; every workgroup computed the same values)
+  if (pose) {
+    double* Rb = st.Rb + (size_t)slot * 12 * nb;
+    for (int i = tid; i < 9 * nb; i += NT) Rb[i] = L.Rb[i];
+    for (int i = tid; i < 3 * nb; i += NT) Rb[9 * nb + i] = L.tb[i];
+  }
+  if (it > 0)  // (the init's x is slot 0's own, which its workgroups are reading)
+    for (int i = tid; i < T.nx; i += NT) st.x[(size_t)slot * T.nx + i] = L.x[i];
   if (tid == 0) {
     *st.f = f;
     st.flags[1] = it;
-    if (bad || done) {
+    if (pose && nonfinite) {
+      st.flags[2] = 2;
+      st.flags[0] = 1;
+    } else if (bad || done) {
       st.flags[2] = bad ? 1 : 0;
       st.flags[0] = 1;
     }
   }
 }
 
-__global__ __launch_bounds__(kStepThreads) void solver_init_kernel(SolverTree T, SolverState st) {
+template <typename TP>
+__global__ __launch_bounds__(kStepThreads) void solver_init_kernel(SolverTree T, SolverState st, LocalModel lm,
+                                                                   PosedModel pm) {
   extern __shared__ double lds[];
   __shared__ int bad;
   const int tid = threadIdx.x;
   if (tid == 0) bad = 0;
-  const Lds L = stage<kStepThreads>(T, st, lds, nullptr);
+  const Lds L = stage<kStepThreads>(T, st, lds, nullptr, 0);  // (x0 in slot 0)
   __syncthreads();
   fk<kStepThreads>(T, L, &bad);  // (ends with a barrier; the host zeroed the flags before this launch)
-  publish<kStepThreads>(T, st, L, true, bad, 0.0, 0, 0);
+  publish<TP, kStepThreads>(T, st, L, true, bad, 0.0, 0, 0, lm, pm);
 }
 
 // One step over NT threads (solver_step_kernel: kStepThreads). (A launch
 // that also did the pass's final reduce — its last workgroup running the step
 // — measured no faster: the hand-off between workgroups costs what the launch
 // saves; branch archive/fused-reduce-step)
-template <int NT>
+template <typename TP, int NT>
 __device__ void step_body(const SolverTree& T, const SolverState& st, const double* __restrict__ accum,
-                          double* __restrict__ lds) {
-  // (the frame's flags load with the stage's loads; the done check waits for them)
-  const int done = __builtin_nontemporal_load(st.flags), it_before = __builtin_nontemporal_load(st.flags + 1);
+                          double* __restrict__ lds, const LocalModel& lm, const PosedModel& pm, int it_before) {
+  // (the frame's done flag loads with the stage's loads; the check waits for it.
+  // Workgroup 0 of this launch may set it at its end: a workgroup that reads it
+  // set returns — no pass follows a converged step)
+  const int done = __builtin_nontemporal_load(st.flags);
   __shared__ int bad, verdict;
   __shared__ double s_f;
   const int tid = threadIdx.x, nb = T.nb, nx = T.nx;
@@ -307,7 +345,7 @@ __device__ void step_body(const SolverTree& T, const SolverState& st, const doub
 #endif
   STAMP(0);
   if (tid == 0) bad = 0;
-  const Lds L = stage<NT>(T, st, lds, accum);
+  const Lds L = stage<NT>(T, st, lds, accum, it_before & 1);
   if (done) return;  // converged (or failed): the frame's remaining steps are no-ops (uniform)
   __syncthreads();
   STAMP(1);
@@ -422,27 +460,33 @@ __device__ void step_body(const SolverTree& T, const SolverState& st, const doub
   const int v = verdict;
   const double f = s_f;
   if (v == 3 || v == 1) {  // failed / converged: x stays
-    publish<NT>(T, st, L, false, v == 3, f, it, 1);
+    publish<TP, NT>(T, st, L, false, v == 3, f, it, 1, lm, pm);
     return;
   }
   for (int i = tid; i < nx; i += NT) L.x[i] = L.x[i] + kin::clipped_step(st.rate, L.g[i], st.max_step);
   if (v == 2) {  // the last iteration: no pass follows
     __syncthreads();
-    publish<NT>(T, st, L, false, 0, f, it, 1);
+    publish<TP, NT>(T, st, L, false, 0, f, it, 1, lm, pm);
     return;
   }
   __syncthreads();
   STAMP(4);
+#if FSDF_SOLVER_TIMES
+  fk<NT>(T, L, &bad, it0);  // (ends with a barrier)
+#else
   fk<NT>(T, L, &bad);  // (ends with a barrier)
+#endif
   STAMP(6);
-  publish<NT>(T, st, L, true, bad, f, it, 0);
+  publish<TP, NT>(T, st, L, true, bad, f, it, 0, lm, pm);
   STAMP(9);
 }
 
+template <typename TP>
 __global__ __launch_bounds__(kStepThreads) void solver_step_kernel(SolverTree T, SolverState st,
-                                                                   const double* __restrict__ accum) {
+                                                                   const double* __restrict__ accum, LocalModel lm,
+                                                                   PosedModel pm, int it_before) {
   extern __shared__ double lds[];
-  step_body<kStepThreads>(T, st, accum, lds);
+  step_body<TP, kStepThreads>(T, st, accum, lds, lm, pm, it_before);
 }
 
 size_t solver_lds_bytes(const SolverTree& T) {
@@ -460,8 +504,22 @@ bool solver_fits(int nb, int nx, int S, int ni) {
          blob * 16 + work_doubles(nb, nx, S) * 8 <= 65536;
 }
 
-hipError_t launch_solver_init(const SolverTree& T, const SolverState& st, hipStream_t s) {
-  hipLaunchKernelGGL(solver_init_kernel, dim3(1), dim3(kStepThreads), solver_lds_bytes(T), s, T, st);
+// one workgroup per kStepThreads work items of the pose, each running the whole
+// step (the same arithmetic on the same inputs: the same values) and then
+// posing its items — the pose in the step's launch, at the latency of one step
+static dim3 solver_grid(const LocalModel& lm) {
+  const int g = (pose_items(lm) + kStepThreads - 1) / kStepThreads;
+  return dim3((unsigned)(g > 0 ? g : 1));
+}
+
+hipError_t launch_solver_init(const SolverTree& T, const SolverState& st, const LocalModel& lm,
+                              const PosedModel& pm, int precision, hipStream_t s) {
+  if (precision == 64)
+    hipLaunchKernelGGL(solver_init_kernel<double>, solver_grid(lm), dim3(kStepThreads), solver_lds_bytes(T), s, T, st,
+                       lm, pm);
+  else
+    hipLaunchKernelGGL(solver_init_kernel<float>, solver_grid(lm), dim3(kStepThreads), solver_lds_bytes(T), s, T, st,
+                       lm, pm);
   return hipGetLastError();
 }
 
@@ -473,8 +531,15 @@ void solver_times(unsigned long long* out) {
 #endif
 }
 
-hipError_t launch_solver_step(const SolverTree& T, const SolverState& st, const double* d_accum, hipStream_t s) {
-  hipLaunchKernelGGL(solver_step_kernel, dim3(1), dim3(kStepThreads), solver_lds_bytes(T), s, T, st, d_accum);
+hipError_t launch_solver_step(const SolverTree& T, const SolverState& st, const double* d_accum,
+                              const LocalModel& lm, const PosedModel& pm, int precision, int it_before,
+                              hipStream_t s) {
+  if (precision == 64)
+    hipLaunchKernelGGL(solver_step_kernel<double>, solver_grid(lm), dim3(kStepThreads), solver_lds_bytes(T), s, T, st,
+                       d_accum, lm, pm, it_before);
+  else
+    hipLaunchKernelGGL(solver_step_kernel<float>, solver_grid(lm), dim3(kStepThreads), solver_lds_bytes(T), s, T, st,
+                       d_accum, lm, pm, it_before);
   return hipGetLastError();
 }
 

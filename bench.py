@@ -333,7 +333,8 @@ def measured_frame(manip, ctx, pts_host, q, torch, frames=5):
                    f"{ITERS_PER_FRAME} iterations, tolerance 1e-3) from q_eval; median of {frames} frames; "
                    "device_loop: solver step on the GPU (solver.hip), host_loop: fsdf_set_solver(0)")
     ctx.set_solver(False)  # (the library's default)
-    out["default"] = "host_loop"
+    out["default"] = "host_loop"  # (fsdf_set_solver's default)
+    out["frame_loop"] = "host_loop_prefetched"  # (what flash.tracking.track / Tracker.step(next_points) run)
     return out
 
 

@@ -27,6 +27,10 @@
 #ifndef FSDF_POSE_OVERLAP
 #define FSDF_POSE_OVERLAP 0  // (pose_model: measured slower, off)
 #endif
+#ifndef FSDF_ORDER_EVERY
+#define FSDF_ORDER_EVERY 16
+#endif
+static constexpr int kOrderEvery = FSDF_ORDER_EVERY;
 
 namespace {
 
@@ -1104,8 +1108,12 @@ extern "C" int fsdf_regroup_points(fsdf_ctx* c) {
   if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "regroup_points: %s", hipGetErrorString(e));
   const int64_t nc = ((c->n + 63) / 64 + 3) & ~(int64_t)3;
   HIPCHECK(c, fsdf::launch_chunk_spheres(c->precision, c->d_pts, c->n, nc, c->d_chunk_ws, c->stream));
-  c->plan_nc = -1;       // other chunks: the next planned pass measures anew
-  c->order_nblocks = 0;  // and the cost-ordered schedule is rebuilt
+  c->plan_nc = -1;  // other chunks: the next planned pass measures anew
+  // the one-wave grid's heaviest-first block order: the next pass still runs
+  // the pre-regroup order (the regroup is a stable sort within windows, the
+  // heavy regions stay where they were) and rebuilds it from its own costs —
+  // unordered, that pass took 163 us instead of 122 (M64 2^20, profiles/r06/regroup_order/)
+  c->order_age = kOrderEvery;
   c->regrouped = true;
   c->regroup_pending = false;
   return FSDF_OK;
@@ -1211,10 +1219,6 @@ static int release_posed(fsdf_ctx* c, int buf) {
   return FSDF_OK;
 }
 
-#ifndef FSDF_ORDER_EVERY
-#define FSDF_ORDER_EVERY 16
-#endif
-static constexpr int kOrderEvery = FSDF_ORDER_EVERY;
 
 static int ensure_chunk_outputs(fsdf_ctx* c, int64_t nc) {
   if (c->co_cap >= nc && c->co_s >= c->lm.S) return FSDF_OK;

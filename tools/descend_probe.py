@@ -65,6 +65,26 @@ def trace(path):
         print(f"device loop: iteration span {statistics.median(spans):.2f} us, kernels busy "
               f"{statistics.median(busy):.2f} us, idle {statistics.median([s - b for s, b in zip(spans, busy)]):.2f} us "
               f"(median over {len(spans)})")
+    # device loop, per frame (from its solver_init_kernel): the first iterations
+    # (the new cloud's unseeded pass, the regroup, the first pass after it)
+    # against the steady ones
+    inits = [i for i, r in enumerate(rows) if "solver_init_kernel" in r["Kernel_Name"]]
+    per = []
+    for fi, i0 in enumerate(inits):
+        i1 = inits[fi + 1] if fi + 1 < len(inits) else len(rows)
+        prev, its = int(rows[i0]["End_Timestamp"]), []
+        for k in range(i0 + 1, i1):
+            if "step_kernel" in rows[k]["Kernel_Name"]:
+                e = int(rows[k]["End_Timestamp"])
+                its.append((e - prev) / 1e3)
+                prev = e
+        if len(its) >= 4:
+            per.append(its)
+    if per:
+        med = lambda j: statistics.median(p[j] for p in per)  # noqa: E731
+        steady = statistics.median(x for p in per for x in p[2:])
+        print(f"device loop per frame: iteration 1 {med(0):.1f} us, iteration 2 {med(1):.1f} us, then "
+              f"{steady:.1f} us (median over {len(per)} frames)")
     # host loop: the iterations' pose -> pass -> reduce triplets (pose_kernel_args) and the gap before each pose
     poses = [i for i, r in enumerate(rows) if "pose_kernel_args" in r["Kernel_Name"]]
     gaps = [(int(rows[i]["Start_Timestamp"]) - int(rows[i - 1]["End_Timestamp"])) / 1e3 for i in poses if i > 0]

@@ -9,5 +9,5 @@ for L in "$@"; do
       > $O/tr_$L.log 2>&1 ) || { echo TRACE FAILED; tail $O/tr_$L.log; exit 1; }
   echo "== $L"; grep loop $O/tr_$L.log
   python3 $GRAFT_REPO_ROOT/tools/descend_probe.py --trace $(ls $O/tr_$L/*/run_kernel_trace.csv $O/tr_$L/run_kernel_trace.csv 2>/dev/null | head -1) > $O/tr_$L.txt
-  grep -E "step_kernel|reduce_tiles|pose_kernel|pass_kernel|span|idle" $O/tr_$L.txt
+  grep -E "step_kernel|reduce_tiles|pose_kernel|pass_kernel|span|idle|per frame" $O/tr_$L.txt
 done

@@ -27,6 +27,9 @@
 #ifndef FSDF_POSE_OVERLAP
 #define FSDF_POSE_OVERLAP 0  // (pose_model: measured slower, off)
 #endif
+#ifndef FSDF_PRIOR_SEEDS
+#define FSDF_PRIOR_SEEDS 1
+#endif
 #ifndef FSDF_ORDER_EVERY
 #define FSDF_ORDER_EVERY 16
 #endif
@@ -140,6 +143,10 @@ struct fsdf_ctx {
   float* d_chunk_ws_next = nullptr;
   int64_t pts_cap_next = 0, perm_cap_next = 0, chunk_ws_cap_next = 0;
   fsdf::SortScratch sort_next;
+  // seeds carried from one cloud to the next (a voxel grid of the last pass's k*)
+  uint8_t* d_vox = nullptr;
+  bool vox_ok = false, seed_pending = false;
+  fsdf::VoxBox vox;
   hipStream_t copy_stream = nullptr;
   hipEvent_t ev_prefetch = nullptr;
   bool ranged = false;               // the resident cloud is a range of a larger one (fsdf_set_points_range)
@@ -151,9 +158,13 @@ struct fsdf_ctx {
   size_t partials_cap = 0;
   // cost-ordered schedule of resident-cloud passes (fsdf::PassOutputs::order)
   uint32_t* d_block_cost = nullptr;  // [kMaxBlocks]
-  int32_t* d_block_order = nullptr;  // [kMaxBlocks]
-  int order_nblocks = 0;             // grid the order was built for (0: none yet)
-  int order_age = 0;                 // passes since the order was rebuilt
+  // the one-wave grid's heaviest-first block orders, one per layout of a frame's
+  // cloud: [0] its Hilbert order (the frame's first pass), [1] regrouped (the
+  // rest of the frame) — each rebuilt from the costs of a pass in its layout, so
+  // a frame's passes run the order the previous frame left for the same layout
+  int32_t* d_block_order[2] = {nullptr, nullptr};  // [kMaxBlocks]
+  int order_nblocks[2] = {0, 0};  // grid the order was built for (0: none yet)
+  int order_age[2] = {0, 0};      // passes since the order was rebuilt
   // planned pass (fsdf::planned_pass_kernel): per-chunk partial rows, chunk
   // durations and the workgroup plan built from them (fsdf_set_plan)
   fsdf::ChunkOutputs co;             // device arrays, [co_cap] chunks
@@ -356,6 +367,7 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   dfree(c->d_perm_next);
   dfree(c->d_chunk_ws_next);
   fsdf::free_sort_scratch(c->sort_next);
+  dfree(c->d_vox);
   if (c->ev_prefetch) (void)hipEventDestroy(c->ev_prefetch);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   dfree(c->d_range_pts);
@@ -369,7 +381,8 @@ extern "C" int fsdf_destroy(fsdf_ctx* c) {
   dfree(c->d_q64);
   dfree(c->d_stats);
   dfree(c->d_block_cost);
-  dfree(c->d_block_order);
+  dfree(c->d_block_order[0]);
+  dfree(c->d_block_order[1]);
   dfree(c->co.hdr);
   dfree(c->co.ent);  // (csum, dense: the same allocation)
   dfree(c->co.dur);
@@ -788,6 +801,47 @@ static int adopt_points_device(fsdf_ctx* c, const double* d_src, int64_t n, void
 
 static int finish_resident(fsdf_ctx* c, int64_t n, bool ranged, bool spheres_done = false);
 
+// Seeds for a new cloud's first pass from the last pass over the previous one
+// (fsdf_set_points / fsdf_set_points_prefetched of sorting hull-only contexts):
+// before the cloud is replaced its points write their k* into a coarse voxel
+// grid (carry_seeds_out), after it the new points read theirs into the seed
+// buffer (finish_resident). The grid's box is the first cloud's box grown by
+// a quarter of its extent each way, fixed for the context. Seeds only order
+// the search — the pass's bits do not depend on them (tests/test_gpu_tracking.py).
+static bool seeds_apply(const fsdf_ctx* c) {
+  return FSDF_PRIOR_SEEDS && c->sort_points && c->lm.R == 0 && c->lm.S <= 64 && c->lm.K > 0;
+}
+
+static int ensure_vox_box(fsdf_ctx* c, const double* d_src, int64_t n) {
+  if (c->vox_ok || n <= 0 || !seeds_apply(c)) return FSDF_OK;
+  double* d_box = nullptr;
+  hipError_t e = fsdf::cloud_box(d_src, n, c->sort, c->stream, &d_box);
+  if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "set_points (seed box): %s", hipGetErrorString(e));
+  double box[6];
+  HIPCHECK(c, hipMemcpyAsync(box, d_box, sizeof box, hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(c, hipStreamSynchronize(c->stream));  // (once per context)
+  for (int j = 0; j < 3; ++j) {
+    const double ext = std::max(box[3 + j] - box[j], 1e-3);
+    if (!std::isfinite(ext)) return FSDF_OK;  // (no seeds)
+    c->vox.lo[j] = box[j] - 0.25 * ext;
+    c->vox.inv[j] = fsdf::kVoxDim / (1.5 * ext);
+  }
+  if (!c->d_vox) HIPCHECK(c, hipMalloc(&c->d_vox, (size_t)fsdf::kVoxDim * fsdf::kVoxDim * fsdf::kVoxDim));
+  c->vox_ok = true;
+  return FSDF_OK;
+}
+
+static int carry_seeds_out(fsdf_ctx* c) {
+  c->seed_pending = false;
+  if (!c->vox_ok || !seeds_apply(c) || c->n <= 0 || !c->prior_ok || !c->d_prior || c->prior_cap < c->n || c->ranged)
+    return FSDF_OK;
+  HIPCHECK(c, hipMemsetAsync(c->d_vox, 0xFF, (size_t)fsdf::kVoxDim * fsdf::kVoxDim * fsdf::kVoxDim, c->stream));
+  hipError_t e = fsdf::vox_scatter(c->precision, c->d_pts, c->n, c->d_prior, c->vox, c->d_vox, c->stream);
+  if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "set_points (seeds): %s", hipGetErrorString(e));
+  c->seed_pending = true;
+  return FSDF_OK;
+}
+
 // [begin, end): the resident cloud is that range of the whole cloud's order
 // (the Hilbert order of all n points with sort_points, else the caller's);
 // the permutation then holds the points' indices in the whole cloud
@@ -805,6 +859,8 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
   HIPCHECK(c, hipSetDevice(c->device));
   // the previous frame's work may still read the staging buffer / the cloud
   HIPCHECK(c, hipStreamSynchronize(c->stream));
+  int rc0 = ranged ? FSDF_OK : carry_seeds_out(c);  // (the previous cloud, still resident)
+  if (rc0) return rc0;
   c->n = 0;
   const double* d_src = src;
   if (!device_src && n > 0) {
@@ -838,6 +894,10 @@ static int set_points_impl(fsdf_ctx* c, const double* src, int64_t n, bool devic
     // spatially coherent resident order + permutation back to caller order
     int rc = ensure_res();
     if (rc) return rc;
+    if (!ranged) {
+      rc = ensure_vox_box(c, d_src, n);
+      if (rc) return rc;
+    }
     if (!ranged) {
       hipError_t e = fsdf::sort_points_spatial(d_src, n, c->precision, c->d_pts, c->d_perm, c->sort, c->stream);
       if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "set_points (sort): %s", hipGetErrorString(e));
@@ -901,13 +961,21 @@ static int finish_resident(fsdf_ctx* c, int64_t n, bool ranged, bool spheres_don
   }
   if (n > 0) {
     if (c->prior_cap < n) {  // (the previous frame's passes are done: synchronised above)
+      HIPCHECK(c, hipStreamSynchronize(c->stream));  // (the seed scatter may still read it)
       dfree(c->d_prior);
       c->prior_cap = 0;
       HIPCHECK(c, hipMalloc(&c->d_prior, (size_t)n));
       c->prior_cap = n;
     }
   }
-  c->prior_ok = false;  // a new cloud: its first pass seeds from the bounds
+  // a new cloud: its first pass seeds from the previous cloud's voxels, else from the bounds
+  c->prior_ok = false;
+  if (c->seed_pending && n > 0 && !ranged && c->d_prior && c->prior_cap >= n) {
+    hipError_t e = fsdf::vox_gather(c->precision, c->d_pts, n, c->vox, c->d_vox, c->d_prior, c->stream);
+    if (e != hipSuccess) return fail(c, FSDF_ERR_HIP, "set_points (seeds): %s", hipGetErrorString(e));
+    c->prior_ok = true;
+  }
+  c->seed_pending = false;
   c->regrouped = false;
   c->regroup_pending = true;  // (the auto regroup follows the new cloud's first iteration pass)
   c->last_pass_shape = 0;
@@ -918,6 +986,10 @@ static int finish_resident(fsdf_ctx* c, int64_t n, bool ranged, bool spheres_don
   // whole cloud: the caller indexes them through the permutation)
   c->ranged = ranged;
   c->plan_nc = -1;  // a new cloud: its first planned pass runs the default shape and measures
+  // and its first one-wave pass runs the previous cloud's Hilbert-layout
+  // order and rebuilds it from its own costs (left to age, a stale order cost
+  // the next passes 0.094 -> 0.111 ms, tools/seed_probe.py)
+  c->order_age[0] = kOrderEvery;
   return FSDF_OK;
 }
 
@@ -1069,6 +1141,10 @@ extern "C" int fsdf_set_points_prefetched(fsdf_ctx* c) {
   // the sorted next cloud becomes resident: the current frame's work is done
   // (synchronised), its buffers become the next prefetch's
   HIPCHECK(c, hipStreamSynchronize(c->stream));
+  int rc = ensure_vox_box(c, c->d_prefetch, n);  // (a first cloud: the seed box)
+  if (rc) return rc;
+  rc = carry_seeds_out(c);  // (the previous cloud, still resident)
+  if (rc) return rc;
   c->n = 0;
   std::swap(c->d_pts, c->d_pts_next);
   std::swap(c->pts_cap, c->pts_cap_next);
@@ -1109,11 +1185,11 @@ extern "C" int fsdf_regroup_points(fsdf_ctx* c) {
   const int64_t nc = ((c->n + 63) / 64 + 3) & ~(int64_t)3;
   HIPCHECK(c, fsdf::launch_chunk_spheres(c->precision, c->d_pts, c->n, nc, c->d_chunk_ws, c->stream));
   c->plan_nc = -1;  // other chunks: the next planned pass measures anew
-  // the one-wave grid's heaviest-first block order: the next pass still runs
-  // the pre-regroup order (the regroup is a stable sort within windows, the
-  // heavy regions stay where they were) and rebuilds it from its own costs —
-  // unordered, that pass took 163 us instead of 122 (M64 2^20, profiles/r06/regroup_order/)
-  c->order_age = kOrderEvery;
+  // the one-wave grid's heaviest-first block order: the next pass runs the
+  // regrouped layout's order (the previous frame's) and rebuilds it from its
+  // own costs — unordered, that pass took 163 us, with the Hilbert layout's
+  // order 177, with the previous regrouped one 122 (M64 2^20, profiles/r06/regroup_order/)
+  c->order_age[1] = kOrderEvery;
   c->regrouped = true;
   c->regroup_pending = false;
   return FSDF_OK;
@@ -1324,9 +1400,6 @@ static int run_planned(fsdf_ctx* c, const fsdf::PosedModel& P, const void* d_pts
   return FSDF_OK;
 }
 
-#ifndef FSDF_PRIOR_SEEDS
-#define FSDF_PRIOR_SEEDS 1
-#endif
 // schedule: resident-cloud passes (repeated over the same cloud) launch their
 // workgroups heaviest-first by the previous pass's durations
 // posed / skip: the device solver loop's pass — its model posed by the
@@ -1375,13 +1448,15 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
     if (prof) c->prof_used += 3;
     return release_posed(c, pbuf);
   }
+  const int ol = c->regrouped ? 1 : 0;  // (the layout's block order)
   if (schedule && n > 0) {
     if (!c->d_block_cost) {
       HIPCHECK(c, hipMalloc(&c->d_block_cost, fsdf::kMaxBlocks * sizeof(uint32_t)));
-      HIPCHECK(c, hipMalloc(&c->d_block_order, fsdf::kMaxBlocks * sizeof(int32_t)));
+      HIPCHECK(c, hipMalloc(&c->d_block_order[0], fsdf::kMaxBlocks * sizeof(int32_t)));
+      HIPCHECK(c, hipMalloc(&c->d_block_order[1], fsdf::kMaxBlocks * sizeof(int32_t)));
     }
     out.cost = c->d_block_cost;
-    out.order = c->order_nblocks == nblocks ? c->d_block_order : nullptr;
+    out.order = c->order_nblocks[ol] == nblocks ? c->d_block_order[ol] : nullptr;
   }
   if (n > 0) {
     // profiling: the pass kernel's start / end and the reduce's end, stamped
@@ -1399,13 +1474,13 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
     // the order is rebuilt on the first scheduled pass of a grid and then every
     // kOrderEvery passes (the heavy blocks of a cloud stay heavy from pass to
     // pass; the rebuild is a ~7 us single-workgroup sort on the reduce launch)
-    const bool rebuild = out.cost && (c->order_nblocks != nblocks || ++c->order_age >= kOrderEvery);
+    const bool rebuild = out.cost && (c->order_nblocks[ol] != nblocks || ++c->order_age[ol] >= kOrderEvery);
     HIPCHECK(c, fsdf::launch_reduce(c->d_partials, nblocks, accum_len(c), d_accum, c->stream,
-                                    rebuild ? out.cost : nullptr, rebuild ? c->d_block_order : nullptr,
+                                    rebuild ? out.cost : nullptr, rebuild ? c->d_block_order[ol] : nullptr,
                                     pe ? pe[2] : nullptr, skip));
     if (rebuild) {
-      c->order_nblocks = nblocks;
-      c->order_age = 0;
+      c->order_nblocks[ol] = nblocks;
+      c->order_age[ol] = 0;
     }
   } else {
     rc = release_posed(c, pbuf);

@@ -320,6 +320,18 @@ hipError_t launch_solver_step(const SolverTree& T, const SolverState& st, const 
 // whole-cloud index) with perm = those indices (< 2^31) — the order a shard of
 // the whole cloud's sort_points_spatial order has. Asynchronous on `st`.
 hipError_t cloud_box(const double* d_src, int64_t n, SortScratch& s, hipStream_t st, double** d_box);
+// Seeds carried from one cloud to the next (sort.hip): a kVoxDim^3 grid of
+// uint8 k* over a box fixed per context (lo, cells per unit length inv)
+constexpr int kVoxDim = 64;
+struct VoxBox {
+  double lo[3] = {0, 0, 0}, inv[3] = {0, 0, 0};
+};
+// every point of a resident cloud (context precision) writes its prior k* (< 64) into its voxel
+hipError_t vox_scatter(int precision, const void* d_pts, int64_t n, const uint8_t* d_prior, const VoxBox& b,
+                       uint8_t* d_grid, hipStream_t st);
+// every point's prior from its voxel (0xFF outside the box or in an empty voxel)
+hipError_t vox_gather(int precision, const void* d_pts, int64_t n, const VoxBox& b, const uint8_t* d_grid,
+                      uint8_t* d_prior, hipStream_t st);
 hipError_t curve_keys(const double* d_src, int64_t n, const double* d_box, uint32_t* d_keys, hipStream_t st);
 hipError_t sort_points_keyed(const double* d_src, const uint32_t* d_keys, const int64_t* d_index, int64_t n,
                              int precision, void* d_dst, int32_t* d_perm, SortScratch& s, hipStream_t st);

@@ -342,7 +342,66 @@ hipError_t grow(P** p, size_t* cap, size_t need) {
   return e;
 }
 
+// Seed carry-over between frames (the new cloud's first pass seeded by the
+// nearest surface the previous cloud's last pass found nearby): a coarse
+// voxel grid over a box fixed per context; each previous point writes its k*
+// into its voxel (any writer wins: a seed only orders the search, every seed
+// gives the same bits), each new point reads its voxel's (0xFF: none).
+__device__ __forceinline__ int vox_cell(double x, double y, double z, const VoxBox& b) {
+  const double u = (x - b.lo[0]) * b.inv[0], v = (y - b.lo[1]) * b.inv[1], w = (z - b.lo[2]) * b.inv[2];
+  if (!(u >= 0.0 && u < kVoxDim && v >= 0.0 && v < kVoxDim && w >= 0.0 && w < kVoxDim)) return -1;
+  return ((int)w * kVoxDim + (int)v) * kVoxDim + (int)u;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void vox_scatter_kernel(const T* __restrict__ pts, int64_t n,
+                                                             const uint8_t* __restrict__ prior, VoxBox b,
+                                                             uint8_t* __restrict__ grid) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t k = prior[i];
+  if (k >= 64) return;
+  const int c = vox_cell((double)pts[3 * i], (double)pts[3 * i + 1], (double)pts[3 * i + 2], b);
+  if (c >= 0) grid[c] = k;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void vox_gather_kernel(const T* __restrict__ pts, int64_t n, VoxBox b,
+                                                            const uint8_t* __restrict__ grid,
+                                                            uint8_t* __restrict__ prior) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int c = vox_cell((double)pts[3 * i], (double)pts[3 * i + 1], (double)pts[3 * i + 2], b);
+  prior[i] = c >= 0 ? grid[c] : (uint8_t)0xFF;
+}
+
 }  // namespace
+
+hipError_t vox_scatter(int precision, const void* d_pts, int64_t n, const uint8_t* d_prior, const VoxBox& b,
+                       uint8_t* d_grid, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
+  if (precision == 64)
+    hipLaunchKernelGGL(vox_scatter_kernel<double>, dim3(grid), dim3(kBlock), 0, st, (const double*)d_pts, n, d_prior,
+                       b, d_grid);
+  else
+    hipLaunchKernelGGL(vox_scatter_kernel<float>, dim3(grid), dim3(kBlock), 0, st, (const float*)d_pts, n, d_prior, b,
+                       d_grid);
+  return hipGetLastError();
+}
+
+hipError_t vox_gather(int precision, const void* d_pts, int64_t n, const VoxBox& b, const uint8_t* d_grid,
+                      uint8_t* d_prior, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const unsigned grid = (unsigned)((n + kBlock - 1) / kBlock);
+  if (precision == 64)
+    hipLaunchKernelGGL(vox_gather_kernel<double>, dim3(grid), dim3(kBlock), 0, st, (const double*)d_pts, n, b, d_grid,
+                       d_prior);
+  else
+    hipLaunchKernelGGL(vox_gather_kernel<float>, dim3(grid), dim3(kBlock), 0, st, (const float*)d_pts, n, b, d_grid,
+                       d_prior);
+  return hipGetLastError();
+}
 
 void free_sort_scratch(SortScratch& s) {
   if (s.part) (void)hipFree(s.part);

@@ -221,8 +221,8 @@ struct fsdf_ctx {
   // device solver loop of fsdf_descend (solver.hip): the mechanism's device
   // arrays (built on the first device descend after fsdf_set_mechanism) and
   // one frame's state; pinned staging for x / divisors in and x, f, flags out
-  int solver_device = 0;             // fsdf_set_solver: 0 host loop (default: measured faster, DESIGN.md §7
-                                     // round 6), 1 device where possible, 2 device required
+  int solver_device = 1;             // fsdf_set_solver: 1 device where possible (default), 0 host loop,
+                                     // 2 device required
   bool solver_tree_ok = false;
   fsdf::SolverTree stree;
   double* d_stree_d = nullptr;       // the tree blob (fsdf::SolverTree::blob)

@@ -311,9 +311,9 @@ class Context:
 
     def set_solver(self, device_loop):
         """fsdf_set_solver: descend's iterations on the device where the scene
-        allows (True / 1: rigid scenes), required there ("require" / 2:
-        FSDF_ERR_STATE otherwise), or the host loop around value_and_gradient
-        (False / 0, the default)."""
+        allows (True / 1, the default: rigid scenes), required there
+        ("require" / 2: FSDF_ERR_STATE otherwise), or the host loop around
+        value_and_gradient (False / 0)."""
         mode = 2 if device_loop == "require" else int(device_loop)
         check(self._lib.fsdf_set_solver(self._ctx, mode), self._ctx, "set_solver")
 

@@ -77,7 +77,7 @@ def test_device_loop_bit_identical_to_host_loop(name, n):
             assert ib == 1 and np.array_equal(xb, x0)
             c, _ = cf.value_and_gradient(x0)
             assert fb == c / len(pts)
-    ctx.set_solver(False)
+    ctx.set_solver(True)  # (the default)
 
 
 def test_device_loop_refuses_bad_configuration():

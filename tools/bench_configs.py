@@ -87,7 +87,7 @@ def track_frame(m, x, pts, precision, iters=30, frames=3):
         ms = statistics.median(ts)
         out[f"frame_{name}_ms_per_iteration"] = ms / its
         out[f"frame_{name}_tracking_evals_per_s"] = len(pts) * its / (ms / 1e3)
-    cf.ctx.set_solver(False)
+    cf.ctx.set_solver(True)  # (the default)
     return out
 
 

@@ -1,8 +1,9 @@
 // solver.hip — estimate_state's solver iteration on the device, for rigid
-// (hull-only) scenes: after a residual pass and its reduce, one small
-// workgroup turns the accumulator into the next configuration and the next
-// surface poses, so a whole frame of iterations is enqueued with no host
-// round trip (fsdf_descend, capi.hip descend_device).
+// (hull-only) scenes: after a residual pass and its reduce, one launch turns
+// the accumulator into the next configuration, the next surface poses and the
+// next pass's posed model, so a whole frame of iterations is enqueued with no
+// host round trip (fsdf_descend, capi.hip descend_device; the default for
+// rigid scenes, fsdf_set_solver).
 //
 // Per iteration, the arithmetic of the host loop (capi.hip fsdf_descend around
 // fsdf_value_and_gradient) in the same order, from kin_impl.h:
@@ -14,11 +15,15 @@
 //   NaiveSolver g = (∂c/∂x / N) ./ divisors, stop at |g| < tolerance, else
 //               x += clamp(-rate g, ±max_step) (flash/tracking.py; the
 //               un-vendored SimpleGradientDescent.jl, src/tracking.jl:12-15)
-//   FK          joint motions in parallel, then composition level by level
-//               (each body's product as the host computes it), surface poses
-// so x, f and the iteration count equal the host loop's bit for bit.
+//   FK          joint motions in parallel, then each body's chain from the
+//               root composed in registers (each product as the host's level
+//               order computes it), surface poses
+// so x, f and the iteration count equal the host loop's bit for bit. Every
+// workgroup of the launch runs the whole step on the same inputs (the same
+// values) and then poses its 1,024 of the model's pose items (pose_impl.h);
+// workgroup 0 alone writes the state, double-buffered by iteration parity.
 //
-// The pose / pass / reduce launches of later iterations read `flags[0]`
+// The pass / reduce / step launches of later iterations read `flags[0]`
 // (SolverState::flags) and return at once after convergence; the remaining
 // iterations of the frame cost their (empty) launches only.
 #include <hip/hip_runtime.h>
@@ -54,7 +59,8 @@ __device__ unsigned long long g_solver_times[64];
 // The step's LDS: the tree blob (doubles [nd], ints [ni], padded to 16 B) |
 // the accumulator [1+6S] | Rb [9nb] | tb [3nb] (the last FK's joint frames:
 // read by the chain rule, then overwritten by this step's FK) | x [nx] |
-// div [nx] | sub [6nb] | LR [9nb] | Lt [3nb] | R [9nb] | t [3nb] | g [nx].
+// div [nx] | sub [6nb] | LR [9nb] | Lt [3nb] | R [9nb] | t [3nb] | g [nx] |
+// P [12S] (the surface poses the pose items read).
 // Every array the level loops touch is here: a level costs LDS latency and a
 // barrier, not a global-memory round trip.
 struct Lds {

@@ -255,7 +255,10 @@ int fsdf_set_surfaces(fsdf_ctx* ctx, const fsdf_surface* surfaces, int32_t n_sur
 int fsdf_set_rbf_params(fsdf_ctx* ctx, const double* params, int64_t n_doubles);
 
 /* Upload the sensed cloud once per frame (src/gradientdescent.jl:43 holds it
- * by reference across every cost evaluation). */
+ * by reference across every cost evaluation). A sorting hull-only context
+ * seeds the new cloud's first pass from the previous cloud's last nearest
+ * surfaces (a voxel grid over the first cloud's box, grown by half its extent;
+ * seeds order the search only — results do not depend on them). */
 int fsdf_set_points(fsdf_ctx* ctx, const double* xyz, int64_t n);
 /* Same, from a device-resident AoS buffer (copied device-to-device). */
 int fsdf_set_points_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n);

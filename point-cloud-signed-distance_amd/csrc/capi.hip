@@ -83,6 +83,7 @@ struct fsdf_ctx {
   int32_t* d_vert_off = nullptr;
   int32_t* d_face_rows = nullptr;
   int32_t* d_hull_surface = nullptr;
+  int32_t* d_item_meta = nullptr;  // LocalModel::item_meta
   int32_t* d_surface_kind = nullptr;
   int32_t* d_rbf_surface = nullptr;
   int32_t* d_rbf_row_off = nullptr;
@@ -262,6 +263,7 @@ static void free_model(fsdf_ctx* c) {
   dfree(c->d_vert_off);
   dfree(c->d_face_rows);
   dfree(c->d_hull_surface);
+  dfree(c->d_item_meta);
   dfree(c->d_surface_kind);
   dfree(c->d_rbf_surface);
   dfree(c->d_rbf_row_off);
@@ -641,6 +643,17 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   HIPCHECK(c, dalloc(&c->d_vert_hull, vert_hull.size() * sizeof(int32_t)));
   HIPCHECK(c, dalloc(&c->d_vert_off, vert_off.size() * sizeof(int32_t)));
   HIPCHECK(c, dalloc(&c->d_face_rows, std::max<size_t>(4, face_rows.size()) * sizeof(int32_t)));
+  std::vector<int32_t> item_meta;  // (LocalModel::item_meta)
+  item_meta.reserve((size_t)(F + V) * 4);
+  auto meta = [&](int h) {
+    const int nf = face_off[h + 1] - face_off[h];
+    item_meta.insert(item_meta.end(), {hull_surface[h] | (nf << 16), h, face_off[h], vert_off[h]});
+  };
+  for (int f = 0; f < F; ++f) meta(face_hull[f]);
+  for (int v = 0; v < V; ++v) meta(vert_hull[v]);
+  HIPCHECK(c, dalloc(&c->d_item_meta, std::max<size_t>(4, item_meta.size()) * sizeof(int32_t)));
+  if (!item_meta.empty())
+    HIPCHECK(c, hipMemcpy(c->d_item_meta, item_meta.data(), item_meta.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   for (fsdf::PosedModel* P : {&c->pm, &c->pm_alt}) {
     HIPCHECK(c, dalloc((char**)&P->verts_w, (size_t)V * 4 * tsz));
     HIPCHECK(c, dalloc((char**)&P->hscale_w, (size_t)K * tsz));
@@ -725,6 +738,7 @@ extern "C" int fsdf_set_surfaces(fsdf_ctx* c, const fsdf_surface* surfs, int32_t
   c->lm.vert_hull = c->d_vert_hull;
   c->lm.vert_off = c->d_vert_off;
   c->lm.face_rows = c->d_face_rows;
+  c->lm.item_meta = c->d_item_meta;
   c->lm.stage_bytes = stage_bytes;
   c->lm.planes64 = planes64;
   c->lm.S = S;

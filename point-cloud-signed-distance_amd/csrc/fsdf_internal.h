@@ -89,6 +89,9 @@ struct LocalModel {
   const int32_t* vert_hull = nullptr;
   const int32_t* vert_off = nullptr;
   const int32_t* face_rows = nullptr;  // [F][4]
+  // per pose item (faces, then vertices) [F+V][4]: surface | nf << 16, hull,
+  // face_off[hull], vert_off[hull] — one 16-B load instead of a chain of them
+  const int32_t* item_meta = nullptr;
   int stage_bytes = 0;                 // per-wave LDS stage, context precision (multiple of 16)
   int planes64 = 0;                    // f64: stage the fp64 planes too (FSDF_STAGE_PLANES64, if they fit)
   // hull-partitioned pass tiers (pass_kernel HPART, hpart_parts): clouds of

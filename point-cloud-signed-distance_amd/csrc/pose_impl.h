@@ -40,7 +40,8 @@ __device__ __forceinline__ void pose_item(const LocalModel& lm, const double* __
   if (tid >= fv_pad) tid -= fv_pad - fv;
   if (tid < lm.F) {
     const int f = tid;
-    const int k = lm.hull_surface[lm.face_hull[f]];
+    const I4 meta = ((const I4*)lm.item_meta)[f];
+    const int k = meta[0] & 0xffff;
     double P[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) P[i] = poses[12 * k + i];
@@ -55,13 +56,13 @@ __device__ __forceinline__ void pose_item(const LocalModel& lm, const double* __
     if (screen_w) {
       // fp32 screening copy, centred on the hull's f32 sphere centre c (the
       // same bits the sphere thread below stores): d' = d - n·c
-      const int h = lm.face_hull[f];
-      const int j = f - lm.face_off[h], nf = lm.face_off[h + 1] - lm.face_off[h];
+      const int h = meta[1], fo = meta[2];
+      const int j = f - fo, nf = meta[0] >> 16;
       double cw[3];
       xf_point(P, lm.sphere_l + 4 * h, cw);
       const double c0 = (double)(float)cw[0], c1 = (double)(float)cw[1], c2 = (double)(float)cw[2];
       const double dc = dw - __builtin_fma(nw[0], c0, __builtin_fma(nw[1], c1, nw[2] * c2));
-      float* pair = screen_w + 4 * (lm.face_off[h] + h + (j & ~1));
+      float* pair = screen_w + 4 * (fo + h + (j & ~1));
       // an exact duplicate of an earlier face's plane (face row word 3) is
       // screened out: h = -1e30, never a maximum nor a near-tie
       const bool dup = lm.face_rows[4 * f + 3] != 0;
@@ -73,7 +74,7 @@ __device__ __forceinline__ void pose_item(const LocalModel& lm, const double* __
 #pragma unroll
         for (int c = 0; c < 4; ++c) pair[2 * c + 1] = v[c];
       if (sizeof(T) == 8 && image_w) {  // the hull's stage image: same pair words, then the fp64 plane
-        I4* img = image_w + 4 * lm.face_off[h] + h + 2 * lm.vert_off[h];
+        I4* img = image_w + 4 * fo + h + 2 * meta[3];
         float* ip = (float*)(img + (j & ~1));
 #pragma unroll
         for (int c = 0; c < 4; ++c) ip[2 * c + (j & 1)] = v[c];
@@ -86,16 +87,15 @@ __device__ __forceinline__ void pose_item(const LocalModel& lm, const double* __
     }
   } else if (tid < lm.F + lm.V) {
     const int v = tid - lm.F;
-    const double* P = poses + 12 * lm.hull_surface[lm.vert_hull[v]];
+    const I4 meta = ((const I4*)lm.item_meta)[tid];
+    const double* P = poses + 12 * (meta[0] & 0xffff);
     double w[3];
     xf_point(P, lm.verts_l + 3 * v, w);
     T* o = verts_w + 4 * v;
     o[0] = (T)w[0]; o[1] = (T)w[1]; o[2] = (T)w[2]; o[3] = (T)0;
     if (sizeof(T) == 8 && image_w) {
-      const int h = lm.vert_hull[v];
-      const int nf = lm.face_off[h + 1] - lm.face_off[h];
-      double* q = (double*)(image_w + 4 * lm.face_off[h] + h + 2 * lm.vert_off[h] + 3 * nf + 1 +
-                            2 * (v - lm.vert_off[h]));
+      const int h = meta[1], nf = meta[0] >> 16;
+      double* q = (double*)(image_w + 4 * meta[2] + h + 2 * meta[3] + 3 * nf + 1 + 2 * (v - meta[3]));
       q[0] = w[0]; q[1] = w[1]; q[2] = w[2]; q[3] = 0.0;
     }
   } else if (tid < lm.F + lm.V + 64 * lm.K) {

@@ -1412,7 +1412,10 @@ __device__ __forceinline__ uint64_t emit_chunk(T px, T py, T pz, bool valid, T b
   }
 
   {
-    if (out.prior_out && valid) out.prior_out[i] = (uint8_t)bk;  // the next pass's seed hint (resident order)
+    // the next pass's seed hint (resident order), stored only where it changed
+    // (re-read here rather than carried from the seed load: a register live
+    // through scene_eval spills at the budget)
+    if (out.prior_out && valid && out.prior_out[i] != (uint8_t)bk) out.prior_out[i] = (uint8_t)bk;
     if (out.perm) {  // caller order: scattered through the sort permutation
       if (valid) {
         const int64_t o = out.perm[i];

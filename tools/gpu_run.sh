@@ -19,6 +19,7 @@
 #   abcheck:LIBS    bit-for-bit agreement of builds with the first (tools/ab_check.py)
 #   lds:LIBS        PMC pass of each build: LDS instructions / bank conflicts / waits
 #   pmc:NAME:CTRS   one PMC pass (commas between counters) of the product library
+#   pmclib:LIBS:CTRS  one PMC pass per library build (commas between libs, '+' between counters)
 #   sweep           bench.py at 2^16 .. 2^20 points           -> size_sweep.jsonl
 #   configs         tools/bench_configs.py (BASELINE configs C2-C5, M64)
 #   rehearse        bench.py N=2 on one GPU (gloo, both ranks on device 0)
@@ -124,6 +125,17 @@ for r in csv.DictReader(open(f)):
           --no-cpu-baseline --no-full-iteration > $GRAFT_REPO_ROOT/$O/pmc_$N.log 2>&1 ) \
         || { echo PMC FAILED; tail $O/pmc_$N.log; exit 1; }
       python tools/pmc_brief.py $O/pmc_$N/run_counter_collection.csv pass_kernel ;;
+    pmclib:*)
+      # pmclib:LIBS:C1,C2,... — one PMC pass per library build (FLASHSDF_LIB; commas between libs, '+' between counters)
+      R=${step#pmclib:}; L=${R%%:*}; C=${R#*:}; C=${C//+/ }
+      for lib in ${L//,/ }; do
+        N=$(basename $lib .so)
+        ( cd /tmp && export TMPDIR=/tmp FLASHSDF_LIB=$GRAFT_REPO_ROOT/$lib && timeout -s KILL 120 rocprofv3 --pmc $C \
+          --output-format csv -d $GRAFT_REPO_ROOT/$O/pmclib_$N -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 \
+          --warmup 3 --no-cpu-baseline --no-full-iteration --inflight 1 > $GRAFT_REPO_ROOT/$O/pmclib_$N.log 2>&1 ) \
+          || { echo PMCLIB FAILED; tail $O/pmclib_$N.log; exit 1; }
+        echo "$N $(python tools/pmc_brief.py $O/pmclib_$N/run_counter_collection.csv pass_kernel)"
+      done ;;
     sweep)
       # M64 pass/step against cloud size (one bench line per size)
       for n in 65536 131072 262144 524288 1048576; do

@@ -614,6 +614,37 @@ def test_regroup_points(m64, ctx_factory, n):
         unsorted.regroup_points()
 
 
+@pytest.mark.parametrize("n", [131077, 1 << 20])
+def test_regroup_follows_last_pass(m64, ctx_factory, n):
+    """The seed bytes a pass leaves behind (PassOutputs::prior_out) are that
+    pass's k* at every point, though a seeded pass stores a byte only where k*
+    changed: after passes at configurations far enough apart that many points
+    change surface, fsdf_regroup_points groups by the LAST pass's k*; and again
+    after more passes over the regrouped cloud."""
+    import flash
+    from flash import synthetic
+    qt, qe = synthetic.perturbed_configuration(m64, 931)
+    confs = [flash.hull_poses(m64, qe + d) for d in (0.0, 0.06, -0.05, 0.03)]
+    pts = synthetic.depth_cloud(m64, qt, n, seed=932, order="shuffled")
+    ctx = ctx_factory(m64, sort_points=True)
+    ctx.set_points(pts)
+    ctx.set_output_order(True)
+    for rounds in range(2):
+        ks = []
+        for p in confs[2 * rounds:2 * rounds + 2]:
+            _, _, (k, _, _) = ctx.eval(p, per_point=True)  # resident order
+            ks.append(k.copy())
+        changed = int(np.count_nonzero(ks[0] != ks[1]))
+        assert changed > n // 1000, changed  # the second pass rewrote many seed bytes
+        perm0 = ctx.permutation()
+        ctx.regroup_points()
+        perm1 = ctx.permutation()
+        pos0 = np.empty(perm0.max() + 1, np.int64)
+        pos0[perm0] = np.arange(len(perm0))
+        kg = ks[1][pos0[perm1]]  # the last pass's k*, in the regrouped order
+        assert np.all(np.diff(kg) >= 0)
+
+
 def test_cost_functor_regroup(irb):
     """CostFunctor.regroup(): after the frame's first evaluation, later ones
     give the same cost and gradient to rounding."""

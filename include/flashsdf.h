@@ -264,10 +264,12 @@ int fsdf_set_points(fsdf_ctx* ctx, const double* xyz, int64_t n);
 int fsdf_set_points_device(fsdf_ctx* ctx, const double* d_xyz, int64_t n);
 /* The next frame's cloud ahead of time (a frame loop over recorded or queued
  * clouds, src/gradientdescent.jl:43 once per frame): fsdf_prefetch_points
- * starts its host-to-device copy on a stream of the context's own and returns
- * at once, so the copy runs during the current frame's passes (overlapped from
- * page-locked memory; the caller keeps xyz unchanged until the next call
- * below returns; a second prefetch replaces a pending one);
+ * queues its host-to-device copy on a stream of the context's own and returns
+ * at once; the copy is issued right after the context's next pass is launched
+ * (or by fsdf_set_points_prefetched when no pass comes between), so it runs
+ * during the current frame's passes (overlapped from page-locked memory; the
+ * caller keeps xyz unchanged until the next call below returns; a second
+ * prefetch replaces a pending one);
  * fsdf_set_points_prefetched then makes it resident as fsdf_set_points would
  * (FSDF_ERR_STATE when nothing is pending). A sorting context also Hilbert-
  * sorts the prefetched cloud on that stream, into a second resident buffer set,

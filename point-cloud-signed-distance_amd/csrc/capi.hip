@@ -137,6 +137,12 @@ struct fsdf_ctx {
   // the next frame's cloud, copied ahead on a stream of its own (fsdf_prefetch_points)
   double* d_prefetch = nullptr;
   int64_t prefetch_cap = 0, prefetch_n = -1;  // -1: none pending
+  // a prefetch is queued on the next pass's launch (its host-side work then
+  // overlaps that pass instead of delaying the frame's first launch): the
+  // caller's cloud, whether it is still to be issued, and the issue's result
+  const double* prefetch_src = nullptr;
+  bool prefetch_deferred = false;
+  int prefetch_rc = 0;
   // ... and its resident form, sorted there too (swapped in by fsdf_set_points_prefetched)
   bool prefetch_sorted = false;
   void* d_pts_next = nullptr;
@@ -1091,10 +1097,14 @@ extern "C" int fsdf_set_points_device(fsdf_ctx* c, const double* d_xyz, int64_t 
 // the per-frame ingest loses its host-link transfer (25 MB at 2^20 points).
 // The copy overlaps only from page-locked host memory; the caller keeps xyz
 // unchanged until fsdf_set_points_prefetched returns. A second prefetch
-// replaces a pending one.
-extern "C" int fsdf_prefetch_points(fsdf_ctx* c, const double* xyz, int64_t n) {
-  if (!c) return FSDF_ERR_ARG;
-  if (n < 0 || (n > 0 && !xyz)) return fail(c, FSDF_ERR_ARG, "prefetch_points: bad buffer (n=%lld)", (long long)n);
+// replaces a pending one. fsdf_prefetch_points only records the cloud;
+// prefetch_issue enqueues the copy and sort on the copy stream, from the next
+// pass's launch (run_pass) or from fsdf_set_points_prefetched when no pass
+// came between.
+static int prefetch_issue(fsdf_ctx* c) {
+  c->prefetch_deferred = false;
+  const double* xyz = c->prefetch_src;
+  const int64_t n = c->prefetch_n;
   HIPCHECK(c, hipSetDevice(c->device));
   // (an earlier prefetch's copy may still write the buffer; a consumed one's
   // sort has finished: fsdf_set_points_prefetched returns after it)
@@ -1140,7 +1150,16 @@ extern "C" int fsdf_prefetch_points(fsdf_ctx* c, const double* xyz, int64_t n) {
     c->prefetch_sorted = true;
   }
   HIPCHECK(c, hipEventRecord(c->ev_prefetch, c->copy_stream));
+  return FSDF_OK;
+}
+
+extern "C" int fsdf_prefetch_points(fsdf_ctx* c, const double* xyz, int64_t n) {
+  if (!c) return FSDF_ERR_ARG;
+  if (n < 0 || (n > 0 && !xyz)) return fail(c, FSDF_ERR_ARG, "prefetch_points: bad buffer (n=%lld)", (long long)n);
+  c->prefetch_src = xyz;
   c->prefetch_n = n;
+  c->prefetch_deferred = true;
+  c->prefetch_rc = FSDF_OK;
   return FSDF_OK;
 }
 
@@ -1148,14 +1167,17 @@ extern "C" int fsdf_set_points_prefetched(fsdf_ctx* c) {
   if (!c) return FSDF_ERR_ARG;
   if (c->prefetch_n < 0) return fail(c, FSDF_ERR_STATE, "set_points_prefetched: no prefetch pending");
   const int64_t n = c->prefetch_n;
+  int rc = c->prefetch_deferred ? prefetch_issue(c) : c->prefetch_rc;
   c->prefetch_n = -1;
+  c->prefetch_rc = FSDF_OK;
+  if (rc) return rc;
   HIPCHECK(c, hipSetDevice(c->device));
   HIPCHECK(c, hipStreamWaitEvent(c->stream, c->ev_prefetch, 0));  // (the copy, and the sort when done there)
   if (!c->prefetch_sorted) return set_points_impl(c, c->d_prefetch, n, true, 0, n);
   // the sorted next cloud becomes resident: the current frame's work is done
   // (synchronised), its buffers become the next prefetch's
   HIPCHECK(c, hipStreamSynchronize(c->stream));
-  int rc = ensure_vox_box(c, c->d_prefetch, n);  // (a first cloud: the seed box)
+  rc = ensure_vox_box(c, c->d_prefetch, n);  // (a first cloud: the seed box)
   if (rc) return rc;
   rc = carry_seeds_out(c);  // (the previous cloud, still resident)
   if (rc) return rc;
@@ -1418,9 +1440,9 @@ static int run_planned(fsdf_ctx* c, const fsdf::PosedModel& P, const void* d_pts
 // workgroups heaviest-first by the previous pass's durations
 // posed / skip: the device solver loop's pass — its model posed by the
 // previous step (pose_model), its done flag
-static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t n, double* d_accum,
-                    int32_t* d_kstar, double* d_d, double* d_grad, const int32_t* d_perm, bool schedule,
-                    bool posed = false, const int* skip = nullptr) {
+static int run_pass_impl(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t n, double* d_accum,
+                         int32_t* d_kstar, double* d_d, double* d_grad, const int32_t* d_perm, bool schedule,
+                         bool posed, const int* skip) {
   if (c->lm.R > 0 && !c->rbf_ready)
     return fail(c, FSDF_ERR_STATE, "eval: the scene has RBF surfaces: call fsdf_set_rbf_params first");
   fsdf::PosedModel* P = nullptr;
@@ -1502,6 +1524,18 @@ static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t
     HIPCHECK(c, hipMemsetAsync(d_accum, 0, (size_t)accum_len(c) * sizeof(double), c->stream));
   }
   return FSDF_OK;
+}
+
+// A pass, then a prefetch still to be issued (fsdf_prefetch_points): its copy,
+// sort launches and their host-side cost go behind this pass, which the device
+// is already running (profiles/r06/prefetch_defer/). Its result waits for
+// fsdf_set_points_prefetched.
+static int run_pass(fsdf_ctx* c, const double* poses, const void* d_pts, int64_t n, double* d_accum,
+                    int32_t* d_kstar, double* d_d, double* d_grad, const int32_t* d_perm, bool schedule,
+                    bool posed = false, const int* skip = nullptr) {
+  const int rc = run_pass_impl(c, poses, d_pts, n, d_accum, d_kstar, d_d, d_grad, d_perm, schedule, posed, skip);
+  if (!rc && c->prefetch_deferred) c->prefetch_rc = prefetch_issue(c);
+  return rc;
 }
 
 // per-point outputs of resident-cloud passes: scattered to caller order through

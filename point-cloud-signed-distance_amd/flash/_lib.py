@@ -249,9 +249,10 @@ class Context:
         self.n = n
 
     def prefetch_points(self, xyz: np.ndarray):
-        """Start the next frame's upload (fsdf_prefetch_points: a copy on the
-        context's own stream, overlapping the current frame's passes when `xyz`
-        is page-locked); set_points_prefetched() makes it resident. The array is
+        """Queue the next frame's upload (fsdf_prefetch_points: a copy and sort
+        on the context's own stream, issued right after the next pass is
+        launched, overlapping the current frame's passes when `xyz` is
+        page-locked); set_points_prefetched() makes it resident. The array is
         held until then (the copy reads it)."""
         pts = np.ascontiguousarray(xyz, np.float64).reshape(-1, 3)
         check(self._lib.fsdf_prefetch_points(self._ctx, ptr(pts), pts.shape[0]), self._ctx, "prefetch_points")

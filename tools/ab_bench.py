@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A/B timing of pass-kernel builds (GPU box): runs bench.py once per library
 (FLASHSDF_LIB override, see csrc/Makefile `make dev`), interleaved over
-rounds, and prints the pass-kernel mean (HIP events) per build.
+rounds, and prints the pass-kernel mean (HIP events), the step and the measured
+prefetched frame (bench measured_frame, unless --no-full-iteration) per build.
 
     python tools/ab_bench.py ab/libA.so ab/libB.so [--rounds 3] [-- bench args]
 """
@@ -37,12 +38,16 @@ def main():
                 print(f"{lib}: FAILED rc={p.returncode}\n{p.stderr[-2000:]}", flush=True)
                 return 1
             j = json.loads(line[-1])
-            res[lib].append((j["roofline"]["kernel_ms"], j["ms_per_step"]))
+            mf = (j.get("measured_frame") or j["config"].get("measured_frame") or {}).get("device_loop_prefetched", {})
+            res[lib].append((j["roofline"]["kernel_ms"], j["ms_per_step"], mf.get("frame_ms", float("nan")),
+                             mf.get("set_points_ms", float("nan"))))
             print(f"round {r} {os.path.basename(lib)}: pass {j['roofline']['kernel_ms']:.4f} ms, "
-                  f"step {j['ms_per_step']:.4f} ms", flush=True)
+                  f"step {j['ms_per_step']:.4f} ms, prefetched frame {res[lib][-1][2]:.4f} ms "
+                  f"(ingest {res[lib][-1][3]:.4f})", flush=True)
     print("summary (min over rounds):")
     for lib, v in res.items():
-        print(f"  {os.path.basename(lib):32s} pass {min(x[0] for x in v):.4f} ms  step {min(x[1] for x in v):.4f} ms")
+        print(f"  {os.path.basename(lib):32s} pass {min(x[0] for x in v):.4f} ms  step {min(x[1] for x in v):.4f} ms  "
+              f"frame {min(x[2] for x in v):.4f} ms  ingest {min(x[3] for x in v):.4f} ms")
     return 0
 
 
